@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""Benchmark: pod placements/sec of the MI355X batched-ensemble engine on 4k-node clusters.
+
+Workload (BASELINE.json configs[2] shape, the metric's "4k-node clusters"): C3 — every GPU runs
+R replicas (default 8,192) of a 4,096-node Alibaba-like cluster, each replica a seed-perturbed copy
+of one synthetic 16,384-pod Alibaba-like trace (integer arrival seconds); a step simulates every
+replica from initialize() until RunUntilAllPodsAreFinished stops it.  Replicas are sharded over
+ranks with distinct seeds (weak scaling: R per GPU); the only collective is one RCCL all-reduce of
+the counter vector per measurement (the reference has no data-path exchange).
+
+Prints ONE JSON line (rank 0).  `value` = placements of all ranks / max-over-ranks wall time of
+the timed steps.  `roofline`: the dominant kernel is k10s_run_kernel (the whole event loop incl. the
+scheduling scans); algorithmic bytes per launch = Σ_attempts (12·|node cache| + 12) + 12·placements
+(SURVEY.md §8(d)), divided by the launch's HIP-event time, against the 8 TB/s HBM3E peak.
+`cpu_baseline`: the repo's CPU oracle (a string-keyed restatement of the reference, kind "port";
+the Rust reference cannot be built here) on a bounded sample of the same workload, one process
+per core.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK = 8.0e12  # MI355X HBM3E peak, MI355X_MICROARCH.md "Chip-level parameters"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--replicas", type=int, default=8192, help="replicas per GPU")
+    ap.add_argument("--nodes", type=int, default=4096)
+    ap.add_argument("--pods", type=int, default=16384)
+    ap.add_argument("--arrival-window", type=float, default=1200.0)
+    ap.add_argument("--budget", type=int, default=0, help="max events per replica per launch (0 = one launch)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-workers", type=int, default=0, help="0 = min(16, cores)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_worker(args_tuple):
+    """One core: the oracle on one replica's materialized trace for ~`seconds` of wall time."""
+    scn, seconds = args_tuple
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_bridge as ob
+    o = ob.OracleSim(scn)
+    t0 = time.perf_counter()
+    t_sim = 0.0
+    while time.perf_counter() - t0 < seconds:
+        t_sim += 20.0
+        o.step_until_time(t_sim)
+        r = o.result()
+        if r["panicked"] or t_sim > 1e6:
+            break
+        if r["counters"]["terminated_pods"] >= r["counters"]["total_pods_in_trace"]:
+            break
+    wall = time.perf_counter() - t0
+    c = o.result()["counters"]
+    return c["placements"], c["attempts"], c["events"], wall, t_sim
+
+
+def cpu_baseline(args, cfg, cluster, workload, params):
+    from multiprocessing import get_context
+    from kubernetriks_amd import workloads as wl
+    from kubernetriks_amd.scenario import scenario_text
+    workers = args.cpu_workers or min(16, os.cpu_count() or 1)
+    jobs = [(scenario_text(cfg, cluster, wl.perturb_workload(workload, params[i].seed)), args.cpu_seconds)
+            for i in range(workers)]
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_bridge as ob
+    ob.build_oracle()
+    with get_context("fork").Pool(workers) as pool:
+        res = pool.map(cpu_worker, jobs)
+    rate = sum(p / w for p, _, _, w, _ in res)
+    sample = (f"{workers} processes x 1 replica of the same C3 workload ({args.nodes} nodes, {args.pods} pods, "
+              f"seed-perturbed), each run ~{args.cpu_seconds:.0f}s of wall time from t=0; "
+              f"{sum(r[0] for r in res)} placements, {sum(r[2] for r in res)} events in total")
+    return {"value": rate, "unit": "placements/s", "cores": workers, "kind": "port", "sample": sample,
+            "per_core_placements_per_s": rate / workers}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    torch.cuda.set_device(local_rank)
+
+    from kubernetriks_amd.build import build
+    build()
+    from kubernetriks_amd import workloads as wl
+    from kubernetriks_amd.native import Engine
+    from kubernetriks_amd.scenario import SimulationConfig, scenario_text
+
+    cfg = SimulationConfig()
+    cluster, workload = wl.c3_traces(args.nodes, args.pods, args.arrival_window)
+    scn = scenario_text(cfg, cluster, workload)
+    R = args.replicas
+    probe = Engine(scn, 1, device=local_rank)
+    defaults = probe.default_params()
+    probe.close()
+    params = wl.replica_params(defaults, R, base_seed=123, perturb=True, replica_offset=rank * R)
+    t = time.perf_counter()
+    eng = Engine(scn, R, params=params, device=local_rank)
+    log(f"[rank {rank}] engine: {R} replicas x {eng.replica_bytes / 2**20:.1f} MiB, init {time.perf_counter() - t:.2f}s")
+
+    def one_step():
+        eng.reset()
+        return eng.run_until_all_finished(max_time=1e7, max_events_per_launch=args.budget)
+
+    for i in range(args.warmup):
+        t = time.perf_counter()
+        one_step()
+        log(f"[rank {rank}] warmup {i}: {time.perf_counter() - t:.2f}s")
+
+    import numpy as np
+    counters = np.zeros(16, dtype=np.float64)
+    kernel_ms = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ms = one_step()
+        kernel_ms.append(ms)
+        res = eng.raw_results()
+        for r in res:
+            for k in range(16):
+                counters[k] += r.counters[k]
+        log(f"[rank {rank}] step {i}: run {ms:.1f} ms")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    statuses = {}
+    for r in eng.raw_results():
+        statuses[r.status] = statuses.get(r.status, 0) + 1
+    if statuses.get(2):
+        log(f"[rank {rank}] WARNING: {statuses[2]} replicas ended in error")
+
+    tvec = torch.tensor([elapsed, sum(kernel_ms) / len(kernel_ms)], dtype=torch.float64, device="cuda")
+    cvec = torch.tensor(counters, dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tvec, op=dist.ReduceOp.MAX)
+        dist.all_reduce(cvec, op=dist.ReduceOp.SUM)  # RCCL over xGMI: metric counters only
+    elapsed, mean_kernel_ms = float(tvec[0]), float(tvec[1])
+    c = cvec.cpu().numpy()
+    placements, attempts, events, scanned = c[12], c[13], c[14], c[15]
+    value = placements / elapsed
+
+    # roofline for the dominant kernel (per launch, this rank's launch time, all-rank bytes / world)
+    per_launch_bytes = (12.0 * scanned + 12.0 * attempts + 12.0 * placements) / (args.steps * world)
+    achieved = per_launch_bytes / (mean_kernel_ms * 1e-3)
+    traffic = None
+    pmc_path = os.path.join(REPO, "profiles", "pmc_run_kernel.json")
+    if os.path.exists(pmc_path):
+        try:
+            pm = json.load(open(pmc_path))
+            if pm.get("config") == [R, args.nodes, args.pods]:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": "pod placements/sec (whole node, 1/2/4/8 GPUs) at 4k-node clusters; % HBM roofline",
+        "value": value,
+        "unit": "placements/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: Alibaba-like 4096-node clusters and 16384-pod traces (notebook statistics), seed-perturbed per replica",
+        "config": {"workload": f"C3: {R} replicas/GPU x {args.nodes}-node Alibaba-like cluster, {args.pods} pods/replica, "
+                               "run until all pods finished (RunUntilAllPodsAreFinished)",
+                   "replicas_per_gpu": R, "total_replicas": R * world, "nodes": args.nodes, "pods_per_replica": args.pods,
+                   "parallelism": f"replica-sharded x{world} (RCCL all-reduce of counters only)"},
+        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK, "traffic": traffic,
+                     "kernel": "k10s_run_kernel", "kernel_ms_per_launch": mean_kernel_ms,
+                     "algorithmic_bytes_per_launch": per_launch_bytes},
+        "totals": {"placements": placements, "attempts": attempts, "events": events, "nodes_scanned": scanned,
+                   "replica_status": {str(k): v for k, v in statuses.items()}},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(args, cfg, cluster, workload, params)
+        except Exception as ex:  # the GPU number stands on its own
+            log("cpu baseline failed:", ex)
+            out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

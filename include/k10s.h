@@ -1,0 +1,244 @@
+/*
+ * k10s.h — C ABI of the MI355X batched-ensemble engine for kubernetriks' scheduling hot path.
+ *
+ * Plain C (bindgen-friendly): explicit-width integers, POD structs, caller-owned host buffers,
+ * engine-owned device memory behind an opaque handle.  No torch types, no HIP types.  The Rust
+ * binding a maintainer would add is in INTEGRATION.md.
+ *
+ * Two surfaces, mirroring the reference's drop-in boundary:
+ *
+ *  (1) k10s_schedule_one_batch — replaces, for R independent problems at once,
+ *        trait PodSchedulingAlgorithm { fn schedule_one(&self, pod: &Pod,
+ *            nodes: &BTreeMap<String, Node>) -> Result<String, ScheduleError>; }
+ *      src/core/scheduler/interface.rs:14-23, implemented by KubeScheduler::schedule_one
+ *      (src/core/scheduler/kube_scheduler.rs:68-151) with Fit + LeastAllocatedResources
+ *      (src/core/scheduler/plugin.rs:34-63).  Nodes are passed in name order (BTreeMap order);
+ *      the result is the chosen node's index in that order instead of its String name.
+ *
+ *  (2) k10s_engine_* — replaces the per-replica event loop that drives it:
+ *        KubernetriksSimulation::{new, initialize, run_with_callbacks, step_until_time,
+ *        step_for_duration}   src/simulator.rs:68-275, 355-401
+ *        RunUntilAllPodsAreFinishedCallbacks::on_step   src/simulation_callbacks.rs:86-91
+ *      for thousands of independent replicas per GPU (one wavefront per replica).
+ *
+ * Errors: every function returns K10S_OK (0) or a negative K10S_E_* code; a reference
+ * `panic!` inside one replica is not an ABI error — it stops that replica and is reported in
+ * k10s_replica_result.error_code (K10S_PANIC_*), like the reference process would abort.
+ * Threading: one handle per device; a handle is not thread-safe.
+ */
+#ifndef K10S_H
+#define K10S_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- schedule_one status (ScheduleError, interface.rs:7-11) ------------------------------ */
+#define K10S_SCHED_OK 0
+#define K10S_SCHED_NO_NODES_IN_CLUSTER 1
+#define K10S_SCHED_NO_SUFFICIENT_RESOURCES 2
+#define K10S_SCHED_REQUESTED_RESOURCES_ARE_ZEROS 3
+
+/* ---- ABI error codes -------------------------------------------------------------------- */
+#define K10S_OK 0
+#define K10S_E_INVALID (-1)       /* bad argument / malformed scenario (message via k10s_last_error) */
+#define K10S_E_NO_DEVICE (-2)     /* no HIP device: the engine never falls back to the CPU */
+#define K10S_E_HIP (-3)           /* HIP runtime error */
+#define K10S_E_CAPACITY (-4)      /* requested capacities do not fit device memory */
+#define K10S_E_STATE (-5)         /* call not valid in the handle's current state */
+
+/* ---- per-replica status ------------------------------------------------------------------ */
+#define K10S_REPLICA_RUNNING 0    /* paused (event budget or until-time reached) */
+#define K10S_REPLICA_FINISHED 1   /* all trace pods terminated at a clock multiple of 1000 */
+#define K10S_REPLICA_ERROR 2      /* reference panic or engine capacity overflow: see error_code */
+#define K10S_REPLICA_TIME_LIMIT 3 /* next event beyond the run's max_time guard */
+
+/* ---- per-replica error codes (reference panic sites) ------------------------- */
+#define K10S_PANIC_NONE 0
+#define K10S_PANIC_POOL_EXHAUSTED 1        /* node_component_pool.rs:56-59 */
+#define K10S_PANIC_DUPLICATE_NODE 2        /* api_server.rs:73-78, persistent_storage.rs:76-81 */
+#define K10S_PANIC_DUPLICATE_POD 3         /* persistent_storage.rs:89-94 */
+#define K10S_PANIC_MISSING_POD 4           /* any pods.get(...).unwrap() on an absent pod */
+#define K10S_PANIC_MISSING_NODE 5          /* any nodes/created_nodes.get(...).unwrap() on an absent node */
+#define K10S_PANIC_BIND_REMOVED_NODE 6     /* node_component.rs:190-202 */
+#define K10S_PANIC_MISSING_ASSIGNMENTS 7   /* scheduler assignments.get_mut(node).unwrap() */
+#define K10S_PANIC_USAGE_MODEL 8           /* resource usage model construction/poll panics */
+#define K10S_PANIC_HPA_UNREGISTERED 9      /* horizontal_pod_autoscaler.rs:214 */
+#define K10S_PANIC_CA_GROUP 10             /* kube_cluster_autoscaler.rs:297-299 */
+#define K10S_PANIC_GROUP_DURATION 11       /* api_server.rs:406-409 */
+#define K10S_PANIC_MISSING_PENDING 12      /* api_server.rs:98-101 */
+#define K10S_PANIC_REMOVE_OTHER_NODE 13    /* node_component.rs:248-254 */
+#define K10S_PANIC_UNKNOWN_PROFILE 14      /* kube_scheduler.rs:95 */
+#define K10S_ERR_HEAP_FULL 100             /* engine capacity: event heap */
+#define K10S_ERR_QUEUE_FULL 101            /* engine capacity: scheduler queues */
+#define K10S_ERR_NAME_BOUND 102            /* engine capacity: generated-name universe bound */
+#define K10S_ERR_SEQ_OVERFLOW 103          /* engine capacity: 2^32 event ids in one replica */
+#define K10S_ERR_CA_BUFFER 104             /* engine capacity: CA action buffer */
+
+/* ---- counters (printer.rs:90-101 + engine throughput counters) ---------------------------- */
+enum k10s_counter {
+    K10S_C_TOTAL_NODES_IN_TRACE = 0,
+    K10S_C_TOTAL_PODS_IN_TRACE,
+    K10S_C_PODS_SUCCEEDED,
+    K10S_C_PODS_UNSCHEDULABLE,
+    K10S_C_PODS_FAILED,
+    K10S_C_PODS_REMOVED,
+    K10S_C_TOTAL_SCALED_UP_NODES,
+    K10S_C_TOTAL_SCALED_DOWN_NODES,
+    K10S_C_TOTAL_SCALED_UP_PODS,
+    K10S_C_TOTAL_SCALED_DOWN_PODS,
+    K10S_C_PROCESSED_NODES,  /* InternalMetrics.processed_nodes (collector.rs:80) */
+    K10S_C_TERMINATED_PODS,  /* InternalMetrics.terminated_pods (collector.rs:84) */
+    K10S_C_PLACEMENTS,       /* successful schedule_one calls (scheduler.rs:309-320) */
+    K10S_C_ATTEMPTS,         /* schedule_one calls reaching the filter (kube_scheduler.rs:89) */
+    K10S_C_EVENTS,           /* delivered (non-canceled) events */
+    K10S_C_NODES_SCANNED,    /* Σ |scheduler cache| over attempts: algorithmic scan volume */
+    K10S_NUM_COUNTERS
+};
+
+/* `average` 0.15 Min/Max/Mean/Variance estimator state (collector.rs:15-74) */
+typedef struct k10s_estimator {
+    uint64_t n;
+    double min, max, mean, sum2; /* population variance = sum2 / n */
+} k10s_estimator;
+
+#define K10S_EST_POD_DURATION 0
+#define K10S_EST_POD_SCHEDULE_TIME 1
+#define K10S_EST_POD_QUEUE_TIME 2
+
+typedef struct k10s_replica_result {
+    uint32_t status;        /* K10S_REPLICA_* */
+    uint32_t error_code;    /* K10S_PANIC_* / K10S_ERR_* */
+    uint32_t error_kind;    /* event kind (k10s_events.h) being handled at the error */
+    uint32_t error_seq;     /* id of that event */
+    double error_time;
+    double clock;           /* simulation time of the last delivered event (dslab time()) */
+    uint64_t counters[K10S_NUM_COUNTERS];
+    k10s_estimator est[3];
+    uint32_t unschedulable_len;  /* scheduler unschedulable_pods.len() (stale entries included) */
+    uint32_t active_len;         /* scheduler action_queue.len() */
+    uint32_t node_count_as, node_count_ps, node_count_s;
+    uint32_t log_len, placements_len, flags;  /* flags bit0: event log overflow, bit1: placement log overflow */
+} k10s_replica_result;
+
+/* Per-replica parameters (scheduler-parameter sweeps, seed-perturbed traces).  Fields mirror
+   SimulationConfig (config.rs:13-37) and the CA/HPA algorithm configs; k10s_default_params fills
+   them from the scenario. */
+typedef struct k10s_replica_params {
+    double scheduling_cycle_interval;
+    double as_to_ps_network_delay, ps_to_sched_network_delay, sched_to_as_network_delay;
+    double as_to_node_network_delay, as_to_ca_network_delay, as_to_hpa_network_delay;
+    double ca_scan_interval, ca_scale_down_utilization_threshold;
+    double hpa_scan_interval, hpa_target_threshold_tolerance;
+    double score_weight;                 /* LeastAllocatedResources weight (kube_scheduler.rs:55) */
+    uint32_t enable_unscheduled_pods_conditional_move;
+    uint32_t perturb;                    /* 0: trace as given; 1: seed-perturbed durations/requests */
+    uint64_t seed;
+    uint64_t ca_max_node_count;          /* read-only here (fixed by the scenario's node pool) */
+} k10s_replica_params;
+
+/* Capacities of per-replica engine structures (0 = derive from the scenario). */
+typedef struct k10s_capacities {
+    uint32_t event_heap, active_queue, unschedulable, group_name_bound, ca_name_bound;
+    uint32_t event_log, placement_log;   /* parity mode logs; 0 = off */
+    uint32_t pod_records;                /* 1 = keep per-pod start/finish/removal times */
+} k10s_capacities;
+
+/* Parity event-log entry: one delivered event (time, id order). */
+typedef struct k10s_log_entry {
+    double time;
+    uint32_t seq;
+    uint16_t kind;   /* k10s_event_kind */
+    int16_t slot;    /* node component (pool slot) for N_* kinds, else -1 */
+    int32_t pod;     /* pod index (name order) or -1 */
+    int32_t node;    /* node index (name order) or -1 */
+} k10s_log_entry;
+
+typedef struct k10s_placement {
+    double assign_time;
+    int32_t pod, node;
+} k10s_placement;
+
+typedef struct k10s_pod_record {
+    double t_running, t_finished, t_removed;  /* NaN when absent */
+    uint32_t state;                           /* 0 none, 1 in storage, 2 succeeded, 3 removed */
+    uint32_t pad;
+} k10s_pod_record;
+
+/* (1) --------------------------------------------------------------------------------------
+ * R independent schedule_one calls.  All pointers are DEVICE pointers.  Problem r sees nodes
+ * [r*node_stride, r*node_stride + n_nodes) in name order; present_bits marks which of them are in
+ * the scheduler cache (bit i of word (r*node_stride + i)/64 — node_stride must be a multiple
+ * of 64).  Writes out_node[r] (index within the problem, -1 on error) and out_status[r].
+ * stream: a hipStream_t or NULL.  Returns K10S_OK or a negative K10S_E_* code. */
+int32_t k10s_schedule_one_batch(const uint32_t* alloc_cpu, const uint64_t* alloc_ram,
+                                const uint64_t* present_bits, uint32_t n_nodes, uint32_t node_stride,
+                                const uint32_t* req_cpu, const uint64_t* req_ram, double weight,
+                                uint32_t n_problems, int32_t* out_node, int32_t* out_status,
+                                void* stream);
+
+/* (2) -------------------------------------------------------------------------------------- */
+typedef struct k10s_engine k10s_engine;
+
+/* Compile a scenario (DESIGN.md §Scenario format) into device tables and allocate n_replicas
+ * replicas on `device`.  params may be NULL (defaults; replica r gets seed = scenario seed + r
+ * and perturb = 0).  caps may be NULL.  Returns NULL on failure (k10s_last_error). */
+k10s_engine* k10s_engine_create(const char* scenario_text, const k10s_replica_params* params,
+                                uint32_t n_replicas, const k10s_capacities* caps, int32_t device);
+void k10s_engine_destroy(k10s_engine* e);
+
+/* Scenario-derived defaults for replica parameters. */
+int32_t k10s_engine_default_params(const k10s_engine* e, k10s_replica_params* out);
+
+/* Reset every replica to the initialized state (KubernetriksSimulation::initialize). */
+int32_t k10s_engine_reset(k10s_engine* e);
+
+#define K10S_RUN_UNTIL_ALL_FINISHED 0   /* run_with_callbacks(RunUntilAllPodsAreFinished) */
+#define K10S_RUN_UNTIL_TIME 1           /* step_until_time(until_time) */
+
+/* Advance every replica.  Each launch processes at most max_events_per_launch delivered events
+ * per replica (0 = unbounded) and the call loops launches until no replica is RUNNING-with-work.
+ * max_time guards runaway runs in mode 0 (replica -> TIME_LIMIT).  Blocks until done.
+ * If elapsed_ms is not NULL it receives the device time of the run (HIP events). */
+int32_t k10s_engine_run(k10s_engine* e, int32_t mode, double until_time, double max_time,
+                        uint64_t max_events_per_launch, double* elapsed_ms);
+
+/* Launch one bounded pass (no host loop, no sync) on the engine stream; *active receives, after
+ * completion, the number of replicas that still have work.  For benches/profilers. */
+int32_t k10s_engine_step_async(k10s_engine* e, int32_t mode, double until_time, double max_time,
+                               uint64_t max_events_per_launch);
+int32_t k10s_engine_sync(k10s_engine* e);
+
+int32_t k10s_engine_results(const k10s_engine* e, k10s_replica_result* out /* [n_replicas] */);
+int32_t k10s_engine_event_log(const k10s_engine* e, uint32_t replica, k10s_log_entry* out, uint32_t cap,
+                              uint32_t* n);
+int32_t k10s_engine_placements(const k10s_engine* e, uint32_t replica, k10s_placement* out, uint32_t cap,
+                               uint32_t* n);
+int32_t k10s_engine_pod_records(const k10s_engine* e, uint32_t replica, k10s_pod_record* out, uint32_t cap,
+                                uint32_t* n);
+/* HPA pod-group state: created_pods.len() and total_created per group (name order). */
+int32_t k10s_engine_group_sizes(const k10s_engine* e, uint32_t replica, uint32_t* created, uint32_t* total,
+                                uint32_t cap, uint32_t* n);
+
+/* Name tables of the compiled scenario (index -> name), for mapping logs back to names. */
+uint32_t k10s_engine_num_nodes(const k10s_engine* e);
+uint32_t k10s_engine_num_pods(const k10s_engine* e);
+uint32_t k10s_engine_num_groups(const k10s_engine* e);
+const char* k10s_engine_node_name(const k10s_engine* e, uint32_t idx);
+const char* k10s_engine_pod_name(const k10s_engine* e, uint32_t idx);
+const char* k10s_engine_group_name(const k10s_engine* e, uint32_t idx);
+
+/* Per-replica device-state footprint in bytes and device pointer of replica r's scheduler
+   cache SoA (for profiling tools). */
+uint64_t k10s_engine_replica_bytes(const k10s_engine* e);
+
+const char* k10s_last_error(void);
+const char* k10s_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* K10S_H */

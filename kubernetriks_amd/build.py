@@ -1,0 +1,63 @@
+"""Build the in-tree HIP engine library (build/libk10s.so) for gfx950.
+
+hipcc cross-compiles without a GPU, so this runs in the CPU container as the "does it build"
+check and produces the .so that travels to the GPU box.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(REPO, "kubernetriks_amd", "csrc")
+OUT = os.path.join(REPO, "build", "libk10s.so")
+SOURCES = ["k10s_kernels.hip", "k10s_host.cpp", "k10s_builder.cpp"]
+HEADERS = ["k10s_common.h", "k10s_state.h", "k10s_engine.h", "k10s_builder.h", "k10s_results.h"]
+ARCH = os.environ.get("K10S_OFFLOAD_ARCH", "gfx950")
+
+# -ffp-contract=off and no fast-math: score/time arithmetic must round exactly like the Rust
+# reference (no FMA contraction; correctly rounded f64 division).
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
+         f"--offload-arch={ARCH}"]
+
+
+def hipcc() -> str:
+    return shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+
+
+def _stale() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + \
+        [os.path.join(REPO, "include", f) for f in ("k10s.h", "k10s_events.h")]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False, extra=()) -> str:
+    if not force and not _stale():
+        return OUT
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    objs = []
+    procs = []
+    for src in SOURCES:
+        obj = os.path.join(REPO, "build", src + ".o")
+        cmd = [hipcc(), *FLAGS, *extra, "-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    for p in procs:
+        if p.wait() != 0:
+            raise RuntimeError("hipcc failed")
+    link = [hipcc(), *FLAGS, "-shared", *objs, "-o", OUT]
+    if verbose:
+        print(" ".join(link), file=sys.stderr)
+    subprocess.check_call(link)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,1508 @@
+// k10s_engine.h — one replica of kubernetriks' scheduling hot path + its event loop.
+//
+// Written once for the MI355X wavefront (64 lanes, wave-uniform control flow, lane-parallel node
+// scans) and, with K10S_LANES == 1, for the host-side check build used only by tests.
+//
+// Reference semantics restated here (file:line of jellythefish/kubernetriks):
+//   event queue        dslab-core (time, id) order, lazy cancel           SURVEY A.1
+//   scheduling cycle   Scheduler::run_scheduling_cycle                     scheduler.rs:246-334
+//   schedule_one       KubeScheduler::schedule_one + Fit + LeastAllocated  kube_scheduler.rs:68-151, plugin.rs:34-63
+//   active queue       Rust BinaryHeap<QueuedPodInfo> sift order            queue.rs:29-33, SURVEY A.2
+//   unschedulable map  BTreeMap<(ts total_cmp, name)>                       queue.rs:49-75
+//   handlers           api_server.rs:127-457, persistent_storage.rs:185-490, scheduler.rs:382-477,
+//                      node_component.rs:178-335, cluster_autoscaler.rs:230-334,
+//                      kube_cluster_autoscaler.rs:62-326, horizontal_pod_autoscaler.rs:146-257,
+//                      kube_horizontal_pod_autoscaler.rs:54-216, collector.rs:263-337,410-431
+//   termination        RunUntilAllPodsAreFinishedCallbacks::on_step          simulation_callbacks.rs:86-91
+#pragma once
+
+#include "k10s_state.h"
+
+namespace k10s {
+
+struct Ctx {
+    const Scenario* sc;
+    const Params* pr;
+    Rep v;
+    const Layout* L;
+    double clock;
+    uint32_t next_seq, heap_size, aq_size, uq_size, trace_cursor;
+    uint32_t err;
+    uint32_t cur_kind, cur_seq;
+};
+
+K10S_HD void fail(Ctx& c, uint32_t code) {
+    if (c.err == 0) {
+        c.err = code;
+        c.v.h->error_code = code;
+        c.v.h->error_kind = c.cur_kind;
+        c.v.h->error_seq = c.cur_seq;
+        c.v.h->error_time = c.clock;
+    }
+}
+
+// ---- small helpers ---------------------------------------------------------------------------
+K10S_HD bool bit_test(const uint64_t* w, uint32_t i) { return (w[i >> 6] >> (i & 63)) & 1ull; }
+K10S_HD void bit_set(uint64_t* w, uint32_t i) { w[i >> 6] |= (1ull << (i & 63)); }
+K10S_HD void bit_clear(uint64_t* w, uint32_t i) { w[i >> 6] &= ~(1ull << (i & 63)); }
+
+K10S_HD bool is_multiple_of_1000(double x) {
+    // fmod(x, 1000.0) == 0.0 for a simulation clock (finite, >= 0, < 2^63)
+    if (!(x >= 0.0) || x >= 9.2e18) return false;
+    double fl = __builtin_floor(x);
+    if (fl != x) return false;
+    return ((uint64_t)x % 1000ull) == 0;
+}
+
+K10S_HD uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// ---- dslab event queue: binary min-heap on (time total order, id) ------------------------------
+K10S_HD bool ev_before(double ta, uint32_t sa, double tb, uint32_t sb) {
+    int64_t ka = total_key(ta), kb = total_key(tb);
+    return ka < kb || (ka == kb && sa < sb);
+}
+
+K10S_HD uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uint32_t a, uint32_t b, double x) {
+    if (c.err) return 0;
+    if (c.next_seq == 0xFFFFFFFFu) {
+        fail(c, K10S_ERR_SEQ_OVERFLOW);
+        return 0;
+    }
+    if (c.heap_size >= c.L->cap_heap) {
+        fail(c, K10S_ERR_HEAP_FULL);
+        return 0;
+    }
+    HeapEv e;
+    e.time = c.clock + delay;
+    e.seq = c.next_seq++;
+    e.kind = (uint16_t)kind;
+    e.slot = (int16_t)slot;
+    e.a = a;
+    e.b = b;
+    e.x = x;
+    HeapEv* hp = c.v.heap;
+    uint32_t pos = c.heap_size++;
+    int64_t k = total_key(e.time);
+    while (pos > 0) {
+        uint32_t parent = (pos - 1) >> 1;
+        HeapEv p = hp[parent];
+        int64_t kp = total_key(p.time);
+        if (!(k < kp || (k == kp && e.seq < p.seq))) break;
+        hp[pos] = p;
+        pos = parent;
+    }
+    hp[pos] = e;
+    return e.seq;
+}
+K10S_HD uint32_t emit0(Ctx& c, uint32_t kind, double delay) { return emit(c, kind, delay, -1, 0, 0, 0.0); }
+
+K10S_HD void heap_pop(Ctx& c) {
+    HeapEv* hp = c.v.heap;
+    uint32_t n = --c.heap_size;
+    if (n == 0) return;
+    HeapEv last = hp[n];
+    int64_t kl = total_key(last.time);
+    uint32_t pos = 0;
+    for (;;) {
+        uint32_t l = 2 * pos + 1;
+        if (l >= n) break;
+        uint32_t r = l + 1;
+        uint32_t m = l;
+        HeapEv cl = hp[l];
+        int64_t km = total_key(cl.time);
+        uint32_t sm = cl.seq;
+        if (r < n) {
+            HeapEv cr = hp[r];
+            int64_t kr = total_key(cr.time);
+            if (kr < km || (kr == km && cr.seq < sm)) {
+                m = r;
+                km = kr;
+                sm = cr.seq;
+                cl = cr;
+            }
+        }
+        if (!(km < kl || (km == kl && sm < last.seq))) break;
+        hp[pos] = cl;
+        pos = m;
+    }
+    hp[pos] = last;
+}
+
+// ---- Rust std BinaryHeap<QueuedPodInfo> (scheduler action queue) ------------------------------
+// Ord: other.timestamp.total_cmp(&self.timestamp) => "a <= b" <=> b.ts <= a.ts (total order).
+K10S_HD bool q_le(const QInfo& a, const QInfo& b) { return total_key(b.timestamp) <= total_key(a.timestamp); }
+
+K10S_HD uint32_t aq_sift_up(QInfo* d, uint32_t start, uint32_t pos, const QInfo& elem) {
+    while (pos > start) {
+        uint32_t parent = (pos - 1) / 2;
+        QInfo p = d[parent];
+        if (q_le(elem, p)) break;
+        d[pos] = p;
+        pos = parent;
+    }
+    d[pos] = elem;
+    return pos;
+}
+K10S_HD void aq_push(Ctx& c, const QInfo& q) {
+    if (c.aq_size >= c.L->cap_aq) {
+        fail(c, K10S_ERR_QUEUE_FULL);
+        return;
+    }
+    uint32_t old = c.aq_size++;
+    aq_sift_up(c.v.aq, 0, old, q);
+}
+K10S_HD QInfo aq_pop(Ctx& c) {
+    QInfo* d = c.v.aq;
+    QInfo item = d[--c.aq_size];
+    uint32_t end = c.aq_size;
+    if (end == 0) return item;
+    QInfo top = d[0];
+    // sift_down_to_bottom(0) with `item` in the hole, then sift_up(0, pos)
+    uint32_t pos = 0;
+    uint32_t child = 1;
+    while (end >= 2 && child <= end - 2) {
+        QInfo a = d[child], b = d[child + 1];
+        if (q_le(a, b)) {
+            child += 1;
+            a = b;
+        }
+        d[pos] = a;
+        pos = child;
+        child = 2 * pos + 1;
+    }
+    if (child == end - 1) {
+        d[pos] = d[child];
+        pos = child;
+    }
+    aq_sift_up(d, 0, pos, item);
+    return top;
+}
+
+// ---- unschedulable_pods: BTreeMap<(insert_timestamp total_cmp, pod name)> as a sorted array -----
+K10S_HD bool u_less(const QInfo& a, const QInfo& b) {
+    int64_t ka = total_key(a.timestamp), kb = total_key(b.timestamp);
+    return ka < kb || (ka == kb && a.pod < b.pod);
+}
+K10S_HD void uq_insert(Ctx& c, const QInfo& q) {
+    if (c.uq_size >= c.L->cap_uq) {
+        fail(c, K10S_ERR_QUEUE_FULL);
+        return;
+    }
+    QInfo* d = c.v.uq;
+    uint32_t pos = c.uq_size++;
+    while (pos > 0) {  // timestamps are almost always >= the tail: short backward walk
+        QInfo prev = d[pos - 1];
+        if (!u_less(q, prev)) {
+            if (prev.pod == q.pod && total_key(prev.timestamp) == total_key(q.timestamp)) {
+                // BTreeMap::insert on an existing key replaces the value
+                d[pos - 1] = q;
+                for (uint32_t i = pos; i + 1 < c.uq_size; i++) d[i] = d[i + 1];
+                c.uq_size--;
+                return;
+            }
+            break;
+        }
+        d[pos] = prev;
+        pos--;
+    }
+    d[pos] = q;
+}
+
+K10S_HD bool pod_in_s(const Ctx& c, uint32_t p) { return (c.v.pflags[p] & PF_IN_S) != 0; }
+
+// move_pods_to_active_queue over a selection, in key order (scheduler.rs:174-185)
+// mode 0: all (move_all_to_active_queue, 235-244); 1: flush (188-203, stay > 300 s);
+// 2: freed-resources conditional (366-379); 3: inverted add-node conditional (396-405).
+K10S_HD void s_move(Ctx& c, int mode, double t, uint32_t cpu, uint64_t ram) {
+    QInfo* d = c.v.uq;
+    uint32_t n = c.uq_size;
+    uint32_t w = 0;
+    uint32_t fc = cpu;
+    uint64_t fr = ram;
+    if (mode >= 2) {
+        // move_to_active_queue_if reads every entry's pod from the cache before moving any
+        // (scheduler.rs:217-232): a stale entry panics with the queues untouched
+        for (uint32_t i = 0; i < n; i++) {
+            if (!pod_in_s(c, d[i].pod)) {
+                fail(c, K10S_PANIC_MISSING_POD);
+                return;
+            }
+        }
+    }
+    for (uint32_t i = 0; i < n; i++) {
+        QInfo q = d[i];
+        bool sel;
+        if (mode == 0) {
+            sel = true;
+        } else if (mode == 1) {
+            sel = (t - q.timestamp) > 5.0 * 60.0;
+        } else {
+            uint32_t rc = c.v.preq_cpu[q.pod];
+            uint64_t rr = c.v.preq_ram[q.pod];
+            if (rc <= fc && rr <= fr) {
+                fc -= rc;
+                fr -= rr;
+                sel = (mode == 2);
+            } else {
+                sel = (mode == 3);
+            }
+        }
+        if (sel && pod_in_s(c, q.pod)) {
+            q.attempts += 1;
+            aq_push(c, q);
+            if (c.err) return;
+        } else {
+            d[w++] = q;  // kept (not selected, or stale entry of a deleted pod)
+        }
+    }
+    c.uq_size = w;
+}
+K10S_HD void s_move_after_free(Ctx& c, uint32_t cpu, uint64_t ram) {
+    if (c.pr->enable_unscheduled_pods_conditional_move) s_move(c, 2, 0.0, cpu, ram);
+    else s_move(c, 0, 0.0, 0, 0);
+}
+
+// ---- running-pod lists of node components ----------------------------------------------------
+K10S_HD void run_insert(Ctx& c, int32_t slot, uint32_t p) {
+    int32_t h = c.v.slot_head[slot];
+    c.v.run_prev[p] = -1;
+    c.v.run_next[p] = h;
+    if (h >= 0) c.v.run_prev[h] = (int32_t)p;
+    c.v.slot_head[slot] = (int32_t)p;
+    c.v.run_slot[p] = slot;
+}
+K10S_HD void run_remove(Ctx& c, uint32_t p) {
+    int32_t slot = c.v.run_slot[p];
+    int32_t pr = c.v.run_prev[p], nx = c.v.run_next[p];
+    if (pr >= 0) c.v.run_next[pr] = nx;
+    else c.v.slot_head[slot] = nx;
+    if (nx >= 0) c.v.run_prev[nx] = pr;
+    c.v.run_slot[p] = -1;
+    c.v.finish_seq[p] = 0;  // cancels a pending finish event (dslab cancel_event)
+    int32_t g = c.sc->pod_group[p];
+    if (g >= 0) c.v.grp[g].running -= 1;
+}
+
+// ---- schedule_one: Fit filter + LeastAllocated score + argmax (the hot scan) -------------------
+K10S_HD double la_score(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr) {
+    double cpu_score = (double)(uint32_t)(ac - rc) * 100.0 / (double)ac;
+    double ram_score = (double)(uint64_t)(ar - rr) * 100.0 / (double)ar;
+    return (cpu_score + ram_score) / 2.0;
+}
+
+// Returns K10S_SCHED_* and writes the chosen node index.  Wave-parallel over node indices
+// (name order): lane l visits n = l, l+64, ...; per-lane "score >= best" keeps the last
+// maximum; the cross-lane (key, n) max reproduces the reference's left-to-right argmax.
+K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
+                          uint32_t rc, uint64_t rr, double weight, int32_t* chosen) {
+    const int lane = lane_id();
+    uint64_t best_key = 0;
+    int32_t best_n = -1;
+    int32_t first = 0x7fffffff;
+    for (uint32_t base = 0; base < n_nodes; base += K10S_LANES) {
+        uint32_t n = base + (uint32_t)lane;
+        if (n < n_nodes && ((present[n >> 6] >> (n & 63)) & 1ull)) {
+            uint32_t ac = s_cpu[n];
+            uint64_t ar = s_ram[n];
+            if (rc <= ac && rr <= ar) {
+                if ((int32_t)n < first) first = (int32_t)n;
+                double s = 0.0 + la_score(ac, ar, rc, rr) * weight;
+                if (!is_nan(s)) {
+                    uint64_t k = score_key(s);
+                    if (k >= best_key) {
+                        best_key = k;
+                        best_n = (int32_t)n;
+                    }
+                }
+            }
+        }
+    }
+    first = wave_min_i32(first);
+    wave_argmax(best_key, best_n);
+    if (first == 0x7fffffff) return K10S_SCHED_NO_SUFFICIENT_RESOURCES;
+    // kube_scheduler.rs:140-148: start from filtered[0]; if its score is NaN nothing replaces it
+    double s0 = 0.0 + la_score(s_cpu[first], s_ram[first], rc, rr) * weight;
+    *chosen = is_nan(s0) ? first : best_n;
+    return K10S_SCHED_OK;
+}
+
+// ---- scheduling cycle (scheduler.rs:246-334) ----------------------------------------------------
+K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
+    double cycle_dur = 0.0;
+    RepHdr* h = c.v.h;
+    const double w = c.pr->score_weight;
+    while (c.aq_size > 0 && !c.err) {
+        QInfo q = aq_pop(c);
+        uint32_t p = q.pod;
+        if (!pod_in_s(c, p)) continue;
+        double queue_t = t - q.initial + cycle_dur;
+        uint32_t nn = h->s_node_count;
+        double sched_time = 0.000001 * (double)nn;  // ConstantTimePerNodeModel (model.rs:24-26)
+        cycle_dur += sched_time;
+        uint32_t rc = c.v.preq_cpu[p];
+        uint64_t rr = c.v.preq_ram[p];
+        int st;
+        int32_t chosen = -1;
+        if (rc == 0 && rr == 0) {
+            st = K10S_SCHED_REQUESTED_RESOURCES_ARE_ZEROS;
+        } else if (nn == 0) {
+            st = K10S_SCHED_NO_NODES_IN_CLUSTER;
+        } else {
+            h->counters[K10S_C_ATTEMPTS] += 1;
+            h->counters[K10S_C_NODES_SCANNED] += nn;
+            st = schedule_scan(c.v.s_cpu, c.v.s_ram, c.v.s_present, c.sc->n_nodes, rc, rr, w, &chosen);
+        }
+        if (st != K10S_SCHED_OK) {
+            q.timestamp = t + cycle_dur;
+            uq_insert(c, q);
+            emit(c, K10S_EV_AS_POD_NOT_SCHEDULED, c.pr->sched_to_as_network_delay, -1, p, 0, t + cycle_dur);
+            continue;
+        }
+        uint32_t n = (uint32_t)chosen;
+        c.v.s_cpu[n] -= rc;  // reserve_node_resources (118-123)
+        c.v.s_ram[n] -= rr;
+        c.v.node_flags[n] |= NF_S_ASSIGN;  // assign_node_to_pod (125-151)
+        c.v.s_assigned[p] = (int32_t)n;
+        emit(c, K10S_EV_AS_ASSIGN_REQ, cycle_dur + c.pr->sched_to_as_network_delay, -1, p, n, t + cycle_dur);
+        h->counters[K10S_C_PLACEMENTS] += 1;
+        if (c.v.place) {
+            uint32_t k = h->place_n;
+            if (k < c.L->cap_place) {
+                c.v.place[k].assign_time = t + cycle_dur;
+                c.v.place[k].pod = (int32_t)p;
+                c.v.place[k].node = (int32_t)n;
+                h->place_n = k + 1;
+            } else {
+                h->flags |= 2u;
+            }
+        }
+        est_add(h->est[K10S_EST_POD_SCHEDULE_TIME], sched_time);
+        est_add(h->est[K10S_EST_POD_QUEUE_TIME], queue_t);
+    }
+    double next = fmax_rs(cycle_dur, c.pr->scheduling_cycle_interval);
+    emit0(c, K10S_EV_S_RUN_CYCLE, next);
+}
+
+// ---- pods of a node in name order (wave ballot over pod indices) ---------------------------------
+// Calls f(p) for every pod p (ascending) with pred(p); stops early if c.err.
+template <typename Pred, typename F>
+K10S_HD void for_each_pod_in_order(Ctx& c, Pred pred, F f) {
+    const uint32_t P = c.sc->n_pods;
+    for (uint32_t base = 0; base < P; base += K10S_LANES) {
+        uint32_t p = base + (uint32_t)lane_id();
+        bool m = p < P && pred(p);
+#if K10S_DEVICE
+        uint64_t mask = __ballot(m);
+        while (mask) {
+            uint32_t b = (uint32_t)__builtin_ctzll(mask);
+            mask &= mask - 1;
+            f(base + b);
+            if (c.err) return;
+        }
+#else
+        if (m) {
+            f(p);
+            if (c.err) return;
+        }
+#endif
+    }
+}
+
+// ---- scheduler handlers (scheduler.rs:382-477) ---------------------------------------------------
+K10S_HD void s_release(Ctx& c, uint32_t p) {  // release_node_resources (153-162)
+    int32_t n = c.v.s_assigned[p];
+    if (n < 0 || !bit_test(c.v.s_present, (uint32_t)n)) {
+        fail(c, K10S_PANIC_MISSING_NODE);
+        return;
+    }
+    c.v.s_cpu[n] += c.v.preq_cpu[p];
+    c.v.s_ram[n] += c.v.preq_ram[p];
+}
+
+K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
+    RepHdr* h = c.v.h;
+    switch (e.kind) {
+    case K10S_EV_S_RUN_CYCLE:
+        run_scheduling_cycle(c, e.time);
+        break;
+    case K10S_EV_S_FLUSH:
+        s_move(c, 1, e.time, 0, 0);
+        emit0(c, K10S_EV_S_FLUSH, 30.0);  // POD_FLUSH_INTERVAL (queue.rs:11)
+        break;
+    case K10S_EV_S_ADD_NODE: {
+        uint32_t n = e.a;
+        uint32_t ac = e.b;
+        uint64_t ar = f2u(e.x);
+        c.v.s_cpu[n] = ac;
+        c.v.s_ram[n] = ar;
+        if (!bit_test(c.v.s_present, n)) {
+            bit_set(c.v.s_present, n);
+            h->s_node_count += 1;
+        }
+        if (c.pr->enable_unscheduled_pods_conditional_move) s_move(c, 3, 0.0, ac, ar);
+        else s_move(c, 0, 0.0, 0, 0);
+        break;
+    }
+    case K10S_EV_S_POD_SCHEDULE_REQ: {
+        uint32_t p = e.a;
+        c.v.pflags[p] |= PF_IN_S;
+        c.v.s_assigned[p] = -1;
+        QInfo q;
+        q.timestamp = e.time;
+        q.initial = e.time;
+        q.attempts = 1;
+        q.pod = p;
+        aq_push(c, q);
+        break;
+    }
+    case K10S_EV_S_POD_FINISHED: {
+        uint32_t p = e.a, n = e.b;
+        if (!pod_in_s(c, p)) {
+            fail(c, K10S_PANIC_MISSING_POD);
+            return;
+        }
+        c.v.pflags[p] &= (uint8_t)~PF_IN_S;
+        if (!(c.v.node_flags[n] & NF_S_ASSIGN)) {
+            fail(c, K10S_PANIC_MISSING_ASSIGNMENTS);
+            return;
+        }
+        s_release(c, p);
+        if (c.err) return;
+        s_move_after_free(c, c.v.preq_cpu[p], c.v.preq_ram[p]);
+        break;
+    }
+    case K10S_EV_S_REMOVE_NODE: {
+        uint32_t n = e.a;
+        if (!bit_test(c.v.s_present, n)) {
+            fail(c, K10S_PANIC_MISSING_NODE);
+            return;
+        }
+        bit_clear(c.v.s_present, n);
+        h->s_node_count -= 1;
+        if (c.v.node_flags[n] & NF_S_ASSIGN) {  // reschedule_unfinished_pods (352-364), name order
+            c.v.node_flags[n] &= (uint8_t)~NF_S_ASSIGN;
+            double t = e.time;
+            for_each_pod_in_order(
+                c, [&](uint32_t p) { return pod_in_s(c, p) && c.v.s_assigned[p] == (int32_t)n; },
+                [&](uint32_t p) {
+                    c.v.s_assigned[p] = -1;
+                    QInfo q;
+                    q.timestamp = t;
+                    q.initial = t;
+                    q.attempts = 1;
+                    q.pod = p;
+                    aq_push(c, q);
+                });
+        }
+        break;
+    }
+    case K10S_EV_S_REMOVE_POD: {
+        uint32_t p = e.a;
+        if (!pod_in_s(c, p)) return;
+        c.v.pflags[p] &= (uint8_t)~PF_IN_S;
+        int32_t n = c.v.s_assigned[p];
+        if (n >= 0) {
+            s_release(c, p);
+            if (c.err) return;
+            if (!(c.v.node_flags[n] & NF_S_ASSIGN)) {
+                fail(c, K10S_PANIC_MISSING_ASSIGNMENTS);
+                return;
+            }
+            s_move_after_free(c, c.v.preq_cpu[p], c.v.preq_ram[p]);
+        }
+        break;
+    }
+    default:
+        break;
+    }
+}
+
+// ---- cluster autoscaler decision (kube_cluster_autoscaler.rs) -----------------------------------
+// Computed when persistent storage builds the Auto info (persistent_storage.rs:381-412): the
+// info is a snapshot of PS state at that instant, and the CA's node-group state is only touched
+// by autoscale() while exactly one request is in flight, so deciding at snapshot time and
+// emitting the actions at delivery time (cluster_autoscaler.rs:309-331) is equivalent.
+K10S_HD void ca_decide(Ctx& c) {
+    RepHdr* h = c.v.h;
+    const Scenario* sc = c.sc;
+    h->ca_n_act = 0;
+    uint32_t* cag = c.v.cag;
+    const uint64_t max_nodes = c.pr->ca_max_node_count;
+    if (h->unsched_cache_count > 0) {
+        // scale_up_info (persistent_storage.rs:137-145) looks every cached unscheduled pod up in
+        // storage before the algorithm runs: a removed one panics (the cache is never cleaned, A.5)
+        for (uint32_t p = 0; p < sc->n_pods; p++) {
+            if ((c.v.pflags[p] & PF_UNSCHED) && !(c.v.pflags[p] & PF_IN_PS)) {
+                fail(c, K10S_PANIC_MISSING_POD);
+                return;
+            }
+        }
+        // scale_up (191-245)
+        uint64_t cur = 0;
+        for (uint32_t g = 0; g < sc->n_ca_groups; g++) cur += cag[2 * g];
+        bool over = true;  // node_count_over_quota (62-80)
+        if (cur < max_nodes) {
+            for (uint32_t g = 0; g < sc->n_ca_groups; g++) {
+                if (!sc->ca_has_max[g] || cag[2 * g] < sc->ca_max[g]) {
+                    over = false;
+                    break;
+                }
+            }
+        }
+        if (over) return;
+        uint32_t nalloc = 0;
+        for (uint32_t p = 0; p < sc->n_pods && !c.err; p++) {
+            if (!(c.v.pflags[p] & PF_UNSCHED)) continue;
+            uint32_t rc = c.v.preq_cpu[p];
+            uint64_t rr = c.v.preq_ram[p];
+            bool fit = false;
+            for (uint32_t i = 0; i < nalloc; i++) {  // try_fit_in_allocated_nodes (114-123)
+                if (rc <= c.v.ca_cpu[i] && rr <= c.v.ca_ram[i]) {
+                    c.v.ca_cpu[i] -= rc;
+                    c.v.ca_ram[i] -= rr;
+                    fit = true;
+                    break;
+                }
+            }
+            if (fit) continue;
+            if (cur >= max_nodes) continue;
+            for (uint32_t g = 0; g < sc->n_ca_groups; g++) {  // try_find_fitting_template (88-112)
+                if (sc->ca_has_max[g] && cag[2 * g] >= sc->ca_max[g]) continue;
+                if (rc <= sc->ca_cpu[g] && rr <= sc->ca_ram[g]) {
+                    cag[2 * g] += 1;
+                    cag[2 * g + 1] += 1;
+                    uint32_t k = cag[2 * g + 1];
+                    if (k > sc->ca_bound) {
+                        fail(c, K10S_ERR_NAME_BOUND);
+                        return;
+                    }
+                    if (nalloc >= c.L->cap_act) {
+                        fail(c, K10S_ERR_CA_BUFFER);
+                        return;
+                    }
+                    c.v.ca_act[nalloc].up = 1;
+                    c.v.ca_act[nalloc].arg = sc->ca_def[g * sc->ca_bound + (k - 1)];
+                    c.v.ca_cpu[nalloc] = sc->ca_cpu[g];
+                    c.v.ca_ram[nalloc] = sc->ca_ram[g];
+                    nalloc++;
+                    cur++;
+                    break;
+                }
+            }
+        }
+        h->ca_n_act = nalloc;
+        return;
+    }
+    // scale_down (247-306) over PS nodes in name order with a mutable copy of their allocatable
+    const uint32_t N = sc->n_nodes;
+    for (uint32_t n = 0; n < N; n++) {
+        c.v.ca_cpu[n] = c.v.ps_cpu[n];
+        c.v.ca_ram[n] = c.v.ps_ram[n];
+    }
+    uint32_t nrem = 0;
+    for (uint32_t n = 0; n < N && !c.err; n++) {
+        if (!(c.v.node_flags[n] & NF_PS_PRESENT)) continue;
+        uint32_t def = c.v.ps_def[n];
+        if (!sc->def_ca_origin[def]) continue;
+        uint32_t cap_c = sc->def_cpu[def];
+        uint64_t cap_r = sc->def_ram[def];
+        double cu = (double)(uint32_t)(cap_c - c.v.ca_cpu[n]) / (double)cap_c;
+        double ru = (double)(uint64_t)(cap_r - c.v.ca_ram[n]) / (double)cap_r;
+        double util = cu > ru ? cu : ru;
+        if (!(util < c.pr->ca_scale_down_utilization_threshold)) continue;
+        // all_pods_can_be_moved_to_other_nodes (148-181): pods in PS assignments[n], name order
+        uint32_t nundo = 0;
+        bool ok = true;
+        uint32_t ep = c.v.ps_epoch[n];
+        for (uint32_t p = 0; p < sc->n_pods && ok; p++) {
+            if (c.v.ps_assigned[p] != (int32_t)n || c.v.ps_aepoch[p] != ep || ep == 0) continue;
+            uint32_t rc = c.v.preq_cpu[p];
+            uint64_t rr = c.v.preq_ram[p];
+            bool placed = false;
+            for (uint32_t m = 0; m < N; m++) {
+                if (m == n || !(c.v.node_flags[m] & NF_PS_PRESENT)) continue;
+                if (rc <= c.v.ca_cpu[m] && rr <= c.v.ca_ram[m]) {
+                    c.v.ca_cpu[m] -= rc;
+                    c.v.ca_ram[m] -= rr;
+                    if (nundo >= c.L->cap_undo) {
+                        fail(c, K10S_ERR_CA_BUFFER);
+                        return;
+                    }
+                    c.v.ca_undo[2 * nundo] = m;
+                    c.v.ca_undo[2 * nundo + 1] = p;
+                    nundo++;
+                    placed = true;
+                    break;
+                }
+            }
+            if (!placed) ok = false;
+        }
+        if (!ok) {
+            for (uint32_t i = 0; i < nundo; i++) {  // *nodes = original
+                uint32_t m = c.v.ca_undo[2 * i], p = c.v.ca_undo[2 * i + 1];
+                c.v.ca_cpu[m] += c.v.preq_cpu[p];
+                c.v.ca_ram[m] += c.v.preq_ram[p];
+            }
+            continue;
+        }
+        if (nrem >= c.L->cap_act) {
+            fail(c, K10S_ERR_CA_BUFFER);
+            return;
+        }
+        c.v.ca_act[nrem].up = 0;
+        c.v.ca_act[nrem].arg = n;
+        nrem++;
+    }
+    for (uint32_t i = 0; i < nrem; i++) {
+        uint32_t n = c.v.ca_act[i].arg;
+        int32_t g = sc->def_ca_group[c.v.ps_def[n]];
+        if (g < 0) {
+            fail(c, K10S_PANIC_CA_GROUP);
+            return;
+        }
+        cag[2 * g] -= 1;
+    }
+    h->ca_n_act = nrem;
+}
+
+// ---- persistent storage (persistent_storage.rs:185-490) --------------------------------------
+K10S_HD void ps_clean_up(Ctx& c, uint32_t p) {  // 173-182
+    int32_t n = c.v.ps_assigned[p];
+    if (n < 0) return;
+    if (c.v.node_flags[n] & NF_PS_PRESENT) {
+        c.v.ps_cpu[n] += c.v.preq_cpu[p];
+        c.v.ps_ram[n] += c.v.preq_ram[p];
+        if (c.v.ps_aepoch[p] == c.v.ps_epoch[n]) c.v.ps_aepoch[p] = 0;
+    }
+}
+
+K10S_HD void on_ps(Ctx& c, const HeapEv& e) {
+    RepHdr* h = c.v.h;
+    const Params* pr = c.pr;
+    switch (e.kind) {
+    case K10S_EV_PS_CREATE_NODE_REQ: {
+        uint32_t def = e.b, n = e.a;
+        if (c.v.node_flags[n] & NF_PS_PRESENT) {
+            fail(c, K10S_PANIC_DUPLICATE_NODE);
+            return;
+        }
+        c.v.node_flags[n] |= NF_PS_PRESENT;
+        c.v.ps_def[n] = def;
+        c.v.ps_cpu[n] = c.sc->def_cpu[def];
+        c.v.ps_ram[n] = c.sc->def_ram[def];
+        c.v.ps_epoch[n] += 1;
+        h->ps_node_count += 1;
+        emit(c, K10S_EV_AS_CREATE_NODE_RESP, pr->as_to_ps_network_delay, -1, n, 0, 0.0);
+        break;
+    }
+    case K10S_EV_PS_NODE_ADDED: {
+        uint32_t n = e.a;
+        if (!(c.v.node_flags[n] & NF_PS_PRESENT)) {
+            fail(c, K10S_PANIC_MISSING_NODE);
+            return;
+        }
+        emit(c, K10S_EV_S_ADD_NODE, pr->ps_to_sched_network_delay, -1, n, c.v.ps_cpu[n], u2f(c.v.ps_ram[n]));
+        h->counters[K10S_C_PROCESSED_NODES] += 1;
+        break;
+    }
+    case K10S_EV_PS_CREATE_POD_REQ: {
+        uint32_t p = e.a;
+        if (c.v.pflags[p] & PF_IN_PS) {
+            fail(c, K10S_PANIC_DUPLICATE_POD);
+            return;
+        }
+        c.v.pflags[p] |= PF_IN_PS;
+        c.v.ps_assigned[p] = -1;
+        if (c.v.prec) c.v.prec[p].state = 1;
+        emit(c, K10S_EV_S_POD_SCHEDULE_REQ, pr->ps_to_sched_network_delay, -1, p, 0, 0.0);
+        break;
+    }
+    case K10S_EV_PS_ASSIGN_REQ: {
+        uint32_t p = e.a, n = e.b;
+        if (!(c.v.pflags[p] & PF_IN_PS)) {
+            fail(c, K10S_PANIC_MISSING_POD);
+            return;
+        }
+        c.v.ps_assigned[p] = (int32_t)n;
+        if (c.v.pflags[p] & PF_UNSCHED) {
+            c.v.pflags[p] &= (uint8_t)~PF_UNSCHED;
+            h->unsched_cache_count -= 1;
+        }
+        if (!(c.v.node_flags[n] & NF_PS_PRESENT)) {
+            fail(c, K10S_PANIC_MISSING_NODE);
+            return;
+        }
+        c.v.ps_cpu[n] -= c.v.preq_cpu[p];
+        c.v.ps_ram[n] -= c.v.preq_ram[p];
+        c.v.ps_aepoch[p] = c.v.ps_epoch[n];
+        emit(c, K10S_EV_AS_ASSIGN_RESP, pr->as_to_ps_network_delay, -1, p, n, 0.0);
+        break;
+    }
+    case K10S_EV_PS_POD_NOT_SCHEDULED: {
+        uint32_t p = e.a;
+        if (!(c.v.pflags[p] & PF_IN_PS)) {
+            fail(c, K10S_PANIC_MISSING_POD);
+            return;
+        }
+        if (!(c.v.pflags[p] & PF_UNSCHED)) {
+            c.v.pflags[p] |= PF_UNSCHED;
+            h->unsched_cache_count += 1;
+        }
+        break;
+    }
+    case K10S_EV_PS_POD_STARTED: {
+        uint32_t p = e.a;
+        if (!(c.v.pflags[p] & PF_IN_PS)) {
+            fail(c, K10S_PANIC_MISSING_POD);
+            return;
+        }
+        if (c.v.prec) c.v.prec[p].t_running = e.x;
+        break;
+    }
+    case K10S_EV_PS_POD_FINISHED: {
+        uint32_t p = e.a;
+        if (c.v.pflags[p] & PF_IN_PS) {
+            c.v.pflags[p] &= (uint8_t)~PF_IN_PS;
+            ps_clean_up(c, p);
+            if (!(c.sc->pod_flags[p] & POD_HAS_DUR)) {
+                fail(c, K10S_PANIC_MISSING_POD);
+                return;
+            }
+            est_add(h->est[K10S_EST_POD_DURATION], c.v.pdur[p]);
+            if (c.v.prec) {
+                c.v.prec[p].t_finished = e.x;
+                c.v.prec[p].state = 2;
+            }
+        }
+        emit(c, K10S_EV_S_POD_FINISHED, pr->ps_to_sched_network_delay, -1, p, e.b, e.x);
+        break;
+    }
+    case K10S_EV_PS_REMOVE_NODE_REQ: {
+        uint32_t n = e.a;
+        if (!(c.v.node_flags[n] & NF_PS_PRESENT)) {
+            fail(c, K10S_PANIC_MISSING_NODE);
+            return;
+        }
+        c.v.node_flags[n] &= (uint8_t)~NF_PS_PRESENT;
+        h->ps_node_count -= 1;
+        emit(c, K10S_EV_AS_REMOVE_NODE_RESP, pr->as_to_ps_network_delay, -1, n, 0, 0.0);
+        break;
+    }
+    case K10S_EV_PS_NODE_REMOVED:
+        emit(c, K10S_EV_S_REMOVE_NODE, pr->ps_to_sched_network_delay, -1, e.a, 0, 0.0);
+        break;
+    case K10S_EV_PS_CA_REQ:
+        ca_decide(c);
+        emit0(c, K10S_EV_AS_CA_RESP, pr->as_to_ps_network_delay);
+        break;
+    case K10S_EV_PS_REMOVE_POD_REQ: {
+        uint32_t p = e.a;
+        if (!(c.v.pflags[p] & PF_IN_PS)) {
+            emit(c, K10S_EV_AS_REMOVE_POD_RESP, pr->as_to_ps_network_delay, -1, p, 0, 0.0);
+            return;
+        }
+        c.v.pflags[p] &= (uint8_t)~PF_IN_PS;
+        if (c.v.prec) {
+            c.v.prec[p].t_removed = e.time;
+            c.v.prec[p].state = 3;
+        }
+        int32_t n = c.v.ps_assigned[p];
+        uint32_t flag = 0;
+        if (n >= 0) {
+            ps_clean_up(c, p);
+            flag = 1;
+        } else {
+            emit(c, K10S_EV_S_REMOVE_POD, pr->ps_to_sched_network_delay, -1, p, 0, 0.0);
+        }
+        emit(c, K10S_EV_AS_REMOVE_POD_RESP, pr->as_to_ps_network_delay, -1, p, flag ? (uint32_t)n : 0u, u2f(flag));
+        break;
+    }
+    case K10S_EV_PS_POD_REMOVED:
+        if (e.b) emit(c, K10S_EV_S_REMOVE_POD, pr->ps_to_sched_network_delay, -1, e.a, 0, 0.0);
+        break;
+    default:
+        break;
+    }
+}
+
+// ---- api server (api_server.rs:127-457) --------------------------------------------------------
+K10S_HD void on_api_server(Ctx& c, const HeapEv& e) {
+    RepHdr* h = c.v.h;
+    const Params* pr = c.pr;
+    const Scenario* sc = c.sc;
+    switch (e.kind) {
+    case K10S_EV_AS_CREATE_NODE_REQ: {
+        uint32_t def = e.b;
+        uint32_t n = sc->def_node[def];
+        c.v.pend_def[n] = (int32_t)def;
+        emit(c, K10S_EV_PS_CREATE_NODE_REQ, pr->as_to_ps_network_delay, -1, n, def, 0.0);
+        break;
+    }
+    case K10S_EV_AS_CREATE_NODE_RESP: {  // handle_create_node (96-115)
+        uint32_t n = e.a;
+        int32_t def = c.v.pend_def[n];
+        if (def < 0) {
+            fail(c, K10S_PANIC_MISSING_PENDING);
+            return;
+        }
+        c.v.pend_def[n] = -1;
+        if (h->pool_count == 0) {
+            fail(c, K10S_PANIC_POOL_EXHAUSTED);
+            return;
+        }
+        uint32_t slot = c.v.pool_ring[h->pool_head];
+        h->pool_head = (h->pool_head + 1) % sc->n_slots;
+        h->pool_count -= 1;
+        c.v.slot_node[slot] = (int32_t)n;
+        c.v.slot_def[slot] = (uint32_t)def;
+        if (c.v.as_slot[n] >= 0) {
+            fail(c, K10S_PANIC_DUPLICATE_NODE);
+            return;
+        }
+        c.v.as_slot[n] = (int32_t)slot;
+        h->as_node_count += 1;
+        emit(c, K10S_EV_PS_NODE_ADDED, pr->as_to_ps_network_delay, -1, n, 0, e.time);
+        break;
+    }
+    case K10S_EV_AS_CREATE_POD_REQ:
+        emit(c, K10S_EV_PS_CREATE_POD_REQ, pr->as_to_ps_network_delay, -1, e.a, 0, 0.0);
+        break;
+    case K10S_EV_AS_ASSIGN_REQ: {
+        uint32_t n = e.b;
+        if (bit_test(c.v.pend_rm, sc->node_uid[n]) || c.v.as_slot[n] < 0) return;
+        emit(c, K10S_EV_PS_ASSIGN_REQ, pr->as_to_ps_network_delay, -1, e.a, n, e.x);
+        break;
+    }
+    case K10S_EV_AS_ASSIGN_RESP: {
+        uint32_t n = e.b;
+        int32_t slot = c.v.as_slot[n];
+        if (slot < 0) {
+            fail(c, K10S_PANIC_MISSING_NODE);
+            return;
+        }
+        emit(c, K10S_EV_N_BIND, pr->as_to_node_network_delay, slot, e.a, n, 0.0);
+        break;
+    }
+    case K10S_EV_AS_POD_NOT_SCHEDULED:
+        emit(c, K10S_EV_PS_POD_NOT_SCHEDULED, pr->as_to_ps_network_delay, -1, e.a, 0, e.x);
+        break;
+    case K10S_EV_AS_POD_STARTED:
+        emit(c, K10S_EV_PS_POD_STARTED, pr->as_to_ps_network_delay, -1, e.a, 0, e.x);
+        break;
+    case K10S_EV_AS_POD_FINISHED:
+        h->counters[K10S_C_TERMINATED_PODS] += 1;
+        h->counters[K10S_C_PODS_SUCCEEDED] += 1;
+        emit(c, K10S_EV_PS_POD_FINISHED, pr->as_to_ps_network_delay, -1, e.a, e.b, e.x);
+        break;
+    case K10S_EV_AS_REMOVE_NODE_REQ:
+        bit_set(c.v.pend_rm, sc->node_uid[e.a]);
+        emit(c, K10S_EV_PS_REMOVE_NODE_REQ, pr->as_to_ps_network_delay, -1, e.a, 0, 0.0);
+        break;
+    case K10S_EV_AS_REMOVE_NODE_RESP: {
+        int32_t slot = c.v.as_slot[e.a];
+        if (slot < 0) {
+            fail(c, K10S_PANIC_MISSING_NODE);
+            return;
+        }
+        emit(c, K10S_EV_N_REMOVE_NODE, pr->as_to_node_network_delay, slot, e.a, 0, 0.0);
+        break;
+    }
+    case K10S_EV_AS_NODE_REMOVED: {
+        uint32_t n = e.a;
+        int32_t slot = c.v.as_slot[n];
+        if (slot < 0) {
+            fail(c, K10S_PANIC_MISSING_NODE);
+            return;
+        }
+        c.v.as_slot[n] = -1;
+        h->as_node_count -= 1;
+        // reclaim_component (node_component_pool.rs:68-77)
+        c.v.slot_node[slot] = -1;
+        c.v.slot_removed[slot] = 0;
+        c.v.slot_rtime[slot] = 0.0;
+        c.v.slot_gen[slot] += 1;
+        c.v.slot_head[slot] = -1;
+        uint32_t tail = (h->pool_head + h->pool_count) % sc->n_slots;
+        c.v.pool_ring[tail] = (uint32_t)slot;
+        h->pool_count += 1;
+        bit_clear(c.v.pend_rm, sc->node_uid[n]);
+        emit(c, K10S_EV_PS_NODE_REMOVED, pr->as_to_ps_network_delay, -1, n, 0, e.x);
+        break;
+    }
+    case K10S_EV_AS_CA_REQ:
+        emit0(c, K10S_EV_PS_CA_REQ, pr->as_to_ps_network_delay);
+        break;
+    case K10S_EV_AS_CA_RESP:
+        emit0(c, K10S_EV_CA_RESP, pr->as_to_ca_network_delay);
+        break;
+    case K10S_EV_AS_REMOVE_POD_REQ:
+        bit_set(c.v.pend_rm, sc->pod_uid[e.a]);  // quirk (api_server.rs:343): the NODE removal set
+        emit(c, K10S_EV_PS_REMOVE_POD_REQ, pr->as_to_ps_network_delay, -1, e.a, 0, 0.0);
+        break;
+    case K10S_EV_AS_REMOVE_POD_RESP: {
+        if (f2u(e.x) != 0) {
+            int32_t slot = c.v.as_slot[e.b];
+            if (slot < 0) {
+                fail(c, K10S_PANIC_MISSING_NODE);
+                return;
+            }
+            emit(c, K10S_EV_N_REMOVE_POD, pr->as_to_node_network_delay, slot, e.a, e.b, 0.0);
+        }
+        break;
+    }
+    case K10S_EV_AS_POD_REMOVED:
+        if (e.b) {
+            h->counters[K10S_C_TERMINATED_PODS] += 1;
+            h->counters[K10S_C_PODS_REMOVED] += 1;
+        }
+        emit(c, K10S_EV_PS_POD_REMOVED, pr->as_to_ps_network_delay, -1, e.a, e.b, e.x);
+        break;
+    case K10S_EV_AS_CREATE_GROUP_REQ: {
+        uint32_t g = e.a;
+        if (sc->g_flags[g] & GF_TMPL_HAS_DUR) {
+            fail(c, K10S_PANIC_GROUP_DURATION);
+            return;
+        }
+        GroupState& gs = c.v.grp[g];
+        gs.creation_time = e.time;
+        gs.cpu_last_start = e.time;
+        gs.ram_last_start = e.time;
+        gs.cpu_idx = 0;
+        gs.ram_idx = 0;
+        gs.created_at_as = 1;
+        uint32_t init = sc->g_initial[g];
+        if (init > sc->group_bound) {
+            fail(c, K10S_ERR_NAME_BOUND);
+            return;
+        }
+        for (uint32_t k = 0; k < init && !c.err; k++)
+            emit(c, K10S_EV_PS_CREATE_POD_REQ, pr->as_to_ps_network_delay, -1, sc->g_pod[g * sc->group_bound + k], 0, 0.0);
+        if (sc->hpa_enabled) emit(c, K10S_EV_HPA_REGISTER_GROUP, pr->as_to_hpa_network_delay, -1, g, 0, e.time);
+        break;
+    }
+    default:
+        break;
+    }
+}
+
+// ---- node components (node_component.rs:178-335) ------------------------------------------------
+K10S_HD void on_node(Ctx& c, const HeapEv& e) {
+    const Params* pr = c.pr;
+    int32_t slot = e.slot;
+    switch (e.kind) {
+    case K10S_EV_N_BIND: {
+        uint32_t p = e.a, n = e.b;
+        if (c.v.slot_removed[slot]) {
+            fail(c, K10S_PANIC_BIND_REMOVED_NODE);
+            return;
+        }
+        if (c.v.slot_node[slot] != (int32_t)n) {
+            fail(c, K10S_PANIC_BIND_REMOVED_NODE);
+            return;
+        }
+        if (c.v.run_slot[p] >= 0) {  // a second concurrent bind of one pod: not modelled
+            fail(c, K10S_PANIC_BIND_REMOVED_NODE);
+            return;
+        }
+        uint32_t fseq = 0;
+        if (c.sc->pod_flags[p] & POD_HAS_DUR) {  // simulate_pod_runtime (114-175)
+            double dur = c.v.pdur[p];
+            fseq = emit(c, K10S_EV_N_POD_FINISHED, dur + pr->as_to_node_network_delay, slot, p, n, e.time + dur);
+        }
+        run_insert(c, slot, p);
+        c.v.finish_seq[p] = fseq;
+        int32_t g = c.sc->pod_group[p];
+        if (g >= 0) c.v.grp[g].running += 1;
+        emit(c, K10S_EV_AS_POD_STARTED, pr->as_to_node_network_delay, -1, p, 0, e.time);
+        break;
+    }
+    case K10S_EV_N_POD_FINISHED: {
+        uint32_t p = e.a;
+        if (c.v.run_slot[p] != slot) {
+            fail(c, K10S_PANIC_MISSING_POD);
+            return;
+        }
+        run_remove(c, p);
+        emit(c, K10S_EV_AS_POD_FINISHED, 0.0, -1, p, e.b, e.x);  // emit_now
+        break;
+    }
+    case K10S_EV_N_REMOVE_NODE: {
+        uint32_t n = e.a;
+        if (c.v.slot_node[slot] != (int32_t)n) {
+            fail(c, K10S_PANIC_REMOVE_OTHER_NODE);
+            return;
+        }
+        // cancel_all_running_pods (95-112)
+        int32_t p = c.v.slot_head[slot];
+        uint32_t gen = c.v.slot_gen[slot];
+        while (p >= 0) {
+            int32_t nx = c.v.run_next[p];
+            c.v.cancel_slot[p] = slot;
+            c.v.cancel_gen[p] = gen;
+            run_remove(c, (uint32_t)p);
+            p = nx;
+        }
+        emit(c, K10S_EV_AS_NODE_REMOVED, pr->as_to_node_network_delay, -1, n, 0, e.time);
+        c.v.slot_removed[slot] = 1;
+        c.v.slot_rtime[slot] = e.time;
+        break;
+    }
+    case K10S_EV_N_REMOVE_POD: {
+        uint32_t p = e.a;
+        if (c.v.slot_node[slot] < 0) {
+            fail(c, K10S_PANIC_MISSING_NODE);
+            return;
+        }
+        if (c.v.run_slot[p] == slot) {
+            run_remove(c, p);
+            emit(c, K10S_EV_AS_POD_REMOVED, pr->as_to_node_network_delay, -1, p, 1, e.time);
+        } else if (c.v.cancel_slot[p] == slot && c.v.cancel_gen[p] == c.v.slot_gen[slot]) {
+            emit(c, K10S_EV_AS_POD_REMOVED, pr->as_to_node_network_delay, -1, p, 1, c.v.slot_rtime[slot]);
+        } else {
+            emit(c, K10S_EV_AS_POD_REMOVED, pr->as_to_node_network_delay, -1, p, 0, 0.0);
+        }
+        break;
+    }
+    default:
+        break;
+    }
+}
+
+// ---- cluster autoscaler proxy (cluster_autoscaler.rs:230-334) --------------------------------
+K10S_HD void on_ca(Ctx& c, const HeapEv& e) {
+    RepHdr* h = c.v.h;
+    const Params* pr = c.pr;
+    if (e.kind == K10S_EV_CA_TICK) {
+        h->ca_last_cycle_time = e.time;
+        emit0(c, K10S_EV_AS_CA_REQ, pr->as_to_ca_network_delay);
+        return;
+    }
+    for (uint32_t i = 0; i < h->ca_n_act && !c.err; i++) {
+        CAAct a = c.v.ca_act[i];
+        if (a.up) {
+            emit(c, K10S_EV_AS_CREATE_NODE_REQ, pr->as_to_ca_network_delay, -1, c.sc->def_node[a.arg], a.arg, 0.0);
+            h->counters[K10S_C_TOTAL_SCALED_UP_NODES] += 1;
+        } else {
+            emit(c, K10S_EV_AS_REMOVE_NODE_REQ, pr->as_to_ca_network_delay, -1, a.arg, 0, 0.0);
+            h->counters[K10S_C_TOTAL_SCALED_DOWN_NODES] += 1;
+        }
+    }
+    h->ca_n_act = 0;
+    double delay = pr->ca_scan_interval;
+    if (e.time - h->ca_last_cycle_time > pr->ca_scan_interval) delay = 0.0;
+    emit0(c, K10S_EV_CA_TICK, delay);
+}
+
+// ---- HPA (horizontal_pod_autoscaler.rs:146-257, kube_horizontal_pod_autoscaler.rs:54-216) ----
+// Groups are visited in name order (the reference iterates a HashMap: A.5).
+K10S_HD uint32_t hpa_desired_by_metric(uint32_t cur, double value, double target, double tol) {
+    double ratio = value / target;
+    if (__builtin_fabs(ratio - 1.0) <= tol) return cur;
+    uint64_t d = f64_as_u64(__builtin_ceil((double)cur * ratio));
+    return d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
+}
+
+K10S_HD void on_hpa(Ctx& c, const HeapEv& e) {
+    RepHdr* h = c.v.h;
+    const Scenario* sc = c.sc;
+    const uint32_t B = sc->group_bound;
+    const uint32_t words = c.L->words_group;
+    if (e.kind == K10S_EV_HPA_REGISTER_GROUP) {
+        uint32_t g = e.a;
+        GroupState& gs = c.v.grp[g];
+        gs.registered = 1;
+        uint64_t* bits = c.v.grp_bits + (uint64_t)g * words;
+        for (uint32_t i = 0; i < words; i++) bits[i] = 0;
+        uint32_t init = sc->g_initial[g];
+        for (uint32_t k = 0; k < init; k++) bit_set(bits, sc->g_pos[g * B + k]);
+        gs.created_count = init;
+        gs.total_created = init;
+        return;
+    }
+    for (uint32_t g = 0; g < sc->n_groups && !c.err; g++) {
+        GroupState& gs = c.v.grp[g];
+        if (!gs.has_metric) continue;
+        if (!gs.registered) {
+            fail(c, K10S_PANIC_HPA_UNREGISTERED);
+            return;
+        }
+        uint8_t gf = sc->g_flags[g];
+        uint32_t cur = gs.created_count;
+        const double tol = c.pr->hpa_target_threshold_tolerance;
+        uint32_t dc = (gf & GF_HAS_TCPU) ? hpa_desired_by_metric(cur, gs.util_cpu, sc->g_tcpu[g], tol) : 0;
+        uint32_t dr = (gf & GF_HAS_TRAM) ? hpa_desired_by_metric(cur, gs.util_ram, sc->g_tram[g], tol) : 0;
+        uint32_t mx = sc->g_max[g];
+        uint32_t desired;
+        if ((gf & GF_HAS_TCPU) && (gf & GF_HAS_TRAM)) desired = (dc > dr ? dc : dr) < mx ? (dc > dr ? dc : dr) : mx;
+        else if (gf & GF_HAS_TCPU) desired = dc < mx ? dc : mx;
+        else if (gf & GF_HAS_TRAM) desired = dr < mx ? dr : mx;
+        else desired = cur;
+        uint64_t* bits = c.v.grp_bits + (uint64_t)g * words;
+        if (cur < desired) {
+            for (uint32_t i = 0; i < desired - cur && !c.err; i++) {
+                uint32_t k = gs.total_created;
+                if (k >= B) {
+                    fail(c, K10S_ERR_NAME_BOUND);
+                    return;
+                }
+                bit_set(bits, sc->g_pos[g * B + k]);
+                gs.created_count += 1;
+                gs.total_created += 1;
+                emit(c, K10S_EV_AS_CREATE_POD_REQ, c.pr->as_to_ca_network_delay, -1, sc->g_pod[g * B + k], 0, 0.0);
+                h->counters[K10S_C_TOTAL_SCALED_UP_PODS] += 1;
+            }
+        } else if (cur > desired) {
+            for (uint32_t i = 0; i < cur - desired && !c.err; i++) {
+                uint32_t j = 0;  // created_pods.pop_first(): smallest name
+                for (uint32_t w = 0; w < words; w++) {
+                    if (bits[w]) {
+                        j = w * 64 + (uint32_t)__builtin_ctzll(bits[w]);
+                        break;
+                    }
+                }
+                bit_clear(bits, j);
+                gs.created_count -= 1;
+                uint32_t k = sc->g_sorted_k[g * B + j];
+                emit(c, K10S_EV_AS_REMOVE_POD_REQ, c.pr->as_to_ca_network_delay, -1, sc->g_pod[g * B + k], 0, 0.0);
+                h->counters[K10S_C_TOTAL_SCALED_DOWN_PODS] += 1;
+            }
+        }
+    }
+    emit0(c, K10S_EV_HPA_TICK, c.pr->hpa_scan_interval);
+}
+
+// ---- metrics collector (collector.rs:263-337, 410-431) -----------------------------------------
+K10S_HD double usage_poll(const Scenario* sc, uint8_t kind, double usage, uint32_t uoff, uint32_t ucnt, double& last_start,
+                          uint32_t& idx, double t, uint32_t count) {
+    if (kind == MODEL_NONE) return 0.0;
+    if (kind == MODEL_CONSTANT) return usage;
+    // PodGroupResourceUsageModel::current_usage (pod_group.rs:167-201)
+    while (last_start + sc->unit_dur[uoff + idx] <= t) {
+        last_start += sc->unit_dur[uoff + idx];
+        idx = (idx + 1) % ucnt;
+    }
+    return fmin_rs(1.0, sc->unit_load[uoff + idx] / (double)count);
+}
+
+K10S_HD void on_metrics(Ctx& c, const HeapEv& e) {
+    if (e.kind == K10S_EV_M_GAUGE_TICK) {  // CSV gauge record: no simulation state (collector.rs:392-407)
+        emit0(c, K10S_EV_M_GAUGE_TICK, 5.0);
+        return;
+    }
+    const Scenario* sc = c.sc;
+    for (uint32_t g = 0; g < sc->n_groups; g++) {
+        GroupState& gs = c.v.grp[g];
+        gs.has_metric = gs.running > 0;
+        if (!gs.has_metric) continue;
+        // every pod of the group reports the same value (same model, creation time and count), so the
+        // Mean estimator over them is exactly that value
+        gs.util_cpu = usage_poll(sc, sc->g_cpu_kind[g], sc->g_cpu_usage[g], sc->g_cpu_uoff[g], sc->g_cpu_ucnt[g],
+                                 gs.cpu_last_start, gs.cpu_idx, e.time, gs.running);
+        gs.util_ram = usage_poll(sc, sc->g_ram_kind[g], sc->g_ram_usage[g], sc->g_ram_uoff[g], sc->g_ram_ucnt[g],
+                                 gs.ram_last_start, gs.ram_idx, e.time, gs.running);
+    }
+    emit0(c, K10S_EV_M_POD_METRICS_TICK, 60.0);
+}
+
+K10S_HD void dispatch(Ctx& c, const HeapEv& e) {
+    uint32_t k = e.kind;
+    if (k <= K10S_EV_M_GAUGE_TICK) on_metrics(c, e);
+    else if (k <= K10S_EV_AS_CREATE_GROUP_REQ) on_api_server(c, e);
+    else if (k <= K10S_EV_PS_POD_REMOVED) on_ps(c, e);
+    else if (k <= K10S_EV_S_REMOVE_POD) on_scheduler(c, e);
+    else if (k <= K10S_EV_N_REMOVE_POD) on_node(c, e);
+    else if (k <= K10S_EV_CA_RESP) on_ca(c, e);
+    else on_hpa(c, e);
+}
+
+// ---- initialize (simulator.rs:68-275 minus the trace emission, which is the shared stream) -----
+K10S_HD void perturb_pod(const Params& pr, uint32_t key, uint32_t& cpu, uint64_t& ram, double& dur) {
+    uint64_t u = splitmix64(pr.seed ^ (0xD1B54A32D192ED03ull * ((uint64_t)key + 1)));
+    uint32_t kd = 8 + (uint32_t)(u % 17ull);              // duration x 0.5 .. 1.5
+    uint32_t kc = 12 + (uint32_t)((u >> 20) % 9ull);      // cpu x 0.75 .. 1.25
+    uint32_t kr = 12 + (uint32_t)((u >> 40) % 9ull);      // ram x 0.75 .. 1.25
+    dur = (dur * (double)kd) * 0.0625;
+    cpu = (uint32_t)(((uint64_t)cpu * kc) >> 4);
+    ram = (ram >> 4) * kr;
+}
+
+K10S_HD void init_replica(const Scenario* sc, const Params* pr, const Layout* L, uint8_t* base, uint32_t r) {
+    const uint32_t* pod_key = sc->pod_key;
+    Rep v = make_rep(base, *L, r);
+    const int lane = lane_id();
+    const uint32_t N = sc->n_nodes, P = sc->n_pods, S = sc->n_slots, G = sc->n_groups;
+    for (uint32_t i = lane; i < N; i += K10S_LANES) {
+        v.s_cpu[i] = 0;
+        v.s_ram[i] = 0;
+        v.node_flags[i] = 0;
+        v.ps_cpu[i] = 0;
+        v.ps_ram[i] = 0;
+        v.ps_def[i] = 0;
+        v.ps_epoch[i] = 0;
+        v.as_slot[i] = -1;
+        v.pend_def[i] = -1;
+    }
+    for (uint32_t i = lane; i < L->words_nodes; i += K10S_LANES) v.s_present[i] = 0;
+    for (uint32_t i = lane; i < L->words_uids; i += K10S_LANES) v.pend_rm[i] = 0;
+    const bool perturb = pr->perturb != 0;
+    for (uint32_t p = lane; p < P; p += K10S_LANES) {
+        uint32_t cpu = sc->pod_cpu[p];
+        uint64_t ram = sc->pod_ram[p];
+        double dur = sc->pod_dur[p];
+        if (perturb && (sc->pod_flags[p] & POD_PERTURB)) perturb_pod(*pr, pod_key[p], cpu, ram, dur);
+        v.preq_cpu[p] = cpu;
+        v.preq_ram[p] = ram;
+        v.pdur[p] = dur;
+        v.pflags[p] = 0;
+        v.s_assigned[p] = -1;
+        v.ps_assigned[p] = -1;
+        v.ps_aepoch[p] = 0;
+        v.run_slot[p] = -1;
+        v.run_prev[p] = -1;
+        v.run_next[p] = -1;
+        v.finish_seq[p] = 0;
+        v.cancel_slot[p] = -1;
+        v.cancel_gen[p] = 0;
+        if (v.prec) {
+            v.prec[p].t_running = __builtin_nan("");
+            v.prec[p].t_finished = __builtin_nan("");
+            v.prec[p].t_removed = __builtin_nan("");
+            v.prec[p].state = 0;
+            v.prec[p].pad = 0;
+        }
+    }
+    for (uint32_t s = lane; s < S; s += K10S_LANES) {
+        v.slot_node[s] = -1;
+        v.slot_def[s] = 0;
+        v.slot_removed[s] = 0;
+        v.slot_rtime[s] = 0.0;
+        v.slot_gen[s] = 0;
+        v.slot_head[s] = -1;
+        v.pool_ring[s] = s;  // pool contexts first (FIFO), default-node components after
+    }
+    for (uint32_t g = lane; g < G; g += K10S_LANES) {
+        GroupState gs;
+        memset(&gs, 0, sizeof gs);
+        v.grp[g] = gs;
+    }
+    for (uint32_t i = lane; i < G * L->words_group; i += K10S_LANES) v.grp_bits[i] = 0;
+    for (uint32_t i = lane; i < 2 * sc->n_ca_groups; i += K10S_LANES) v.cag[i] = 0;
+    wave_sync();
+
+    // serial part (wave-uniform)
+    RepHdr* h = v.h;
+    RepHdr z;
+    memset(&z, 0, sizeof z);
+    *h = z;
+    for (int i = 0; i < 3; i++) est_reset(h->est[i]);
+    h->counters[K10S_C_TOTAL_PODS_IN_TRACE] = sc->total_pods_in_trace;
+    h->counters[K10S_C_TOTAL_NODES_IN_TRACE] = sc->total_nodes_in_trace;
+    h->pool_head = 0;
+    h->pool_count = sc->n_pool;
+    // initialize_default_cluster (simulator.rs:303-344): present in PS, AS (own component) and S
+    for (uint32_t j = 0; j < sc->n_default; j++) {
+        uint32_t def = sc->default_defs[j];
+        uint32_t n = sc->def_node[def];
+        uint32_t slot = sc->n_pool + j;
+        v.node_flags[n] |= NF_PS_PRESENT;
+        v.ps_def[n] = def;
+        v.ps_cpu[n] = sc->def_cpu[def];
+        v.ps_ram[n] = sc->def_ram[def];
+        v.ps_epoch[n] = 1;
+        v.as_slot[n] = (int32_t)slot;
+        v.slot_node[slot] = (int32_t)n;
+        v.slot_def[slot] = def;
+        v.s_cpu[n] = sc->def_cpu[def];
+        v.s_ram[n] = sc->def_ram[def];
+        bit_set(v.s_present, n);
+    }
+    h->s_node_count = sc->n_default;
+    h->ps_node_count = sc->n_default;
+    h->as_node_count = sc->n_default;
+
+    Ctx c;
+    c.sc = sc;
+    c.pr = pr;
+    c.v = v;
+    c.L = L;
+    c.clock = 0.0;
+    c.next_seq = 0;
+    c.heap_size = 0;
+    c.aq_size = 0;
+    c.uq_size = 0;
+    c.trace_cursor = 0;
+    c.err = 0;
+    c.cur_kind = 0xFFFF;
+    c.cur_seq = 0;
+    emit0(c, K10S_EV_M_POD_METRICS_TICK, 0.0);  // id 0 (simulator.rs:156-158)
+    emit0(c, K10S_EV_M_GAUGE_TICK, 0.0);        // id 1 (simulator.rs:159-161)
+    c.next_seq = sc->first_dynamic_seq;         // trace events hold ids 2 .. 2 + n_trace - 1
+    emit0(c, K10S_EV_S_RUN_CYCLE, 0.0);         // Scheduler::start (scheduler.rs:78-81)
+    emit0(c, K10S_EV_S_FLUSH, 0.0);
+    if (sc->ca_enabled) emit0(c, K10S_EV_CA_TICK, 0.0);
+    if (sc->hpa_enabled) emit0(c, K10S_EV_HPA_TICK, 0.0);
+    h->clock = c.clock;
+    h->next_seq = c.next_seq;
+    h->heap_size = c.heap_size;
+    h->aq_size = 0;
+    h->uq_size = 0;
+    h->trace_cursor = 0;
+    h->status = K10S_REPLICA_RUNNING;
+    h->error_code = c.err;
+}
+
+// ---- the event loop -----------------------------------------------------------------------------
+// Returns 1 if the replica still has work (event budget exhausted), else 0.
+K10S_HD int run_replica(const Scenario* sc, const Params* pr, const Layout* L, uint8_t* base, uint32_t r, int mode,
+                        double until_time, double max_time, uint64_t budget) {
+    Rep v = make_rep(base, *L, r);
+    RepHdr* h = v.h;
+    if (h->status != K10S_REPLICA_RUNNING) return 0;
+    Ctx c;
+    c.sc = sc;
+    c.pr = pr;
+    c.v = v;
+    c.L = L;
+    c.clock = h->clock;
+    c.next_seq = h->next_seq;
+    c.heap_size = h->heap_size;
+    c.aq_size = h->aq_size;
+    c.uq_size = h->uq_size;
+    c.trace_cursor = h->trace_cursor;
+    c.err = h->error_code;
+    c.cur_kind = 0xFFFF;
+    c.cur_seq = 0;
+    const uint64_t total_pods = sc->total_pods_in_trace;
+    const TraceEv* tr = sc->trace;
+    const uint32_t ntr = sc->n_trace;
+    uint64_t done = 0;
+    int more = 0;
+    uint32_t status = K10S_REPLICA_RUNNING;
+    while (!c.err) {
+        if (mode == K10S_RUN_UNTIL_ALL_FINISHED && is_multiple_of_1000(c.clock) &&
+            h->counters[K10S_C_TERMINATED_PODS] >= total_pods) {
+            status = K10S_REPLICA_FINISHED;
+            break;
+        }
+        // next non-canceled event: merge the shared trace stream with the dynamic heap
+        HeapEv e;
+        bool from_trace = false;
+        bool have = false;
+        for (;;) {
+            bool ht = c.trace_cursor < ntr;
+            bool hh = c.heap_size > 0;
+            if (!ht && !hh) break;
+            if (ht) {
+                const TraceEv& te = tr[c.trace_cursor];
+                if (!hh || ev_before(te.time, te.seq, c.v.heap[0].time, c.v.heap[0].seq)) {
+                    e.time = te.time;
+                    e.seq = te.seq;
+                    e.kind = (uint16_t)te.kind;
+                    e.slot = -1;
+                    e.x = 0.0;
+                    e.a = te.arg;
+                    e.b = 0;
+                    if (te.kind == K10S_EV_AS_CREATE_NODE_REQ) {
+                        e.a = sc->def_node[te.arg];
+                        e.b = te.arg;
+                    }
+                    from_trace = true;
+                    have = true;
+                    break;
+                }
+            }
+            e = c.v.heap[0];
+            if (e.kind == K10S_EV_N_POD_FINISHED && c.v.finish_seq[e.a] != e.seq) {  // canceled
+                heap_pop(c);
+                continue;
+            }
+            have = true;
+            break;
+        }
+        if (!have) {
+            if (mode == K10S_RUN_UNTIL_TIME) c.clock = until_time;
+            status = mode == K10S_RUN_UNTIL_TIME ? K10S_REPLICA_RUNNING : K10S_REPLICA_FINISHED;
+            break;
+        }
+        if (mode == K10S_RUN_UNTIL_TIME && e.time > until_time) {
+            c.clock = until_time;
+            break;
+        }
+        if (mode == K10S_RUN_UNTIL_ALL_FINISHED && e.time > max_time) {
+            status = K10S_REPLICA_TIME_LIMIT;
+            break;
+        }
+        if (budget && done >= budget) {
+            more = 1;
+            break;
+        }
+        if (from_trace) c.trace_cursor++;
+        else heap_pop(c);
+        c.clock = e.time;
+        c.cur_kind = e.kind;
+        c.cur_seq = e.seq;
+        done++;
+        h->counters[K10S_C_EVENTS] += 1;
+        if (v.log) {
+            uint32_t k = h->log_n;
+            if (k < L->cap_log) {
+                k10s_log_entry le;
+                le.time = e.time;
+                le.seq = e.seq;
+                le.kind = e.kind;
+                le.slot = e.slot;
+                int32_t pod = -1, node = -1;
+                switch (e.kind) {
+                case K10S_EV_AS_CREATE_NODE_REQ: case K10S_EV_AS_CREATE_NODE_RESP: case K10S_EV_AS_REMOVE_NODE_REQ:
+                case K10S_EV_AS_REMOVE_NODE_RESP: case K10S_EV_AS_NODE_REMOVED: case K10S_EV_PS_CREATE_NODE_REQ:
+                case K10S_EV_PS_NODE_ADDED: case K10S_EV_PS_REMOVE_NODE_REQ: case K10S_EV_PS_NODE_REMOVED:
+                case K10S_EV_S_ADD_NODE: case K10S_EV_S_REMOVE_NODE: case K10S_EV_N_REMOVE_NODE:
+                    node = (int32_t)e.a;
+                    break;
+                case K10S_EV_AS_ASSIGN_REQ: case K10S_EV_AS_ASSIGN_RESP: case K10S_EV_AS_POD_FINISHED:
+                case K10S_EV_PS_ASSIGN_REQ: case K10S_EV_PS_POD_FINISHED: case K10S_EV_S_POD_FINISHED:
+                case K10S_EV_N_BIND: case K10S_EV_N_POD_FINISHED:
+                    pod = (int32_t)e.a;
+                    node = (int32_t)e.b;
+                    break;
+                case K10S_EV_AS_REMOVE_POD_RESP:
+                    pod = (int32_t)e.a;
+                    node = f2u(e.x) ? (int32_t)e.b : -1;
+                    break;
+                case K10S_EV_AS_CREATE_POD_REQ: case K10S_EV_AS_POD_NOT_SCHEDULED: case K10S_EV_AS_POD_STARTED:
+                case K10S_EV_AS_REMOVE_POD_REQ: case K10S_EV_AS_POD_REMOVED: case K10S_EV_PS_CREATE_POD_REQ:
+                case K10S_EV_PS_POD_NOT_SCHEDULED: case K10S_EV_PS_POD_STARTED: case K10S_EV_PS_REMOVE_POD_REQ:
+                case K10S_EV_PS_POD_REMOVED: case K10S_EV_S_POD_SCHEDULE_REQ: case K10S_EV_S_REMOVE_POD:
+                case K10S_EV_N_REMOVE_POD:
+                    pod = (int32_t)e.a;
+                    break;
+                default:
+                    break;
+                }
+                le.pod = pod;
+                le.node = node;
+                v.log[k] = le;
+                h->log_n = k + 1;
+            } else {
+                h->flags |= 1u;
+            }
+        }
+        dispatch(c, e);
+    }
+    if (c.err) status = K10S_REPLICA_ERROR;
+    h->clock = c.clock;
+    h->next_seq = c.next_seq;
+    h->heap_size = c.heap_size;
+    h->aq_size = c.aq_size;
+    h->uq_size = c.uq_size;
+    h->trace_cursor = c.trace_cursor;
+    h->status = status;
+    return more;
+}
+
+}  // namespace k10s

@@ -1,0 +1,309 @@
+// k10s_host.cpp — C ABI (include/k10s.h) of the MI355X engine: scenario compilation, device
+// memory, launches, result readback.  Requires a HIP device; there is no CPU fallback.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/k10s.h"
+#include "k10s_builder.h"
+#include "k10s_results.h"
+
+using namespace k10s;
+
+hipError_t k10s_launch_init(const Scenario& sc, const Params* d_params, const Layout& L, uint8_t* d_state,
+                            uint32_t n_replicas, hipStream_t s);
+hipError_t k10s_launch_run(const Scenario& sc, const Params* d_params, const Layout& L, uint8_t* d_state,
+                           uint32_t n_replicas, int mode, double until_time, double max_time, uint64_t budget,
+                           uint32_t* d_active, hipStream_t s);
+hipError_t k10s_launch_schedule(const uint32_t* alloc_cpu, const uint64_t* alloc_ram, const uint64_t* present,
+                                uint32_t n_nodes, uint32_t node_stride, const uint32_t* req_cpu, const uint64_t* req_ram,
+                                double weight, uint32_t n_problems, int32_t* out_node, int32_t* out_status,
+                                hipStream_t s);
+
+namespace {
+thread_local std::string g_err;
+
+int32_t set_err(int32_t code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+#define HIPCHK(x)                                                                           \
+    do {                                                                                    \
+        hipError_t _e = (x);                                                                \
+        if (_e != hipSuccess) return set_err(K10S_E_HIP, std::string(#x ": ") + hipGetErrorString(_e)); \
+    } while (0)
+}  // namespace
+
+struct k10s_engine {
+    HostScenario hs;
+    Scenario dsc;       // device view
+    Layout L;
+    uint32_t R = 0;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    void* d_scen = nullptr;
+    uint8_t* d_state = nullptr;
+    Params* d_params = nullptr;
+    uint32_t* d_active = nullptr;
+    uint32_t* h_active = nullptr;  // pinned
+    std::vector<Params> params;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+static void engine_free(k10s_engine* e) {
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    if (e->d_scen) (void)hipFree(e->d_scen);
+    if (e->d_state) (void)hipFree(e->d_state);
+    if (e->d_params) (void)hipFree(e->d_params);
+    if (e->d_active) (void)hipFree(e->d_active);
+    if (e->h_active) (void)hipHostFree(e->h_active);
+    if (e->ev0) (void)hipEventDestroy(e->ev0);
+    if (e->ev1) (void)hipEventDestroy(e->ev1);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+}
+
+static int32_t engine_init(k10s_engine* e) {
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(k10s_launch_init(e->dsc, e->d_params, e->L, e->d_state, e->R, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return K10S_OK;
+}
+
+extern "C" {
+
+const char* k10s_last_error(void) { return g_err.c_str(); }
+const char* k10s_version(void) { return "k10s-mi355x 0.1 (gfx950)"; }
+
+int32_t k10s_schedule_one_batch(const uint32_t* alloc_cpu, const uint64_t* alloc_ram, const uint64_t* present_bits,
+                                uint32_t n_nodes, uint32_t node_stride, const uint32_t* req_cpu, const uint64_t* req_ram,
+                                double weight, uint32_t n_problems, int32_t* out_node, int32_t* out_status,
+                                void* stream) {
+    if (n_problems == 0) return K10S_OK;
+    if (!alloc_cpu || !alloc_ram || !present_bits || !req_cpu || !req_ram || !out_node || !out_status)
+        return set_err(K10S_E_INVALID, "null pointer");
+    if (node_stride % 64 != 0 || node_stride < n_nodes) return set_err(K10S_E_INVALID, "node_stride must be a multiple of 64 and >= n_nodes");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return set_err(K10S_E_NO_DEVICE, "no HIP device");
+    HIPCHK(k10s_launch_schedule(alloc_cpu, alloc_ram, present_bits, n_nodes, node_stride, req_cpu, req_ram, weight,
+                                n_problems, out_node, out_status, (hipStream_t)stream));
+    return K10S_OK;
+}
+
+k10s_engine* k10s_engine_create(const char* scenario_text, const k10s_replica_params* params, uint32_t n_replicas,
+                                const k10s_capacities* caps, int32_t device) {
+    if (!scenario_text || n_replicas == 0) {
+        set_err(K10S_E_INVALID, "scenario_text is NULL or n_replicas == 0");
+        return nullptr;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        set_err(K10S_E_NO_DEVICE, "no HIP device: the k10s engine runs only on the GPU");
+        return nullptr;
+    }
+    if (device < 0 || device >= ndev) {
+        set_err(K10S_E_INVALID, "device index out of range");
+        return nullptr;
+    }
+    k10s_capacities c;
+    std::memset(&c, 0, sizeof c);
+    if (caps) c = *caps;
+    auto* e = new k10s_engine();
+    e->device = device;
+    e->R = n_replicas;
+    std::string err;
+    if (!build_scenario(scenario_text, c.group_name_bound, c.ca_name_bound, e->hs, err)) {
+        set_err(K10S_E_INVALID, "scenario: " + err);
+        delete e;
+        return nullptr;
+    }
+    e->L = make_layout(e->hs, c);
+    e->params.resize(n_replicas);
+    for (uint32_t r = 0; r < n_replicas; r++) {
+        if (params) {
+            e->params[r] = params[r];
+        } else {
+            e->params[r] = e->hs.defaults;
+            e->params[r].seed = e->hs.defaults.seed + r;
+        }
+        e->params[r].ca_max_node_count = e->hs.defaults.ca_max_node_count;  // fixed by the node pool
+    }
+    auto fail = [&](const std::string& m) -> k10s_engine* {
+        set_err(K10S_E_HIP, m);
+        engine_free(e);
+        return nullptr;
+    };
+    if (hipSetDevice(device) != hipSuccess) return fail("hipSetDevice");
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return fail("hipStreamCreate");
+    (void)hipEventCreate(&e->ev0);
+    (void)hipEventCreate(&e->ev1);
+    Scenario offs;
+    std::vector<uint8_t> img = pack_scenario(e->hs, offs);
+    if (hipMalloc(&e->d_scen, img.size()) != hipSuccess) return fail("hipMalloc scenario");
+    if (hipMemcpy(e->d_scen, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess) return fail("upload scenario");
+    e->dsc = rebase_scenario(offs, (const uint8_t*)e->d_scen);
+    size_t bytes = (size_t)e->L.stride * n_replicas;
+    size_t free_b = 0, total_b = 0;
+    (void)hipMemGetInfo(&free_b, &total_b);
+    if (bytes + (64ull << 20) > free_b) {
+        set_err(K10S_E_CAPACITY, "replica state (" + std::to_string(bytes >> 20) + " MiB) exceeds free device memory");
+        engine_free(e);
+        return nullptr;
+    }
+    if (hipMalloc(&e->d_state, bytes) != hipSuccess) return fail("hipMalloc replica state");
+    if (hipMalloc(&e->d_params, sizeof(Params) * n_replicas) != hipSuccess) return fail("hipMalloc params");
+    if (hipMemcpy(e->d_params, e->params.data(), sizeof(Params) * n_replicas, hipMemcpyHostToDevice) != hipSuccess)
+        return fail("upload params");
+    if (hipMalloc(&e->d_active, 64) != hipSuccess) return fail("hipMalloc active");
+    if (hipHostMalloc(&e->h_active, 64) != hipSuccess) return fail("hipHostMalloc");
+    if (engine_init(e) != K10S_OK) {
+        std::string m = g_err;
+        engine_free(e);
+        set_err(K10S_E_HIP, m);
+        return nullptr;
+    }
+    return e;
+}
+
+void k10s_engine_destroy(k10s_engine* e) { engine_free(e); }
+
+int32_t k10s_engine_default_params(const k10s_engine* e, k10s_replica_params* out) {
+    if (!e || !out) return set_err(K10S_E_INVALID, "null");
+    *out = e->hs.defaults;
+    return K10S_OK;
+}
+
+int32_t k10s_engine_reset(k10s_engine* e) {
+    if (!e) return set_err(K10S_E_INVALID, "null");
+    return engine_init(e);
+}
+
+int32_t k10s_engine_step_async(k10s_engine* e, int32_t mode, double until_time, double max_time,
+                               uint64_t max_events_per_launch) {
+    if (!e) return set_err(K10S_E_INVALID, "null");
+    if (mode != K10S_RUN_UNTIL_ALL_FINISHED && mode != K10S_RUN_UNTIL_TIME) return set_err(K10S_E_INVALID, "bad mode");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipMemsetAsync(e->d_active, 0, 4, e->stream));
+    HIPCHK(k10s_launch_run(e->dsc, e->d_params, e->L, e->d_state, e->R, mode, until_time, max_time,
+                           max_events_per_launch, e->d_active, e->stream));
+    HIPCHK(hipMemcpyAsync(e->h_active, e->d_active, 4, hipMemcpyDeviceToHost, e->stream));
+    return K10S_OK;
+}
+
+int32_t k10s_engine_sync(k10s_engine* e) {
+    if (!e) return set_err(K10S_E_INVALID, "null");
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return K10S_OK;
+}
+
+int32_t k10s_engine_run(k10s_engine* e, int32_t mode, double until_time, double max_time,
+                        uint64_t max_events_per_launch, double* elapsed_ms) {
+    if (!e) return set_err(K10S_E_INVALID, "null");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipEventRecord(e->ev0, e->stream));
+    for (;;) {
+        int32_t rc = k10s_engine_step_async(e, mode, until_time, max_time, max_events_per_launch);
+        if (rc != K10S_OK) return rc;
+        HIPCHK(hipStreamSynchronize(e->stream));
+        if (max_events_per_launch == 0 || *e->h_active == 0) break;
+    }
+    HIPCHK(hipEventRecord(e->ev1, e->stream));
+    HIPCHK(hipEventSynchronize(e->ev1));
+    if (elapsed_ms) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
+        *elapsed_ms = ms;
+    }
+    return K10S_OK;
+}
+
+int32_t k10s_engine_results(const k10s_engine* e, k10s_replica_result* out) {
+    if (!e || !out) return set_err(K10S_E_INVALID, "null");
+    std::vector<RepHdr> hdr(e->R);
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipMemcpy2D(hdr.data(), sizeof(RepHdr), e->d_state + e->L.hdr, e->L.stride, sizeof(RepHdr), e->R,
+                       hipMemcpyDeviceToHost));
+    for (uint32_t r = 0; r < e->R; r++) hdr_to_result(hdr[r], out[r]);
+    return K10S_OK;
+}
+
+static int32_t read_hdr(const k10s_engine* e, uint32_t r, RepHdr& h) {
+    if (r >= e->R) return set_err(K10S_E_INVALID, "replica index out of range");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipMemcpy(&h, e->d_state + (size_t)r * e->L.stride + e->L.hdr, sizeof h, hipMemcpyDeviceToHost));
+    return K10S_OK;
+}
+
+int32_t k10s_engine_event_log(const k10s_engine* e, uint32_t r, k10s_log_entry* out, uint32_t cap, uint32_t* n) {
+    if (!e || !n) return set_err(K10S_E_INVALID, "null");
+    RepHdr h;
+    int32_t rc = read_hdr(e, r, h);
+    if (rc) return rc;
+    uint32_t k = e->L.cap_log ? (h.log_n < cap ? h.log_n : cap) : 0;
+    if (k) HIPCHK(hipMemcpy(out, e->d_state + (size_t)r * e->L.stride + e->L.log, sizeof(k10s_log_entry) * k,
+                            hipMemcpyDeviceToHost));
+    *n = k;
+    return K10S_OK;
+}
+
+int32_t k10s_engine_placements(const k10s_engine* e, uint32_t r, k10s_placement* out, uint32_t cap, uint32_t* n) {
+    if (!e || !n) return set_err(K10S_E_INVALID, "null");
+    RepHdr h;
+    int32_t rc = read_hdr(e, r, h);
+    if (rc) return rc;
+    uint32_t k = e->L.cap_place ? (h.place_n < cap ? h.place_n : cap) : 0;
+    if (k) HIPCHK(hipMemcpy(out, e->d_state + (size_t)r * e->L.stride + e->L.place, sizeof(k10s_placement) * k,
+                            hipMemcpyDeviceToHost));
+    *n = k;
+    return K10S_OK;
+}
+
+int32_t k10s_engine_pod_records(const k10s_engine* e, uint32_t r, k10s_pod_record* out, uint32_t cap, uint32_t* n) {
+    if (!e || !n) return set_err(K10S_E_INVALID, "null");
+    if (r >= e->R) return set_err(K10S_E_INVALID, "replica index out of range");
+    uint32_t k = e->L.rec_on ? (e->hs.n_pods < cap ? e->hs.n_pods : cap) : 0;
+    HIPCHK(hipSetDevice(e->device));
+    if (k) HIPCHK(hipMemcpy(out, e->d_state + (size_t)r * e->L.stride + e->L.prec, sizeof(k10s_pod_record) * k,
+                            hipMemcpyDeviceToHost));
+    *n = k;
+    return K10S_OK;
+}
+
+int32_t k10s_engine_group_sizes(const k10s_engine* e, uint32_t r, uint32_t* created, uint32_t* total, uint32_t cap,
+                                uint32_t* n) {
+    if (!e || !n) return set_err(K10S_E_INVALID, "null");
+    if (r >= e->R) return set_err(K10S_E_INVALID, "replica index out of range");
+    uint32_t G = (uint32_t)e->hs.group_names.size();
+    uint32_t k = G < cap ? G : cap;
+    std::vector<GroupState> gs(G);
+    HIPCHK(hipSetDevice(e->device));
+    if (G) HIPCHK(hipMemcpy(gs.data(), e->d_state + (size_t)r * e->L.stride + e->L.grp, sizeof(GroupState) * G,
+                            hipMemcpyDeviceToHost));
+    for (uint32_t g = 0; g < k; g++) {
+        created[g] = gs[g].registered ? gs[g].created_count : 0;
+        total[g] = gs[g].total_created;
+    }
+    *n = k;
+    return K10S_OK;
+}
+
+uint32_t k10s_engine_num_nodes(const k10s_engine* e) { return e ? e->hs.n_nodes : 0; }
+uint32_t k10s_engine_num_pods(const k10s_engine* e) { return e ? e->hs.n_pods : 0; }
+uint32_t k10s_engine_num_groups(const k10s_engine* e) { return e ? (uint32_t)e->hs.group_names.size() : 0; }
+const char* k10s_engine_node_name(const k10s_engine* e, uint32_t i) {
+    return (e && i < e->hs.n_nodes) ? e->hs.node_names[i].c_str() : "";
+}
+const char* k10s_engine_pod_name(const k10s_engine* e, uint32_t i) {
+    return (e && i < e->hs.n_pods) ? e->hs.pod_names[i].c_str() : "";
+}
+const char* k10s_engine_group_name(const k10s_engine* e, uint32_t i) {
+    return (e && i < e->hs.group_names.size()) ? e->hs.group_names[i].c_str() : "";
+}
+uint64_t k10s_engine_replica_bytes(const k10s_engine* e) { return e ? e->L.stride : 0; }
+
+}  // extern "C"

@@ -1,0 +1,88 @@
+// k10s_kernels.hip — gfx950 kernels of the batched-ensemble engine.
+//
+//   k10s_init_kernel      one 64-lane wavefront per replica: KubernetriksSimulation::initialize
+//   k10s_run_kernel       one 64-lane wavefront per replica: the dslab step loop with every
+//                         handler; the scheduling hot path (Fit + LeastAllocated + argmax over the
+//                         node cache) is lane-parallel, everything else wave-uniform
+//   k10s_schedule_kernel  unit-parity surface: R independent schedule_one calls, one wave each
+//
+// No MFMA: nothing on this path is a dense contraction.  Node state is SoA in HBM (12 B/node),
+// read coalesced (lane l reads node base+l), reductions by cross-lane shuffles (DPP/swizzle).
+// Built with -ffp-contract=off and without fast-math: the f64 score arithmetic must round exactly
+// like the Rust reference (correctly rounded division, no FMA contraction).
+#include <hip/hip_runtime.h>
+
+#include "k10s_engine.h"
+
+using namespace k10s;
+
+__global__ __launch_bounds__(64) void k10s_init_kernel(Scenario sc, const Params* __restrict__ params, Layout L,
+                                                         uint8_t* base, uint32_t n_replicas) {
+    uint32_t r = blockIdx.x;
+    if (r >= n_replicas) return;
+    Params p = params[r];
+    init_replica(&sc, &p, &L, base, r);
+}
+
+__global__ __launch_bounds__(64) void k10s_run_kernel(Scenario sc, const Params* __restrict__ params, Layout L,
+                                                        uint8_t* base, uint32_t n_replicas, int mode, double until_time,
+                                                        double max_time, uint64_t budget, uint32_t* active) {
+    uint32_t r = blockIdx.x;
+    if (r >= n_replicas) return;
+    Params p = params[r];
+    int more = run_replica(&sc, &p, &L, base, r, mode, until_time, max_time, budget);
+    if (more && threadIdx.x == 0) atomicAdd(active, 1u);
+}
+
+__global__ __launch_bounds__(64) void k10s_schedule_kernel(const uint32_t* __restrict__ alloc_cpu,
+                                                             const uint64_t* __restrict__ alloc_ram,
+                                                             const uint64_t* __restrict__ present, uint32_t n_nodes,
+                                                             uint32_t node_stride, const uint32_t* __restrict__ req_cpu,
+                                                             const uint64_t* __restrict__ req_ram, double weight,
+                                                             uint32_t n_problems, int32_t* out_node, int32_t* out_status) {
+    uint32_t r = blockIdx.x;
+    if (r >= n_problems) return;
+    const uint64_t off = (uint64_t)r * node_stride;
+    const uint32_t rc = req_cpu[r];
+    const uint64_t rr = req_ram[r];
+    int32_t chosen = -1;
+    int st;
+    uint32_t cnt = 0;
+    for (uint32_t w = threadIdx.x; w < (n_nodes + 63) / 64; w += 64) {
+        uint64_t bits = present[(off >> 6) + w];
+        if ((w + 1) * 64 > n_nodes) bits &= (n_nodes & 63) ? ((1ull << (n_nodes & 63)) - 1) : ~0ull;
+        cnt += (uint32_t)__popcll(bits);
+    }
+    cnt = wave_sum_u32(cnt);
+    if (rc == 0 && rr == 0) st = K10S_SCHED_REQUESTED_RESOURCES_ARE_ZEROS;
+    else if (cnt == 0) st = K10S_SCHED_NO_NODES_IN_CLUSTER;
+    else st = schedule_scan(alloc_cpu + off, alloc_ram + off, present + (off >> 6), n_nodes, rc, rr, weight, &chosen);
+    if (threadIdx.x == 0) {
+        out_status[r] = st;
+        out_node[r] = st == K10S_SCHED_OK ? chosen : -1;
+    }
+}
+
+// ---- launchers (called from k10s_host.cpp) -------------------------------------------------------
+hipError_t k10s_launch_init(const Scenario& sc, const Params* d_params, const Layout& L, uint8_t* d_state,
+                            uint32_t n_replicas, hipStream_t s) {
+    hipLaunchKernelGGL(k10s_init_kernel, dim3(n_replicas), dim3(64), 0, s, sc, d_params, L, d_state, n_replicas);
+    return hipGetLastError();
+}
+
+hipError_t k10s_launch_run(const Scenario& sc, const Params* d_params, const Layout& L, uint8_t* d_state,
+                           uint32_t n_replicas, int mode, double until_time, double max_time, uint64_t budget,
+                           uint32_t* d_active, hipStream_t s) {
+    hipLaunchKernelGGL(k10s_run_kernel, dim3(n_replicas), dim3(64), 0, s, sc, d_params, L, d_state, n_replicas, mode,
+                       until_time, max_time, budget, d_active);
+    return hipGetLastError();
+}
+
+hipError_t k10s_launch_schedule(const uint32_t* alloc_cpu, const uint64_t* alloc_ram, const uint64_t* present,
+                                uint32_t n_nodes, uint32_t node_stride, const uint32_t* req_cpu, const uint64_t* req_ram,
+                                double weight, uint32_t n_problems, int32_t* out_node, int32_t* out_status,
+                                hipStream_t s) {
+    hipLaunchKernelGGL(k10s_schedule_kernel, dim3(n_problems), dim3(64), 0, s, alloc_cpu, alloc_ram, present, n_nodes,
+                       node_stride, req_cpu, req_ram, weight, n_problems, out_node, out_status);
+    return hipGetLastError();
+}

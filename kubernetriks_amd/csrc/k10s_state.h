@@ -1,0 +1,296 @@
+// k10s_state.h — device-resident layout of a compiled scenario and of per-replica state.
+//
+// Scenario tables (read-only, shared by every replica on a GPU) are indexed by name rank:
+// node index n = rank of the node's name among all node names, pod index p = rank of the pod's
+// name among all pod names (byte order, == Rust String order).  So "iterate n ascending" is the
+// BTreeMap<String, Node> order the reference's scheduler scans, and "iterate p ascending" is the
+// BTreeSet<String> order of its pod sets.  A unified rank u covers node and pod names together
+// (the api server keeps pod names in its node-removal set, api_server.rs:343).
+//
+// Per-replica state is one contiguous region per replica (stride = Layout::stride), SoA inside:
+// the scheduler cache (s_cpu u32[N], s_ram u64[N], s_present bit[N]) is the hot scan target,
+// 12 B/node + 1 bit, read coalesced by the 64 lanes of the replica's wavefront.
+#pragma once
+
+#include "../../include/k10s.h"
+#include "../../include/k10s_events.h"
+#include "k10s_common.h"
+
+namespace k10s {
+
+struct TraceEv {          // one client-emitted trace event (simulator.rs:234-253)
+    double time;
+    uint32_t seq;         // dslab event id: 2 + position in (cluster trace ++ workload trace)
+    uint32_t kind;        // K10S_EV_AS_* kind delivered to the api server
+    uint32_t arg;         // node def / node idx / pod idx / group idx
+    uint32_t pad;
+};
+
+enum : uint8_t {
+    POD_HAS_DEF = 1,      // created by the trace or a pod group (else: only named by remove_pod)
+    POD_HAS_DUR = 2,      // running_duration is Some
+    POD_PERTURB = 4,      // trace pod: subject to seed perturbation
+};
+enum : uint8_t { GF_HAS_TCPU = 1, GF_HAS_TRAM = 2, GF_TMPL_HAS_DUR = 4 };
+enum : uint8_t { MODEL_NONE = 0, MODEL_CONSTANT = 1, MODEL_POD_GROUP = 2 };
+
+struct Scenario {
+    uint32_t n_nodes, n_pods, n_uids, n_defs, n_slots, n_pool, n_default, n_trace;
+    uint32_t n_groups, n_ca_groups, group_bound, ca_bound, n_units;
+    uint32_t ca_enabled, hpa_enabled;
+    uint32_t first_dynamic_seq;
+    uint64_t total_pods_in_trace, total_nodes_in_trace;
+
+    const uint32_t* node_uid;      // [N]
+    const uint32_t* def_node;      // [D] node idx of node instance def
+    const uint32_t* def_cpu;       // [D] capacity
+    const uint64_t* def_ram;
+    const int32_t* def_ca_group;   // [D] "node_group" label -> CA group idx (-1 none, -2 unknown)
+    const uint8_t* def_ca_origin;  // [D] label origin == "cluster autoscaler"
+    const uint32_t* pod_uid;       // [P]
+    const uint32_t* pod_cpu;       // [P] requests
+    const uint64_t* pod_ram;
+    const double* pod_dur;
+    const uint8_t* pod_flags;
+    const int32_t* pod_group;      // [P] pod group idx or -1
+    const uint32_t* pod_key;       // [P] perturbation key (workload-trace position)
+    const uint32_t* default_defs;  // [n_default] defs of default-cluster nodes, slot order
+    const TraceEv* trace;          // [n_trace] merged (time, seq) order
+
+    // pod groups (name order)
+    const uint32_t* g_initial;
+    const uint32_t* g_max;
+    const uint32_t* g_cpu;
+    const uint64_t* g_ram;
+    const uint8_t* g_flags;
+    const double* g_tcpu;
+    const double* g_tram;
+    const uint8_t* g_cpu_kind;
+    const uint8_t* g_ram_kind;
+    const double* g_cpu_usage;
+    const double* g_ram_usage;
+    const uint32_t* g_cpu_uoff;
+    const uint32_t* g_cpu_ucnt;
+    const uint32_t* g_ram_uoff;
+    const uint32_t* g_ram_ucnt;
+    const uint32_t* g_pod;         // [G*group_bound] pod idx of "{g}_{k}"
+    const uint32_t* g_pos;         // [G*group_bound] name-order position of k within the group
+    const uint32_t* g_sorted_k;    // [G*group_bound] k at name-order position j
+    const double* unit_dur;
+    const double* unit_load;
+
+    // cluster-autoscaler node groups (name order; cluster_autoscaler.rs:175-200)
+    const uint8_t* ca_has_max;
+    const uint64_t* ca_max;
+    const uint32_t* ca_def;        // [CG*ca_bound] def of "{group}_{k}", k = 1..ca_bound
+    const uint32_t* ca_cpu;
+    const uint64_t* ca_ram;
+};
+
+// Replica parameters as consumed by the device (k10s_replica_params with derived fields).
+typedef k10s_replica_params Params;
+
+struct Estimator {          // `average` 0.15 concatenate!(Min, Max, Mean, Variance)
+    uint64_t n;
+    double mn, mx, avg, sum2;
+};
+K10S_HD void est_reset(Estimator& e) {
+    e.n = 0;
+    e.mn = __builtin_inf();
+    e.mx = -__builtin_inf();
+    e.avg = 0.0;
+    e.sum2 = 0.0;
+}
+K10S_HD void est_add(Estimator& e, double x) {
+    e.mn = fmin_rs(e.mn, x);
+    e.mx = fmax_rs(e.mx, x);
+    e.n += 1;
+    double nf = (double)e.n;
+    double delta_n = (x - e.avg) / nf;
+    e.avg += delta_n;
+    e.sum2 += delta_n * delta_n * nf * (nf - 1.0);
+}
+
+struct RepHdr {
+    double clock;
+    uint32_t next_seq;
+    uint32_t trace_cursor;
+    uint32_t heap_size;
+    uint32_t aq_size;
+    uint32_t uq_size;
+    uint32_t s_node_count;
+    uint32_t ps_node_count;
+    uint32_t as_node_count;
+    uint32_t pool_head;
+    uint32_t pool_count;
+    uint32_t status;
+    uint32_t error_code;
+    uint32_t error_kind;
+    uint32_t error_seq;
+    double error_time;
+    uint64_t counters[K10S_NUM_COUNTERS];
+    Estimator est[3];
+    double ca_last_cycle_time;
+    uint32_t ca_n_act;
+    uint32_t log_n;
+    uint32_t place_n;
+    uint32_t flags;
+    uint32_t unsched_cache_count;
+    uint32_t pad[3];
+};
+
+struct HeapEv {             // dslab Event {id, time, dst, data}, 32 B
+    double time;
+    uint32_t seq;
+    uint16_t kind;
+    int16_t slot;           // node component for N_* kinds
+    uint32_t a;             // pod idx / node idx / group idx
+    uint32_t b;             // node idx / def id / alloc cpu / flags
+    double x;               // event time field (assign/finish/removal/add/start) or alloc ram bits
+};
+
+struct QInfo {              // QueuedPodInfo (queue.rs:13-27), 24 B
+    double timestamp;
+    double initial;
+    uint32_t attempts;
+    uint32_t pod;
+};
+
+struct GroupState {         // HPA PodGroupInfo + metrics/usage-model state of one pod group
+    double creation_time;
+    double util_cpu, util_ram;        // last pod-metrics tick (collector.rs:263-337)
+    double cpu_last_start, ram_last_start;   // PodGroupResourceUsageModel step state
+    uint32_t cpu_idx, ram_idx;
+    uint32_t registered;              // HPA received RegisterPodGroup
+    uint32_t created_count;           // created_pods.len()
+    uint32_t total_created;
+    uint32_t running;                 // running pods of this group on created nodes
+    uint32_t has_metric;              // pod_utilization_metrics contains the group
+    uint32_t created_at_as;           // AS handled the CreatePodGroupRequest
+};
+
+struct CAAct {
+    uint32_t up;            // 1 = ScaleUp(node def), 0 = ScaleDown(node)
+    uint32_t arg;           // def id (up) / node idx (down)
+};
+
+enum : uint8_t { NF_S_ASSIGN = 1, NF_PS_PRESENT = 2 };
+enum : uint8_t { PF_IN_S = 1, PF_IN_PS = 2, PF_UNSCHED = 4 };
+
+// Offsets (bytes) of per-replica arrays within one replica's region.
+struct Layout {
+    uint64_t stride;
+    uint64_t hdr;
+    uint64_t s_cpu, s_ram, s_present, node_flags, ps_cpu, ps_ram, ps_def, ps_epoch, as_slot, pend_def;
+    uint64_t pend_rm;
+    uint64_t preq_cpu, preq_ram, pdur, pflags, s_assigned, ps_assigned, ps_aepoch, run_slot, run_prev,
+        run_next, finish_seq, cancel_slot, cancel_gen, prec;
+    uint64_t slot_node, slot_def, slot_removed, slot_rtime, slot_gen, slot_head, pool_ring;
+    uint64_t grp, grp_bits;
+    uint64_t cag, ca_act, ca_cpu, ca_ram, ca_undo;
+    uint64_t heap, aq, uq, log, place;
+    uint32_t cap_heap, cap_aq, cap_uq, cap_act, cap_log, cap_place, cap_undo, rec_on;
+    uint32_t words_nodes, words_uids, words_group;
+    uint32_t pad;
+};
+
+struct Rep {                // typed view of one replica's region
+    RepHdr* h;
+    uint32_t* s_cpu;
+    uint64_t* s_ram;
+    uint64_t* s_present;
+    uint8_t* node_flags;
+    uint32_t* ps_cpu;
+    uint64_t* ps_ram;
+    uint32_t* ps_def;
+    uint32_t* ps_epoch;
+    int32_t* as_slot;
+    int32_t* pend_def;
+    uint64_t* pend_rm;
+    uint32_t* preq_cpu;
+    uint64_t* preq_ram;
+    double* pdur;
+    uint8_t* pflags;
+    int32_t* s_assigned;
+    int32_t* ps_assigned;
+    uint32_t* ps_aepoch;
+    int32_t* run_slot;
+    int32_t* run_prev;
+    int32_t* run_next;
+    uint32_t* finish_seq;
+    int32_t* cancel_slot;
+    uint32_t* cancel_gen;
+    k10s_pod_record* prec;
+    int32_t* slot_node;
+    uint32_t* slot_def;
+    uint8_t* slot_removed;
+    double* slot_rtime;
+    uint32_t* slot_gen;
+    int32_t* slot_head;
+    uint32_t* pool_ring;
+    GroupState* grp;
+    uint64_t* grp_bits;
+    uint32_t* cag;          // [CG*2]: current_count, total_allocated
+    CAAct* ca_act;
+    uint32_t* ca_cpu;
+    uint64_t* ca_ram;
+    uint32_t* ca_undo;      // node indices modified during one all_pods_can_be_moved attempt
+    HeapEv* heap;
+    QInfo* aq;
+    QInfo* uq;
+    k10s_log_entry* log;
+    k10s_placement* place;
+};
+
+K10S_HD Rep make_rep(uint8_t* base, const Layout& L, uint32_t r) {
+    uint8_t* b = base + (uint64_t)r * L.stride;
+    Rep v;
+    v.h = (RepHdr*)(b + L.hdr);
+    v.s_cpu = (uint32_t*)(b + L.s_cpu);
+    v.s_ram = (uint64_t*)(b + L.s_ram);
+    v.s_present = (uint64_t*)(b + L.s_present);
+    v.node_flags = (uint8_t*)(b + L.node_flags);
+    v.ps_cpu = (uint32_t*)(b + L.ps_cpu);
+    v.ps_ram = (uint64_t*)(b + L.ps_ram);
+    v.ps_def = (uint32_t*)(b + L.ps_def);
+    v.ps_epoch = (uint32_t*)(b + L.ps_epoch);
+    v.as_slot = (int32_t*)(b + L.as_slot);
+    v.pend_def = (int32_t*)(b + L.pend_def);
+    v.pend_rm = (uint64_t*)(b + L.pend_rm);
+    v.preq_cpu = (uint32_t*)(b + L.preq_cpu);
+    v.preq_ram = (uint64_t*)(b + L.preq_ram);
+    v.pdur = (double*)(b + L.pdur);
+    v.pflags = (uint8_t*)(b + L.pflags);
+    v.s_assigned = (int32_t*)(b + L.s_assigned);
+    v.ps_assigned = (int32_t*)(b + L.ps_assigned);
+    v.ps_aepoch = (uint32_t*)(b + L.ps_aepoch);
+    v.run_slot = (int32_t*)(b + L.run_slot);
+    v.run_prev = (int32_t*)(b + L.run_prev);
+    v.run_next = (int32_t*)(b + L.run_next);
+    v.finish_seq = (uint32_t*)(b + L.finish_seq);
+    v.cancel_slot = (int32_t*)(b + L.cancel_slot);
+    v.cancel_gen = (uint32_t*)(b + L.cancel_gen);
+    v.prec = L.rec_on ? (k10s_pod_record*)(b + L.prec) : nullptr;
+    v.slot_node = (int32_t*)(b + L.slot_node);
+    v.slot_def = (uint32_t*)(b + L.slot_def);
+    v.slot_removed = (uint8_t*)(b + L.slot_removed);
+    v.slot_rtime = (double*)(b + L.slot_rtime);
+    v.slot_gen = (uint32_t*)(b + L.slot_gen);
+    v.slot_head = (int32_t*)(b + L.slot_head);
+    v.pool_ring = (uint32_t*)(b + L.pool_ring);
+    v.grp = (GroupState*)(b + L.grp);
+    v.grp_bits = (uint64_t*)(b + L.grp_bits);
+    v.cag = (uint32_t*)(b + L.cag);
+    v.ca_act = (CAAct*)(b + L.ca_act);
+    v.ca_cpu = (uint32_t*)(b + L.ca_cpu);
+    v.ca_ram = (uint64_t*)(b + L.ca_ram);
+    v.ca_undo = (uint32_t*)(b + L.ca_undo);
+    v.heap = (HeapEv*)(b + L.heap);
+    v.aq = (QInfo*)(b + L.aq);
+    v.uq = (QInfo*)(b + L.uq);
+    v.log = L.cap_log ? (k10s_log_entry*)(b + L.log) : nullptr;
+    v.place = L.cap_place ? (k10s_placement*)(b + L.place) : nullptr;
+    return v;
+}
+
+}  // namespace k10s

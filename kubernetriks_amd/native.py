@@ -1,0 +1,288 @@
+"""ctypes binding of the engine's C ABI (include/k10s.h) — the Python mirror of the reference's
+KubernetriksSimulation surface for the batched-ensemble engine.
+
+The shared library is built in-tree (``build/libk10s.so``, see ``kubernetriks_amd/build.py``).
+There is no CPU fallback: without the library or without a GPU every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+from typing import Dict, List, Optional, Sequence
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(REPO, "build", "libk10s.so")
+
+NUM_COUNTERS = 16
+COUNTER_NAMES = [
+    "total_nodes_in_trace", "total_pods_in_trace", "pods_succeeded", "pods_unschedulable", "pods_failed",
+    "pods_removed", "total_scaled_up_nodes", "total_scaled_down_nodes", "total_scaled_up_pods",
+    "total_scaled_down_pods", "processed_nodes", "terminated_pods", "placements", "attempts", "events",
+    "nodes_scanned",
+]
+EST_NAMES = ["pod_duration", "pod_schedule_time", "pod_queue_time"]
+
+RUN_UNTIL_ALL_FINISHED = 0
+RUN_UNTIL_TIME = 1
+
+STATUS = {0: "running", 1: "finished", 2: "error", 3: "time_limit"}
+
+
+class Estimator(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint64), ("min", ctypes.c_double), ("max", ctypes.c_double),
+                ("mean", ctypes.c_double), ("sum2", ctypes.c_double)]
+
+
+class ReplicaResult(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_uint32), ("error_code", ctypes.c_uint32), ("error_kind", ctypes.c_uint32),
+                ("error_seq", ctypes.c_uint32), ("error_time", ctypes.c_double), ("clock", ctypes.c_double),
+                ("counters", ctypes.c_uint64 * NUM_COUNTERS), ("est", Estimator * 3),
+                ("unschedulable_len", ctypes.c_uint32), ("active_len", ctypes.c_uint32),
+                ("node_count_as", ctypes.c_uint32), ("node_count_ps", ctypes.c_uint32),
+                ("node_count_s", ctypes.c_uint32), ("log_len", ctypes.c_uint32),
+                ("placements_len", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+class ReplicaParams(ctypes.Structure):
+    _fields_ = [("scheduling_cycle_interval", ctypes.c_double),
+                ("as_to_ps_network_delay", ctypes.c_double), ("ps_to_sched_network_delay", ctypes.c_double),
+                ("sched_to_as_network_delay", ctypes.c_double), ("as_to_node_network_delay", ctypes.c_double),
+                ("as_to_ca_network_delay", ctypes.c_double), ("as_to_hpa_network_delay", ctypes.c_double),
+                ("ca_scan_interval", ctypes.c_double), ("ca_scale_down_utilization_threshold", ctypes.c_double),
+                ("hpa_scan_interval", ctypes.c_double), ("hpa_target_threshold_tolerance", ctypes.c_double),
+                ("score_weight", ctypes.c_double),
+                ("enable_unscheduled_pods_conditional_move", ctypes.c_uint32), ("perturb", ctypes.c_uint32),
+                ("seed", ctypes.c_uint64), ("ca_max_node_count", ctypes.c_uint64)]
+
+
+class Capacities(ctypes.Structure):
+    _fields_ = [("event_heap", ctypes.c_uint32), ("active_queue", ctypes.c_uint32),
+                ("unschedulable", ctypes.c_uint32), ("group_name_bound", ctypes.c_uint32),
+                ("ca_name_bound", ctypes.c_uint32), ("event_log", ctypes.c_uint32),
+                ("placement_log", ctypes.c_uint32), ("pod_records", ctypes.c_uint32)]
+
+
+class LogEntry(ctypes.Structure):
+    _fields_ = [("time", ctypes.c_double), ("seq", ctypes.c_uint32), ("kind", ctypes.c_uint16),
+                ("slot", ctypes.c_int16), ("pod", ctypes.c_int32), ("node", ctypes.c_int32)]
+
+
+class Placement(ctypes.Structure):
+    _fields_ = [("assign_time", ctypes.c_double), ("pod", ctypes.c_int32), ("node", ctypes.c_int32)]
+
+
+class PodRecord(ctypes.Structure):
+    _fields_ = [("t_running", ctypes.c_double), ("t_finished", ctypes.c_double), ("t_removed", ctypes.c_double),
+                ("state", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+
+
+def result_to_dict(r: ReplicaResult) -> dict:
+    return {
+        "status": STATUS.get(r.status, r.status), "error_code": r.error_code, "error_kind": r.error_kind,
+        "error_seq": r.error_seq, "error_time": r.error_time, "time": r.clock,
+        "counters": {COUNTER_NAMES[i]: int(r.counters[i]) for i in range(NUM_COUNTERS)},
+        "estimators": {EST_NAMES[i]: [int(r.est[i].n), r.est[i].min, r.est[i].max, r.est[i].mean,
+                                      (r.est[i].sum2 / r.est[i].n) if r.est[i].n else math.nan]
+                       for i in range(3)},
+        "unschedulable_len": r.unschedulable_len, "active_len": r.active_len,
+        "node_counts": [r.node_count_as, r.node_count_ps, r.node_count_s],
+        "log_len": r.log_len, "placements_len": r.placements_len, "flags": r.flags,
+    }
+
+
+def _decl(L, prefix: str):
+    """Declare the engine-surface signatures shared by the product library and the test build."""
+    vp, u32, u64, i32, dbl = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32, ctypes.c_double
+    P = ctypes.POINTER
+    sig = {
+        "results": (i32, [vp, P(ReplicaResult)]),
+        "event_log": (i32, [vp, u32, P(LogEntry), u32, P(u32)]),
+        "placements": (i32, [vp, u32, P(Placement), u32, P(u32)]),
+        "pod_records": (i32, [vp, u32, P(PodRecord), u32, P(u32)]),
+        "group_sizes": (i32, [vp, u32, P(u32), P(u32), u32, P(u32)]),
+        "num_nodes": (u32, [vp]), "num_pods": (u32, [vp]), "num_groups": (u32, [vp]),
+        "node_name": (ctypes.c_char_p, [vp, u32]), "pod_name": (ctypes.c_char_p, [vp, u32]),
+        "group_name": (ctypes.c_char_p, [vp, u32]), "replica_bytes": (u64, [vp]),
+        "default_params": (i32, [vp, P(ReplicaParams)]),
+    }
+    out = {}
+    for name, (res, args) in sig.items():
+        f = getattr(L, prefix + name)
+        f.restype = res
+        f.argtypes = args
+        out[name] = f
+    return out
+
+
+class EngineBase:
+    """Common result accessors (names resolved through the compiled scenario's rank tables)."""
+
+    _fn: dict
+    _h: int
+    n_replicas: int
+
+    def _names(self):
+        if not hasattr(self, "_node_names"):
+            f = self._fn
+            self._node_names = [f["node_name"](self._h, i).decode() for i in range(f["num_nodes"](self._h))]
+            self._pod_names = [f["pod_name"](self._h, i).decode() for i in range(f["num_pods"](self._h))]
+            self._group_names = [f["group_name"](self._h, i).decode() for i in range(f["num_groups"](self._h))]
+        return self._node_names, self._pod_names, self._group_names
+
+    @property
+    def node_names(self) -> List[str]:
+        return self._names()[0]
+
+    @property
+    def pod_names(self) -> List[str]:
+        return self._names()[1]
+
+    @property
+    def group_names(self) -> List[str]:
+        return self._names()[2]
+
+    def default_params(self) -> ReplicaParams:
+        p = ReplicaParams()
+        self._check(self._fn["default_params"](self._h, ctypes.byref(p)))
+        return p
+
+    def raw_results(self):
+        arr = (ReplicaResult * self.n_replicas)()
+        self._check(self._fn["results"](self._h, arr))
+        return arr
+
+    def results(self) -> List[dict]:
+        return [result_to_dict(r) for r in self.raw_results()]
+
+    def event_log(self, r: int, cap: int = 1 << 22) -> List[tuple]:
+        buf = (LogEntry * cap)()
+        n = ctypes.c_uint32()
+        self._check(self._fn["event_log"](self._h, r, buf, cap, ctypes.byref(n)))
+        nn, pn, _ = self._names()
+        return [(e.seq, e.time, e.kind, pn[e.pod] if e.pod >= 0 else "", nn[e.node] if e.node >= 0 else "", e.slot)
+                for e in buf[: n.value]]
+
+    def placements(self, r: int, cap: int = 1 << 22) -> List[tuple]:
+        buf = (Placement * cap)()
+        n = ctypes.c_uint32()
+        self._check(self._fn["placements"](self._h, r, buf, cap, ctypes.byref(n)))
+        nn, pn, _ = self._names()
+        return [(pn[x.pod], nn[x.node], x.assign_time) for x in buf[: n.value]]
+
+    def pod_records(self, r: int) -> Dict[str, tuple]:
+        cap = self._fn["num_pods"](self._h)
+        buf = (PodRecord * max(cap, 1))()
+        n = ctypes.c_uint32()
+        self._check(self._fn["pod_records"](self._h, r, buf, cap, ctypes.byref(n)))
+        _, pn, _ = self._names()
+        return {pn[i]: (buf[i].t_running, buf[i].t_finished, buf[i].t_removed, buf[i].state)
+                for i in range(n.value) if buf[i].state != 0}
+
+    def group_sizes(self, r: int) -> Dict[str, tuple]:
+        G = self._fn["num_groups"](self._h)
+        c = (ctypes.c_uint32 * max(G, 1))()
+        t = (ctypes.c_uint32 * max(G, 1))()
+        n = ctypes.c_uint32()
+        self._check(self._fn["group_sizes"](self._h, r, c, t, G, ctypes.byref(n)))
+        _, _, gn = self._names()
+        return {gn[i]: (c[i], t[i]) for i in range(n.value)}
+
+    @property
+    def replica_bytes(self) -> int:
+        return int(self._fn["replica_bytes"](self._h))
+
+    def _check(self, rc):
+        if rc != 0:
+            raise RuntimeError(f"engine call failed with {rc}: {self._last_error()}")
+
+    def _last_error(self) -> str:
+        return ""
+
+
+_lib = None
+
+
+def lib():
+    """Load build/libk10s.so (the HIP engine).  Raises if it is missing: no fallback."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        L.k10s_last_error.restype = ctypes.c_char_p
+        L.k10s_version.restype = ctypes.c_char_p
+        L.k10s_engine_create.restype = ctypes.c_void_p
+        L.k10s_engine_create.argtypes = [ctypes.c_char_p, ctypes.POINTER(ReplicaParams), ctypes.c_uint32,
+                                         ctypes.POINTER(Capacities), ctypes.c_int32]
+        L.k10s_engine_destroy.argtypes = [ctypes.c_void_p]
+        L.k10s_engine_reset.argtypes = [ctypes.c_void_p]
+        L.k10s_engine_reset.restype = ctypes.c_int32
+        L.k10s_engine_run.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
+                                      ctypes.c_uint64, ctypes.POINTER(ctypes.c_double)]
+        L.k10s_engine_run.restype = ctypes.c_int32
+        L.k10s_engine_step_async.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
+                                             ctypes.c_uint64]
+        L.k10s_engine_step_async.restype = ctypes.c_int32
+        L.k10s_engine_sync.argtypes = [ctypes.c_void_p]
+        L.k10s_engine_sync.restype = ctypes.c_int32
+        L.k10s_schedule_one_batch.restype = ctypes.c_int32
+        L.k10s_schedule_one_batch.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint32, ctypes.c_uint32] + \
+            [ctypes.c_void_p] * 2 + [ctypes.c_double, ctypes.c_uint32] + [ctypes.c_void_p] * 3
+        _lib = L
+    return _lib
+
+
+class Engine(EngineBase):
+    """A batch of independent kubernetriks replicas on one MI355X (one wavefront per replica)."""
+
+    def __init__(self, scenario: str, n_replicas: int, params: Optional[Sequence[ReplicaParams]] = None,
+                 caps: Optional[Capacities] = None, device: int = 0):
+        L = lib()
+        self._L = L
+        self._fn = _decl(L, "k10s_engine_")
+        self.n_replicas = n_replicas
+        parr = None
+        if params is not None:
+            parr = (ReplicaParams * n_replicas)(*params)
+        h = L.k10s_engine_create(scenario.encode(), parr, n_replicas, ctypes.byref(caps) if caps else None, device)
+        if not h:
+            raise RuntimeError("k10s_engine_create failed: " + L.k10s_last_error().decode())
+        self._h = h
+
+    def _last_error(self) -> str:
+        return self._L.k10s_last_error().decode()
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.k10s_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def reset(self):
+        self._check(self._L.k10s_engine_reset(self._h))
+
+    def run(self, mode: int = RUN_UNTIL_ALL_FINISHED, until_time: float = 0.0, max_time: float = 1e12,
+            max_events_per_launch: int = 0) -> float:
+        ms = ctypes.c_double()
+        self._check(self._L.k10s_engine_run(self._h, mode, until_time, max_time, max_events_per_launch,
+                                            ctypes.byref(ms)))
+        return ms.value
+
+    def run_until_all_finished(self, max_time: float = 1e12, max_events_per_launch: int = 0) -> float:
+        return self.run(RUN_UNTIL_ALL_FINISHED, 0.0, max_time, max_events_per_launch)
+
+    def step_until_time(self, t: float, max_events_per_launch: int = 0) -> float:
+        return self.run(RUN_UNTIL_TIME, t, 1e300, max_events_per_launch)
+
+    def step_async(self, mode: int, until_time: float, max_time: float, budget: int):
+        self._check(self._L.k10s_engine_step_async(self._h, mode, until_time, max_time, budget))
+
+    def sync(self):
+        self._check(self._L.k10s_engine_sync(self._h))
+
+
+def version() -> str:
+    return lib().k10s_version().decode()

@@ -1,0 +1,224 @@
+"""Synthetic workloads for the BASELINE.json configs (data: synthetic; no network, no trace CSVs).
+
+C1  config.yaml + bundled generic example trace, 1 replica            -> c1_scenario()
+C2  31-node default cluster (config.yaml:45-68), seed-perturbed        -> c2_scenario()
+C3  4,096 Alibaba-like nodes, Alibaba-like pods, integer arrivals      -> c3_scenario()
+C4  HPA pod groups + cluster-autoscaler node groups                    -> c4_scenario()
+C5  C3-shaped replicas with a scheduler/autoscaler parameter sweep     -> c5_params()
+
+Per-replica variation ("seed-perturbed traces") is applied on the device by the engine's init
+kernel (k10s_engine.h: perturb_pod) when k10s_replica_params.perturb = 1: each trace pod's
+duration is scaled by k/16 (k in 8..24) and its cpu/ram requests by k/16 (k in 12..20), with k drawn
+from splitmix64(seed, pod's workload-trace position).  `perturb_workload` restates that function
+bit-exactly so a replica's trace can be materialized for the CPU oracle.
+
+Alibaba-like statistics are the ones the reference's notebook prints
+(experiments/alibaba_demo.ipynb cells 1 and 3).
+"""
+from __future__ import annotations
+
+import math
+import random
+from typing import List, Optional
+
+from .scenario import (CANodeGroup, DefaultNodeGroup, GenericClusterTrace, GenericWorkloadTrace, Node, Pod,
+                       PodGroup, SimulationConfig, UsageModel, WorkloadEvent, scenario_text)
+
+M64 = (1 << 64) - 1
+
+
+def splitmix64(x: int) -> int:
+    x = (x + 0x9E3779B97F4A7C15) & M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & M64
+    return x ^ (x >> 31)
+
+
+def perturb_pod(seed: int, key: int, cpu: int, ram: int, dur: Optional[float]):
+    """Bit-exact restatement of k10s_engine.h perturb_pod."""
+    u = splitmix64(seed ^ ((0xD1B54A32D192ED03 * (key + 1)) & M64))
+    kd = 8 + u % 17
+    kc = 12 + (u >> 20) % 9
+    kr = 12 + (u >> 40) % 9
+    if dur is not None:
+        dur = (dur * float(kd)) * 0.0625
+    cpu = ((cpu * kc) >> 4) & 0xFFFFFFFF
+    ram = ((ram >> 4) * kr) & M64
+    return cpu, ram, dur
+
+
+def perturb_workload(workload: GenericWorkloadTrace, seed: int) -> GenericWorkloadTrace:
+    out = GenericWorkloadTrace()
+    for pos, e in enumerate(workload.events):
+        if e.kind == "create_pod":
+            cpu, ram, dur = perturb_pod(seed, pos, e.pod.cpu, e.pod.ram, e.pod.duration)
+            out.events.append(WorkloadEvent(e.timestamp, "create_pod",
+                                            pod=Pod(e.pod.name, cpu, ram, dur, dict(e.pod.labels))))
+        else:
+            out.events.append(e)
+    return out
+
+
+# ----------------------------------------------------------------------------------------------
+def c1_scenario() -> str:
+    """src/config.yaml with the bundled generic trace (generic_{cluster,workload}_trace_example.yaml)."""
+    cfg = SimulationConfig()
+    c = GenericClusterTrace()
+    lab = {"storage_type": "ssd", "proc_type": "intel"}
+    c.create_node(1, Node("node_21", 16000, 17179869184, dict(lab)))
+    c.remove_node(600, "node_21")
+    c.create_node(601, Node("node_22", 16000, 17179869184, dict(lab)))
+    w = GenericWorkloadTrace()
+    for ts, name, dur in ((550, "pod_16", 21.0), (551, "pod_25", 76.0), (552, "pod_42", 4.0), (553, "pod_101", 4221.0)):
+        w.create_pod(ts, Pod(name, 4000, 8589934592, dur))
+    w.remove_pod(5001, "pod_42")
+    return scenario_text(cfg, c, w)
+
+
+def default_cluster_31() -> List[DefaultNodeGroup]:
+    """The (commented) default cluster of src/config.yaml:45-68."""
+    return [DefaultNodeGroup(None, Node("super_node_1024cpu_512gb", 1024000, 549755813888)),
+            DefaultNodeGroup(10, Node("default_128cpu_256gb_node", 128000, 274877906944)),
+            DefaultNodeGroup(20, Node("default_64cpu_128gb_node", 64000, 137438953472))]
+
+
+def c2_workload(n_pods: int = 2000, seed: int = 123, horizon: float = 5000.0) -> GenericWorkloadTrace:
+    """Pod distribution of tests/test_determinism.rs:49-68 (cpu ceil(U*1000) mcpu, ram U*1e10 B,
+    duration U*1000 s), with arrivals over `horizon` seconds."""
+    rng = random.Random(seed)
+    w = GenericWorkloadTrace()
+    for i in range(n_pods):
+        w.create_pod(rng.random() * horizon,
+                     Pod(f"pod_{i}", int(math.ceil(rng.random() * 1000.0)), int(rng.random() * 10000000000.0),
+                         rng.random() * 1000.0))
+    return w
+
+
+def c2_scenario(n_pods: int = 2000, seed: int = 123) -> str:
+    cfg = SimulationConfig()
+    cfg.default_cluster = default_cluster_31()
+    return scenario_text(cfg, GenericClusterTrace(), c2_workload(n_pods, seed))
+
+
+# ---- Alibaba-like (C3) ------------------------------------------------------------------------
+ALIBABA_NODE_MEM = 0.6899697150104833   # modal machine memory (cluster.rs test fixture / notebook)
+GIB128 = 128 * 1024 * 1024 * 1024
+
+
+def _machine_mem(rng: random.Random) -> float:
+    # notebook: 1313 machines, mean 0.692729, sd 0.029690, min 0.574788, quartiles ~0.68997, max 1.0
+    r = rng.random()
+    if r < 0.85:
+        return ALIBABA_NODE_MEM
+    if r < 0.93:
+        return 0.690001
+    if r < 0.97:
+        return rng.uniform(0.574788, 0.68997)
+    return rng.uniform(0.69, 1.0)
+
+
+def _task_mem(rng: random.Random) -> float:
+    # notebook quantiles of normalized memory request: min 0.003815, 25% 0.004110, 50% 0.007941,
+    # 75% 0.009334, max 0.127332
+    r = rng.random()
+    if r < 0.25:
+        return rng.uniform(0.003815, 0.004110)
+    if r < 0.5:
+        return rng.uniform(0.004110, 0.007941)
+    if r < 0.75:
+        return rng.uniform(0.007941, 0.009334)
+    if r < 0.99:
+        return rng.uniform(0.009334, 0.02)
+    return rng.uniform(0.02, 0.127332)
+
+
+def _task_cpu(rng: random.Random) -> int:
+    # santicores per instance: mean 49.96, sd 0.946, min 40, quartiles 50, max 60
+    r = rng.random()
+    c = 50 if r < 0.97 else (40 if r < 0.985 else 60)
+    return c * 10  # cpu_santicores * 10 millicores (workload.rs:305-308)
+
+
+def c3_traces(n_nodes: int = 4096, n_pods: int = 16384, arrival_window: float = 1200.0, seed: int = 2017,
+              mean_duration: float = 193.0):
+    rng = random.Random(seed)
+    c = GenericClusterTrace()
+    for k in range(1, n_nodes + 1):
+        ram = int(_machine_mem(rng) * float(GIB128))
+        c.create_node(0.0, Node(f"alibaba_node_{k}", 64 * 1000, ram))
+    w = GenericWorkloadTrace()
+    for i in range(n_pods):
+        start = float(int(rng.random() * arrival_window) + 1)  # integer seconds: many equal timestamps
+        dur = float(max(1, int(rng.expovariate(1.0 / mean_duration))))
+        ram = int(_task_mem(rng) * float(GIB128))
+        w.create_pod(start, Pod(f"{1000 + i // 64}_{i}_{i}", _task_cpu(rng), ram, dur))
+    return c, w
+
+
+def c3_scenario(n_nodes: int = 4096, n_pods: int = 16384, arrival_window: float = 1200.0, seed: int = 2017) -> str:
+    cfg = SimulationConfig()
+    c, w = c3_traces(n_nodes, n_pods, arrival_window, seed)
+    return scenario_text(cfg, c, w)
+
+
+# ---- HPA + CA (C4) ----------------------------------------------------------------------------
+def c4_scenario(n_batch_pods: int = 400, seed: int = 7) -> str:
+    """tests/test_hpa.rs pod group + config.yaml:14-33 CA node groups, with a burst of batch pods
+    that forces scale-up and then drains (scale-down)."""
+    rng = random.Random(seed)
+    cfg = SimulationConfig()
+    cfg.hpa_enabled = True
+    cfg.ca_enabled = True
+    cfg.ca_max_node_count = 200
+    cfg.ca_node_groups = [CANodeGroup("autoscaler_128cpu_256gb_node", 50, 128000, 274877906944),
+                          CANodeGroup("autoscaler_64cpu_128gb_node", None, 64000, 137438953472)]
+    c = GenericClusterTrace().create_node(5.0, Node("trace_node_42", 64000, 68719476736))
+    w = GenericWorkloadTrace()
+    g = PodGroup("pod_group_1", 5, 100, Pod("pod_group_1", 100, 104857600, None), 0.6, None,
+                 UsageModel("pod_group", units=[(500.0, 8.0), (200.0, 2.0)]), None)
+    w.events.append(WorkloadEvent(59.5, "create_pod_group", pod_group=g))
+    for i in range(n_batch_pods):
+        w.create_pod(float(100 + int(rng.random() * 300)),
+                     Pod(f"batch_{i}", rng.choice([4000, 8000, 16000]), rng.choice([8, 16, 32]) << 30,
+                         float(rng.randint(60, 600))))
+    return scenario_text(cfg, c, w)
+
+
+# ---- parameter sweep (C5) ---------------------------------------------------------------------
+def c5_params(defaults, n: int, base_seed: int = 123, replica_offset: int = 0):
+    """Per-replica k10s_replica_params for the 65,536-replica sweep."""
+    from .native import ReplicaParams
+    out = []
+    for i in range(n):
+        r = replica_offset + i
+        p = ReplicaParams()
+        ctypes_copy(p, defaults)
+        p.scheduling_cycle_interval = (1.0, 5.0, 10.0, 30.0)[r % 4]
+        p.enable_unscheduled_pods_conditional_move = (r // 4) % 2
+        f = (0.5, 1.0, 2.0)[(r // 8) % 3]
+        p.sched_to_as_network_delay = defaults.sched_to_as_network_delay * f
+        p.ps_to_sched_network_delay = defaults.ps_to_sched_network_delay * f
+        p.ca_scale_down_utilization_threshold = (0.3, 0.5, 0.7)[(r // 24) % 3]
+        p.hpa_target_threshold_tolerance = (0.05, 0.1, 0.2)[(r // 72) % 3]
+        p.seed = base_seed + r
+        p.perturb = 1
+        out.append(p)
+    return out
+
+
+def ctypes_copy(dst, src):
+    import ctypes
+    ctypes.memmove(ctypes.addressof(dst), ctypes.addressof(src), ctypes.sizeof(dst))
+
+
+def replica_params(defaults, n: int, base_seed: int = 123, perturb: bool = True, replica_offset: int = 0):
+    """Seed-perturbed replicas with the scenario's config (C2/C3)."""
+    from .native import ReplicaParams
+    out = []
+    for i in range(n):
+        p = ReplicaParams()
+        ctypes_copy(p, defaults)
+        p.seed = base_seed + replica_offset + i
+        p.perturb = 1 if perturb else 0
+        out.append(p)
+    return out

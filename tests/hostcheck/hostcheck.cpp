@@ -1,0 +1,143 @@
+// tests/hostcheck/hostcheck.cpp — TEST-ONLY host build of the engine's per-replica code.
+//
+// Compiles kubernetriks_amd/csrc/k10s_engine.h with g++ (K10S_LANES == 1) so the kernels' logic
+// can be diffed against the CPU oracle on machines without a GPU.  It is not part of the product:
+// the product C ABI (include/k10s.h, libk10s.so) only runs on the GPU and fails loudly without one.
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../kubernetriks_amd/csrc/k10s_builder.h"
+#include "../../kubernetriks_amd/csrc/k10s_engine.h"
+#include "../../kubernetriks_amd/csrc/k10s_results.h"
+
+using namespace k10s;
+
+struct HC {
+    HostScenario hs;
+    std::vector<uint8_t> scen_bytes;
+    Scenario sc;
+    Layout L;
+    std::vector<Params> params;
+    std::vector<uint8_t> state;
+    uint32_t R = 0;
+};
+
+extern "C" {
+
+void* hc_create(const char* text, const k10s_replica_params* params, uint32_t R, const k10s_capacities* caps,
+                char* err, int errlen) {
+    HC* h = new HC();
+    std::string e;
+    k10s_capacities c;
+    std::memset(&c, 0, sizeof c);
+    if (caps) c = *caps;
+    if (!build_scenario(text, c.group_name_bound, c.ca_name_bound, h->hs, e)) {
+        if (err) std::snprintf(err, (size_t)errlen, "%s", e.c_str());
+        delete h;
+        return nullptr;
+    }
+    Scenario offs;
+    h->scen_bytes = pack_scenario(h->hs, offs);
+    h->sc = rebase_scenario(offs, h->scen_bytes.data());
+    h->L = make_layout(h->hs, c);
+    h->R = R;
+    h->params.resize(R);
+    for (uint32_t r = 0; r < R; r++) {
+        if (params) {
+            h->params[r] = params[r];
+        } else {
+            h->params[r] = h->hs.defaults;
+            h->params[r].seed = h->hs.defaults.seed + r;
+        }
+        h->params[r].ca_max_node_count = h->hs.defaults.ca_max_node_count;
+    }
+    h->state.assign((size_t)h->L.stride * R, 0);
+    for (uint32_t r = 0; r < R; r++) init_replica(&h->sc, &h->params[r], &h->L, h->state.data(), r);
+    return h;
+}
+void hc_free(void* p) { delete (HC*)p; }
+int hc_default_params(void* p, k10s_replica_params* out) {
+    *out = ((HC*)p)->hs.defaults;
+    return 0;
+}
+int hc_run(void* p, int mode, double until, double max_time, uint64_t budget) {
+    HC* h = (HC*)p;
+    int active = 0;
+    for (uint32_t r = 0; r < h->R; r++) {
+        while (run_replica(&h->sc, &h->params[r], &h->L, h->state.data(), r, mode, until, max_time, budget)) {
+        }
+    }
+    return active;
+}
+int hc_results(void* p, k10s_replica_result* out) {
+    HC* h = (HC*)p;
+    for (uint32_t r = 0; r < h->R; r++) {
+        Rep v = make_rep(h->state.data(), h->L, r);
+        hdr_to_result(*v.h, out[r]);
+    }
+    return 0;
+}
+int hc_event_log(void* p, uint32_t r, k10s_log_entry* out, uint32_t cap, uint32_t* n) {
+    HC* h = (HC*)p;
+    Rep v = make_rep(h->state.data(), h->L, r);
+    uint32_t k = v.h->log_n < cap ? v.h->log_n : cap;
+    if (v.log) std::memcpy(out, v.log, sizeof(k10s_log_entry) * k);
+    *n = v.log ? k : 0;
+    return 0;
+}
+int hc_placements(void* p, uint32_t r, k10s_placement* out, uint32_t cap, uint32_t* n) {
+    HC* h = (HC*)p;
+    Rep v = make_rep(h->state.data(), h->L, r);
+    uint32_t k = v.h->place_n < cap ? v.h->place_n : cap;
+    if (v.place) std::memcpy(out, v.place, sizeof(k10s_placement) * k);
+    *n = v.place ? k : 0;
+    return 0;
+}
+int hc_pod_records(void* p, uint32_t r, k10s_pod_record* out, uint32_t cap, uint32_t* n) {
+    HC* h = (HC*)p;
+    Rep v = make_rep(h->state.data(), h->L, r);
+    uint32_t k = h->hs.n_pods < cap ? h->hs.n_pods : cap;
+    if (v.prec) std::memcpy(out, v.prec, sizeof(k10s_pod_record) * k);
+    *n = v.prec ? k : 0;
+    return 0;
+}
+int hc_group_sizes(void* p, uint32_t r, uint32_t* created, uint32_t* total, uint32_t cap, uint32_t* n) {
+    HC* h = (HC*)p;
+    Rep v = make_rep(h->state.data(), h->L, r);
+    uint32_t G = (uint32_t)h->hs.group_names.size();
+    uint32_t k = G < cap ? G : cap;
+    for (uint32_t g = 0; g < k; g++) {
+        created[g] = v.grp[g].registered ? v.grp[g].created_count : 0;
+        total[g] = v.grp[g].total_created;
+    }
+    *n = k;
+    return 0;
+}
+uint32_t hc_num_nodes(void* p) { return ((HC*)p)->hs.n_nodes; }
+uint32_t hc_num_pods(void* p) { return ((HC*)p)->hs.n_pods; }
+uint32_t hc_num_groups(void* p) { return (uint32_t)((HC*)p)->hs.group_names.size(); }
+const char* hc_node_name(void* p, uint32_t i) { return ((HC*)p)->hs.node_names[i].c_str(); }
+const char* hc_pod_name(void* p, uint32_t i) { return ((HC*)p)->hs.pod_names[i].c_str(); }
+const char* hc_group_name(void* p, uint32_t i) { return ((HC*)p)->hs.group_names[i].c_str(); }
+uint64_t hc_replica_bytes(void* p) { return ((HC*)p)->L.stride; }
+
+}  // extern "C"
+
+extern "C" int hc_debug_queues(void* p, uint32_t r, double* aq, uint32_t* aq_pod, uint32_t* naq, double* uq,
+                               uint32_t* uq_pod, uint32_t* nuq, uint32_t cap) {
+    HC* h = (HC*)p;
+    Rep v = make_rep(h->state.data(), h->L, r);
+    *naq = v.h->aq_size;
+    *nuq = v.h->uq_size;
+    for (uint32_t i = 0; i < v.h->aq_size && i < cap; i++) {
+        aq[i] = v.aq[i].timestamp;
+        aq_pod[i] = v.aq[i].pod;
+    }
+    for (uint32_t i = 0; i < v.h->uq_size && i < cap; i++) {
+        uq[i] = v.uq[i].timestamp;
+        uq_pod[i] = v.uq[i].pod;
+    }
+    return 0;
+}

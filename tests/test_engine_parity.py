@@ -1,0 +1,182 @@
+"""Engine vs oracle parity: bit-exact counters, estimators, clocks, placements, per-pod times and
+per-event (id, time, kind, pod, node, slot) logs.
+
+Each test body runs against two backends:
+  * "gpu"  — the product: build/libk10s.so on a MI355X (pytest -m gpu);
+  * "host" — the TEST-ONLY host build of the same engine source (tests/hostcheck), on CPU.
+"""
+import math
+import random
+
+import pytest
+
+import gen
+import oracle_bridge as ob
+import parity
+import scenarios as sc
+from hostcheck_bridge import HostEngine
+from kubernetriks_amd import workloads as wl
+from kubernetriks_amd.native import RUN_UNTIL_ALL_FINISHED, RUN_UNTIL_TIME
+from kubernetriks_amd.scenario import SimulationConfig, scenario_text
+
+
+def _gpu_engine():
+    from kubernetriks_amd.native import Engine
+    return Engine
+
+
+BACKENDS = [
+    pytest.param("host", id="host"),
+    pytest.param("gpu", id="gpu", marks=pytest.mark.gpu),
+]
+
+
+def engine_cls(backend):
+    return HostEngine if backend == "host" else _gpu_engine()
+
+
+STEP_SCENARIOS = {"node_removed_same_time_as_assignment": 1000.0, "hpa": 1200.0}
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+@pytest.mark.parametrize("name", sorted(sc.ALL_TEST_SCENARIOS))
+def test_reference_scenarios(backend, name):
+    scn = sc.ALL_TEST_SCENARIOS[name]()
+    if name in STEP_SCENARIOS:
+        od, eng = parity.run_pair(engine_cls(backend), scn, mode=RUN_UNTIL_TIME, until=STEP_SCENARIOS[name])
+    else:
+        od, eng = parity.run_pair(engine_cls(backend), scn)
+    assert parity.compare(od, eng) == []
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_hpa_checkpoints(backend):
+    """tests/test_hpa.rs:91-134 through the engine's stepping API."""
+    import json, os
+    G = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_goldens.json")))
+    eng = engine_cls(backend)(sc.sc_hpa(), 1, caps=parity.parity_caps(False))
+    for t, size in G["hpa"]["checkpoints"]:
+        eng.step_until_time(t)
+        assert eng.group_sizes(0)["pod_group_1"][0] == size, t
+
+
+FUZZ_SEEDS_HOST = list(range(0, 120))
+FUZZ_SEEDS_GPU = list(range(0, 60))
+
+
+def _fuzz(backend, seed):
+    kw = dict(ca=(seed % 3 == 1), hpa=(seed % 4 == 2))
+    scn = gen.random_scenario(seed, **kw)
+    mode = RUN_UNTIL_TIME if kw["hpa"] else RUN_UNTIL_ALL_FINISHED
+    od, eng = parity.run_pair(engine_cls(backend), scn, mode=mode, until=3000.0, max_time=20000.0)
+    assert parity.compare(od, eng) == [], seed
+
+
+@pytest.mark.parametrize("seed", FUZZ_SEEDS_HOST)
+def test_fuzz_host(seed):
+    _fuzz("host", seed)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", FUZZ_SEEDS_GPU)
+def test_fuzz_gpu(seed):
+    _fuzz("gpu", seed)
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_budgeted_launches_equal_one_launch(backend):
+    """Pausing every few events (multi-launch runs) must not change anything."""
+    scn = gen.random_scenario(7, n_pods=80)
+    E = engine_cls(backend)
+    a = E(scn, 1, caps=parity.parity_caps(True))
+    a.run_until_all_finished(20000.0)
+    b = E(scn, 1, caps=parity.parity_caps(True))
+    b.run_until_all_finished(20000.0, max_events_per_launch=37)
+    assert a.results() == b.results()
+    assert a.event_log(0) == b.event_log(0)
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_batched_replicas_match_oracle_per_replica(backend):
+    """R seed-perturbed replicas in one batch: each equals the oracle on its materialized trace."""
+    c, w = wl.c3_traces(n_nodes=256, n_pods=600, arrival_window=300.0, seed=5)
+    cfg = SimulationConfig()
+    scn = scenario_text(cfg, c, w)
+    E = engine_cls(backend)
+    R = 48 if backend == "gpu" else 6
+    probe = E(scn, 1)
+    params = wl.replica_params(probe.default_params(), R, base_seed=1000, perturb=True)
+    eng = E(scn, R, params=params, caps=parity.parity_caps(False))
+    eng.run_until_all_finished(1e6)
+    for r in sorted({0, R // 2, R - 1}):
+        o = ob.OracleSim(scenario_text(cfg, c, wl.perturb_workload(w, params[r].seed)))
+        st = o.run_until_all_finished(1e6)
+        od = o.result(placements=True)
+        od["status_name"] = parity.ORACLE_STATUS[st]
+        assert parity.compare(od, eng, r=r, log=False) == [], r
+
+
+# ---- unit-parity surface: k10s_schedule_one_batch ---------------------------------------------
+def _random_problem(rng, n_nodes):
+    nodes = []
+    for i in range(n_nodes):
+        if rng.random() < 0.1:
+            cpu = 0
+        else:
+            cpu = rng.choice([1000, 2000, 4000, 8000, rng.randint(1, 20000)])
+        ram = rng.choice([0, 1 << 30, 2 << 30, 4 << 30, rng.randint(1, 1 << 34)]) if rng.random() < 0.9 else 0
+        present = rng.random() < 0.85
+        nodes.append((f"n{i:05d}", cpu, ram, present))
+    r = rng.random()
+    if r < 0.05:
+        pc, pr = 0, 0
+    elif r < 0.15:
+        pc, pr = 0, rng.randint(1, 1 << 30)
+    else:
+        pc, pr = rng.choice([500, 1000, 2000]), rng.choice([1 << 28, 1 << 30])
+    return nodes, pc, pr
+
+
+@pytest.mark.gpu
+def test_schedule_one_batch_matches_oracle():
+    import ctypes
+    import torch
+    from kubernetriks_amd.native import lib
+    rng = random.Random(11)
+    R, N, stride = 400, 300, 320
+    cpu = torch.zeros(R * stride, dtype=torch.int64)
+    ram = torch.zeros(R * stride, dtype=torch.int64)
+    bits = torch.zeros(R * stride // 64, dtype=torch.int64)
+    rc = torch.zeros(R, dtype=torch.int64)
+    rr = torch.zeros(R, dtype=torch.int64)
+    problems = []
+    for r in range(R):
+        nodes, pc, pr = _random_problem(rng, N if r % 7 else rng.randint(0, 5))
+        problems.append((nodes, pc, pr))
+        for i, (_, c_, r_, p_) in enumerate(nodes):
+            cpu[r * stride + i] = c_
+            ram[r * stride + i] = r_ - (1 << 64) if r_ >= (1 << 63) else r_
+            if p_:
+                w = (r * stride + i) // 64
+                v = int(bits[w]) & ((1 << 64) - 1)
+                v |= 1 << ((r * stride + i) % 64)
+                bits[w] = v - (1 << 64) if v >= (1 << 63) else v
+        rc[r], rr[r] = pc, pr
+    dev = torch.device("cuda:0")
+    d_cpu = cpu.to(torch.int32).to(dev)
+    d_ram, d_bits = ram.to(dev), bits.to(dev)
+    d_rc, d_rr = rc.to(torch.int32).to(dev), rr.to(dev)
+    out_node = torch.full((R,), -7, dtype=torch.int32, device=dev)
+    out_st = torch.full((R,), -7, dtype=torch.int32, device=dev)
+    rcode = lib().k10s_schedule_one_batch(d_cpu.data_ptr(), d_ram.data_ptr(), d_bits.data_ptr(), N, stride,
+                                          d_rc.data_ptr(), d_rr.data_ptr(), 1.0, R, out_node.data_ptr(),
+                                          out_st.data_ptr(), None)
+    assert rcode == 0
+    torch.cuda.synchronize()
+    got_n, got_s = out_node.cpu().tolist(), out_st.cpu().tolist()
+    for r, (nodes, pc, pr) in enumerate(problems):
+        present = [(nm, c_, r_) for nm, c_, r_, p_ in nodes if p_]
+        st, name = ob.schedule_one(present, pc, pr)
+        assert got_s[r] == st, r
+        if st == 0:
+            assert nodes[got_n[r]][0] == name, r
