@@ -660,38 +660,15 @@ Layout make_layout(const HostScenario& hs, const k10s_capacities& caps) {
         return o;
     };
     L.hdr = take(sizeof(RepHdr));
-    // hot scheduler-cache SoA first
+    // hot scheduler-cache SoA first (the scan target), then per-entity records
     L.s_cpu = take(4 * N);
     L.s_ram = take(8 * N);
     L.s_present = take(8 * (uint64_t)L.words_nodes);
-    L.node_flags = take(N);
-    L.ps_cpu = take(4 * N);
-    L.ps_ram = take(8 * N);
-    L.ps_def = take(4 * N);
-    L.ps_epoch = take(4 * N);
-    L.as_slot = take(4 * N);
-    L.pend_def = take(4 * N);
+    L.node = take(sizeof(NodeState) * N);
     L.pend_rm = take(8 * (uint64_t)L.words_uids);
-    L.preq_cpu = take(4 * P);
-    L.preq_ram = take(8 * P);
-    L.pdur = take(8 * P);
-    L.pflags = take(P);
-    L.s_assigned = take(4 * P);
-    L.ps_assigned = take(4 * P);
-    L.ps_aepoch = take(4 * P);
-    L.run_slot = take(4 * P);
-    L.run_prev = take(4 * P);
-    L.run_next = take(4 * P);
-    L.finish_seq = take(4 * P);
-    L.cancel_slot = take(4 * P);
-    L.cancel_gen = take(4 * P);
+    L.pod = take(sizeof(PodState) * P);
     L.prec = take(L.rec_on ? sizeof(k10s_pod_record) * P : 0);
-    L.slot_node = take(4 * S);
-    L.slot_def = take(4 * S);
-    L.slot_removed = take(S);
-    L.slot_rtime = take(8 * S);
-    L.slot_gen = take(4 * S);
-    L.slot_head = take(4 * S);
+    L.slot = take(sizeof(SlotState) * S);
     L.pool_ring = take(4 * S);
     L.grp = take(sizeof(GroupState) * G);
     L.grp_bits = take(8 * G * (uint64_t)L.words_group);

@@ -34,10 +34,10 @@ struct Ctx {
 K10S_HD void fail(Ctx& c, uint32_t code) {
     if (c.err == 0) {
         c.err = code;
-        c.v.h->error_code = code;
-        c.v.h->error_kind = c.cur_kind;
-        c.v.h->error_seq = c.cur_seq;
-        c.v.h->error_time = c.clock;
+        c.v.h()->error_code = code;
+        c.v.h()->error_kind = c.cur_kind;
+        c.v.h()->error_seq = c.cur_seq;
+        c.v.h()->error_time = c.clock;
     }
 }
 
@@ -85,7 +85,7 @@ K10S_HD uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uint32_
     e.a = a;
     e.b = b;
     e.x = x;
-    HeapEv* hp = c.v.heap;
+    HeapEv* hp = c.v.heap();
     uint32_t pos = c.heap_size++;
     int64_t k = total_key(e.time);
     while (pos > 0) {
@@ -102,7 +102,7 @@ K10S_HD uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uint32_
 K10S_HD uint32_t emit0(Ctx& c, uint32_t kind, double delay) { return emit(c, kind, delay, -1, 0, 0, 0.0); }
 
 K10S_HD void heap_pop(Ctx& c) {
-    HeapEv* hp = c.v.heap;
+    HeapEv* hp = c.v.heap();
     uint32_t n = --c.heap_size;
     if (n == 0) return;
     HeapEv last = hp[n];
@@ -154,10 +154,10 @@ K10S_HD void aq_push(Ctx& c, const QInfo& q) {
         return;
     }
     uint32_t old = c.aq_size++;
-    aq_sift_up(c.v.aq, 0, old, q);
+    aq_sift_up(c.v.aq(), 0, old, q);
 }
 K10S_HD QInfo aq_pop(Ctx& c) {
-    QInfo* d = c.v.aq;
+    QInfo* d = c.v.aq();
     QInfo item = d[--c.aq_size];
     uint32_t end = c.aq_size;
     if (end == 0) return item;
@@ -193,7 +193,7 @@ K10S_HD void uq_insert(Ctx& c, const QInfo& q) {
         fail(c, K10S_ERR_QUEUE_FULL);
         return;
     }
-    QInfo* d = c.v.uq;
+    QInfo* d = c.v.uq();
     uint32_t pos = c.uq_size++;
     while (pos > 0) {  // timestamps are almost always >= the tail: short backward walk
         QInfo prev = d[pos - 1];
@@ -213,13 +213,13 @@ K10S_HD void uq_insert(Ctx& c, const QInfo& q) {
     d[pos] = q;
 }
 
-K10S_HD bool pod_in_s(const Ctx& c, uint32_t p) { return (c.v.pflags[p] & PF_IN_S) != 0; }
+K10S_HD bool pod_in_s(const Ctx& c, uint32_t p) { return (c.v.pod(p).flags & PF_IN_S) != 0; }
 
 // move_pods_to_active_queue over a selection, in key order (scheduler.rs:174-185)
 // mode 0: all (move_all_to_active_queue, 235-244); 1: flush (188-203, stay > 300 s);
 // 2: freed-resources conditional (366-379); 3: inverted add-node conditional (396-405).
 K10S_HD void s_move(Ctx& c, int mode, double t, uint32_t cpu, uint64_t ram) {
-    QInfo* d = c.v.uq;
+    QInfo* d = c.v.uq();
     uint32_t n = c.uq_size;
     uint32_t w = 0;
     uint32_t fc = cpu;
@@ -242,8 +242,8 @@ K10S_HD void s_move(Ctx& c, int mode, double t, uint32_t cpu, uint64_t ram) {
         } else if (mode == 1) {
             sel = (t - q.timestamp) > 5.0 * 60.0;
         } else {
-            uint32_t rc = c.v.preq_cpu[q.pod];
-            uint64_t rr = c.v.preq_ram[q.pod];
+            uint32_t rc = c.v.pod(q.pod).req_cpu;
+            uint64_t rr = c.v.pod(q.pod).req_ram;
             if (rc <= fc && rr <= fr) {
                 fc -= rc;
                 fr -= rr;
@@ -269,23 +269,23 @@ K10S_HD void s_move_after_free(Ctx& c, uint32_t cpu, uint64_t ram) {
 
 // ---- running-pod lists of node components ----------------------------------------------------
 K10S_HD void run_insert(Ctx& c, int32_t slot, uint32_t p) {
-    int32_t h = c.v.slot_head[slot];
-    c.v.run_prev[p] = -1;
-    c.v.run_next[p] = h;
-    if (h >= 0) c.v.run_prev[h] = (int32_t)p;
-    c.v.slot_head[slot] = (int32_t)p;
-    c.v.run_slot[p] = slot;
+    int32_t h = c.v.slot(slot).head;
+    c.v.pod(p).run_prev = -1;
+    c.v.pod(p).run_next = h;
+    if (h >= 0) c.v.pod(h).run_prev = (int32_t)p;
+    c.v.slot(slot).head = (int32_t)p;
+    c.v.pod(p).run_slot = slot;
 }
 K10S_HD void run_remove(Ctx& c, uint32_t p) {
-    int32_t slot = c.v.run_slot[p];
-    int32_t pr = c.v.run_prev[p], nx = c.v.run_next[p];
-    if (pr >= 0) c.v.run_next[pr] = nx;
-    else c.v.slot_head[slot] = nx;
-    if (nx >= 0) c.v.run_prev[nx] = pr;
-    c.v.run_slot[p] = -1;
-    c.v.finish_seq[p] = 0;  // cancels a pending finish event (dslab cancel_event)
+    int32_t slot = c.v.pod(p).run_slot;
+    int32_t pr = c.v.pod(p).run_prev, nx = c.v.pod(p).run_next;
+    if (pr >= 0) c.v.pod(pr).run_next = nx;
+    else c.v.slot(slot).head = nx;
+    if (nx >= 0) c.v.pod(nx).run_prev = pr;
+    c.v.pod(p).run_slot = -1;
+    c.v.pod(p).finish_seq = 0;  // cancels a pending finish event (dslab cancel_event)
     int32_t g = c.sc->pod_group[p];
-    if (g >= 0) c.v.grp[g].running -= 1;
+    if (g >= 0) c.v.grp()[g].running -= 1;
 }
 
 // ---- schedule_one: Fit filter + LeastAllocated score + argmax (the hot scan) -------------------
@@ -334,7 +334,7 @@ K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const ui
 // ---- scheduling cycle (scheduler.rs:246-334) ----------------------------------------------------
 K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
     double cycle_dur = 0.0;
-    RepHdr* h = c.v.h;
+    RepHdr* h = c.v.h();
     const double w = c.pr->score_weight;
     while (c.aq_size > 0 && !c.err) {
         QInfo q = aq_pop(c);
@@ -344,8 +344,8 @@ K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
         uint32_t nn = h->s_node_count;
         double sched_time = 0.000001 * (double)nn;  // ConstantTimePerNodeModel (model.rs:24-26)
         cycle_dur += sched_time;
-        uint32_t rc = c.v.preq_cpu[p];
-        uint64_t rr = c.v.preq_ram[p];
+        uint32_t rc = c.v.pod(p).req_cpu;
+        uint64_t rr = c.v.pod(p).req_ram;
         int st;
         int32_t chosen = -1;
         if (rc == 0 && rr == 0) {
@@ -355,7 +355,7 @@ K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
         } else {
             h->counters[K10S_C_ATTEMPTS] += 1;
             h->counters[K10S_C_NODES_SCANNED] += nn;
-            st = schedule_scan(c.v.s_cpu, c.v.s_ram, c.v.s_present, c.sc->n_nodes, rc, rr, w, &chosen);
+            st = schedule_scan(c.v.s_cpu(), c.v.s_ram(), c.v.s_present(), c.sc->n_nodes, rc, rr, w, &chosen);
         }
         if (st != K10S_SCHED_OK) {
             q.timestamp = t + cycle_dur;
@@ -364,18 +364,18 @@ K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
             continue;
         }
         uint32_t n = (uint32_t)chosen;
-        c.v.s_cpu[n] -= rc;  // reserve_node_resources (118-123)
-        c.v.s_ram[n] -= rr;
-        c.v.node_flags[n] |= NF_S_ASSIGN;  // assign_node_to_pod (125-151)
-        c.v.s_assigned[p] = (int32_t)n;
+        c.v.s_cpu()[n] -= rc;  // reserve_node_resources (118-123)
+        c.v.s_ram()[n] -= rr;
+        c.v.node(n).flags |= NF_S_ASSIGN;  // assign_node_to_pod (125-151)
+        c.v.pod(p).s_assigned = (int32_t)n;
         emit(c, K10S_EV_AS_ASSIGN_REQ, cycle_dur + c.pr->sched_to_as_network_delay, -1, p, n, t + cycle_dur);
         h->counters[K10S_C_PLACEMENTS] += 1;
-        if (c.v.place) {
+        if (c.v.place()) {
             uint32_t k = h->place_n;
             if (k < c.L->cap_place) {
-                c.v.place[k].assign_time = t + cycle_dur;
-                c.v.place[k].pod = (int32_t)p;
-                c.v.place[k].node = (int32_t)n;
+                c.v.place()[k].assign_time = t + cycle_dur;
+                c.v.place()[k].pod = (int32_t)p;
+                c.v.place()[k].node = (int32_t)n;
                 h->place_n = k + 1;
             } else {
                 h->flags |= 2u;
@@ -415,17 +415,17 @@ K10S_HD void for_each_pod_in_order(Ctx& c, Pred pred, F f) {
 
 // ---- scheduler handlers (scheduler.rs:382-477) ---------------------------------------------------
 K10S_HD void s_release(Ctx& c, uint32_t p) {  // release_node_resources (153-162)
-    int32_t n = c.v.s_assigned[p];
-    if (n < 0 || !bit_test(c.v.s_present, (uint32_t)n)) {
+    int32_t n = c.v.pod(p).s_assigned;
+    if (n < 0 || !bit_test(c.v.s_present(), (uint32_t)n)) {
         fail(c, K10S_PANIC_MISSING_NODE);
         return;
     }
-    c.v.s_cpu[n] += c.v.preq_cpu[p];
-    c.v.s_ram[n] += c.v.preq_ram[p];
+    c.v.s_cpu()[n] += c.v.pod(p).req_cpu;
+    c.v.s_ram()[n] += c.v.pod(p).req_ram;
 }
 
 K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
-    RepHdr* h = c.v.h;
+    RepHdr* h = c.v.h();
     switch (e.kind) {
     case K10S_EV_S_RUN_CYCLE:
         run_scheduling_cycle(c, e.time);
@@ -438,10 +438,10 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
         uint32_t n = e.a;
         uint32_t ac = e.b;
         uint64_t ar = f2u(e.x);
-        c.v.s_cpu[n] = ac;
-        c.v.s_ram[n] = ar;
-        if (!bit_test(c.v.s_present, n)) {
-            bit_set(c.v.s_present, n);
+        c.v.s_cpu()[n] = ac;
+        c.v.s_ram()[n] = ar;
+        if (!bit_test(c.v.s_present(), n)) {
+            bit_set(c.v.s_present(), n);
             h->s_node_count += 1;
         }
         if (c.pr->enable_unscheduled_pods_conditional_move) s_move(c, 3, 0.0, ac, ar);
@@ -450,8 +450,8 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
     }
     case K10S_EV_S_POD_SCHEDULE_REQ: {
         uint32_t p = e.a;
-        c.v.pflags[p] |= PF_IN_S;
-        c.v.s_assigned[p] = -1;
+        c.v.pod(p).flags |= PF_IN_S;
+        c.v.pod(p).s_assigned = -1;
         QInfo q;
         q.timestamp = e.time;
         q.initial = e.time;
@@ -466,31 +466,31 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
             fail(c, K10S_PANIC_MISSING_POD);
             return;
         }
-        c.v.pflags[p] &= (uint8_t)~PF_IN_S;
-        if (!(c.v.node_flags[n] & NF_S_ASSIGN)) {
+        c.v.pod(p).flags &= (uint8_t)~PF_IN_S;
+        if (!(c.v.node(n).flags & NF_S_ASSIGN)) {
             fail(c, K10S_PANIC_MISSING_ASSIGNMENTS);
             return;
         }
         s_release(c, p);
         if (c.err) return;
-        s_move_after_free(c, c.v.preq_cpu[p], c.v.preq_ram[p]);
+        s_move_after_free(c, c.v.pod(p).req_cpu, c.v.pod(p).req_ram);
         break;
     }
     case K10S_EV_S_REMOVE_NODE: {
         uint32_t n = e.a;
-        if (!bit_test(c.v.s_present, n)) {
+        if (!bit_test(c.v.s_present(), n)) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
         }
-        bit_clear(c.v.s_present, n);
+        bit_clear(c.v.s_present(), n);
         h->s_node_count -= 1;
-        if (c.v.node_flags[n] & NF_S_ASSIGN) {  // reschedule_unfinished_pods (352-364), name order
-            c.v.node_flags[n] &= (uint8_t)~NF_S_ASSIGN;
+        if (c.v.node(n).flags & NF_S_ASSIGN) {  // reschedule_unfinished_pods (352-364), name order
+            c.v.node(n).flags &= (uint8_t)~NF_S_ASSIGN;
             double t = e.time;
             for_each_pod_in_order(
-                c, [&](uint32_t p) { return pod_in_s(c, p) && c.v.s_assigned[p] == (int32_t)n; },
+                c, [&](uint32_t p) { return pod_in_s(c, p) && c.v.pod(p).s_assigned == (int32_t)n; },
                 [&](uint32_t p) {
-                    c.v.s_assigned[p] = -1;
+                    c.v.pod(p).s_assigned = -1;
                     QInfo q;
                     q.timestamp = t;
                     q.initial = t;
@@ -504,16 +504,16 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
     case K10S_EV_S_REMOVE_POD: {
         uint32_t p = e.a;
         if (!pod_in_s(c, p)) return;
-        c.v.pflags[p] &= (uint8_t)~PF_IN_S;
-        int32_t n = c.v.s_assigned[p];
+        c.v.pod(p).flags &= (uint8_t)~PF_IN_S;
+        int32_t n = c.v.pod(p).s_assigned;
         if (n >= 0) {
             s_release(c, p);
             if (c.err) return;
-            if (!(c.v.node_flags[n] & NF_S_ASSIGN)) {
+            if (!(c.v.node(n).flags & NF_S_ASSIGN)) {
                 fail(c, K10S_PANIC_MISSING_ASSIGNMENTS);
                 return;
             }
-            s_move_after_free(c, c.v.preq_cpu[p], c.v.preq_ram[p]);
+            s_move_after_free(c, c.v.pod(p).req_cpu, c.v.pod(p).req_ram);
         }
         break;
     }
@@ -528,16 +528,16 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
 // by autoscale() while exactly one request is in flight, so deciding at snapshot time and
 // emitting the actions at delivery time (cluster_autoscaler.rs:309-331) is equivalent.
 K10S_HD void ca_decide(Ctx& c) {
-    RepHdr* h = c.v.h;
+    RepHdr* h = c.v.h();
     const Scenario* sc = c.sc;
     h->ca_n_act = 0;
-    uint32_t* cag = c.v.cag;
+    uint32_t* cag = c.v.cag();
     const uint64_t max_nodes = c.pr->ca_max_node_count;
     if (h->unsched_cache_count > 0) {
         // scale_up_info (persistent_storage.rs:137-145) looks every cached unscheduled pod up in
         // storage before the algorithm runs: a removed one panics (the cache is never cleaned, A.5)
         for (uint32_t p = 0; p < sc->n_pods; p++) {
-            if ((c.v.pflags[p] & PF_UNSCHED) && !(c.v.pflags[p] & PF_IN_PS)) {
+            if ((c.v.pod(p).flags & PF_UNSCHED) && !(c.v.pod(p).flags & PF_IN_PS)) {
                 fail(c, K10S_PANIC_MISSING_POD);
                 return;
             }
@@ -557,14 +557,14 @@ K10S_HD void ca_decide(Ctx& c) {
         if (over) return;
         uint32_t nalloc = 0;
         for (uint32_t p = 0; p < sc->n_pods && !c.err; p++) {
-            if (!(c.v.pflags[p] & PF_UNSCHED)) continue;
-            uint32_t rc = c.v.preq_cpu[p];
-            uint64_t rr = c.v.preq_ram[p];
+            if (!(c.v.pod(p).flags & PF_UNSCHED)) continue;
+            uint32_t rc = c.v.pod(p).req_cpu;
+            uint64_t rr = c.v.pod(p).req_ram;
             bool fit = false;
             for (uint32_t i = 0; i < nalloc; i++) {  // try_fit_in_allocated_nodes (114-123)
-                if (rc <= c.v.ca_cpu[i] && rr <= c.v.ca_ram[i]) {
-                    c.v.ca_cpu[i] -= rc;
-                    c.v.ca_ram[i] -= rr;
+                if (rc <= c.v.ca_cpu()[i] && rr <= c.v.ca_ram()[i]) {
+                    c.v.ca_cpu()[i] -= rc;
+                    c.v.ca_ram()[i] -= rr;
                     fit = true;
                     break;
                 }
@@ -585,10 +585,10 @@ K10S_HD void ca_decide(Ctx& c) {
                         fail(c, K10S_ERR_CA_BUFFER);
                         return;
                     }
-                    c.v.ca_act[nalloc].up = 1;
-                    c.v.ca_act[nalloc].arg = sc->ca_def[g * sc->ca_bound + (k - 1)];
-                    c.v.ca_cpu[nalloc] = sc->ca_cpu[g];
-                    c.v.ca_ram[nalloc] = sc->ca_ram[g];
+                    c.v.ca_act()[nalloc].up = 1;
+                    c.v.ca_act()[nalloc].arg = sc->ca_def[g * sc->ca_bound + (k - 1)];
+                    c.v.ca_cpu()[nalloc] = sc->ca_cpu[g];
+                    c.v.ca_ram()[nalloc] = sc->ca_ram[g];
                     nalloc++;
                     cur++;
                     break;
@@ -601,40 +601,40 @@ K10S_HD void ca_decide(Ctx& c) {
     // scale_down (247-306) over PS nodes in name order with a mutable copy of their allocatable
     const uint32_t N = sc->n_nodes;
     for (uint32_t n = 0; n < N; n++) {
-        c.v.ca_cpu[n] = c.v.ps_cpu[n];
-        c.v.ca_ram[n] = c.v.ps_ram[n];
+        c.v.ca_cpu()[n] = c.v.node(n).ps_cpu;
+        c.v.ca_ram()[n] = c.v.node(n).ps_ram;
     }
     uint32_t nrem = 0;
     for (uint32_t n = 0; n < N && !c.err; n++) {
-        if (!(c.v.node_flags[n] & NF_PS_PRESENT)) continue;
-        uint32_t def = c.v.ps_def[n];
+        if (!(c.v.node(n).flags & NF_PS_PRESENT)) continue;
+        uint32_t def = c.v.node(n).ps_def;
         if (!sc->def_ca_origin[def]) continue;
         uint32_t cap_c = sc->def_cpu[def];
         uint64_t cap_r = sc->def_ram[def];
-        double cu = (double)(uint32_t)(cap_c - c.v.ca_cpu[n]) / (double)cap_c;
-        double ru = (double)(uint64_t)(cap_r - c.v.ca_ram[n]) / (double)cap_r;
+        double cu = (double)(uint32_t)(cap_c - c.v.ca_cpu()[n]) / (double)cap_c;
+        double ru = (double)(uint64_t)(cap_r - c.v.ca_ram()[n]) / (double)cap_r;
         double util = cu > ru ? cu : ru;
         if (!(util < c.pr->ca_scale_down_utilization_threshold)) continue;
         // all_pods_can_be_moved_to_other_nodes (148-181): pods in PS assignments[n], name order
         uint32_t nundo = 0;
         bool ok = true;
-        uint32_t ep = c.v.ps_epoch[n];
+        uint32_t ep = c.v.node(n).ps_epoch;
         for (uint32_t p = 0; p < sc->n_pods && ok; p++) {
-            if (c.v.ps_assigned[p] != (int32_t)n || c.v.ps_aepoch[p] != ep || ep == 0) continue;
-            uint32_t rc = c.v.preq_cpu[p];
-            uint64_t rr = c.v.preq_ram[p];
+            if (c.v.pod(p).ps_assigned != (int32_t)n || c.v.pod(p).ps_aepoch != ep || ep == 0) continue;
+            uint32_t rc = c.v.pod(p).req_cpu;
+            uint64_t rr = c.v.pod(p).req_ram;
             bool placed = false;
             for (uint32_t m = 0; m < N; m++) {
-                if (m == n || !(c.v.node_flags[m] & NF_PS_PRESENT)) continue;
-                if (rc <= c.v.ca_cpu[m] && rr <= c.v.ca_ram[m]) {
-                    c.v.ca_cpu[m] -= rc;
-                    c.v.ca_ram[m] -= rr;
+                if (m == n || !(c.v.node(m).flags & NF_PS_PRESENT)) continue;
+                if (rc <= c.v.ca_cpu()[m] && rr <= c.v.ca_ram()[m]) {
+                    c.v.ca_cpu()[m] -= rc;
+                    c.v.ca_ram()[m] -= rr;
                     if (nundo >= c.L->cap_undo) {
                         fail(c, K10S_ERR_CA_BUFFER);
                         return;
                     }
-                    c.v.ca_undo[2 * nundo] = m;
-                    c.v.ca_undo[2 * nundo + 1] = p;
+                    c.v.ca_undo()[2 * nundo] = m;
+                    c.v.ca_undo()[2 * nundo + 1] = p;
                     nundo++;
                     placed = true;
                     break;
@@ -644,9 +644,9 @@ K10S_HD void ca_decide(Ctx& c) {
         }
         if (!ok) {
             for (uint32_t i = 0; i < nundo; i++) {  // *nodes = original
-                uint32_t m = c.v.ca_undo[2 * i], p = c.v.ca_undo[2 * i + 1];
-                c.v.ca_cpu[m] += c.v.preq_cpu[p];
-                c.v.ca_ram[m] += c.v.preq_ram[p];
+                uint32_t m = c.v.ca_undo()[2 * i], p = c.v.ca_undo()[2 * i + 1];
+                c.v.ca_cpu()[m] += c.v.pod(p).req_cpu;
+                c.v.ca_ram()[m] += c.v.pod(p).req_ram;
             }
             continue;
         }
@@ -654,13 +654,13 @@ K10S_HD void ca_decide(Ctx& c) {
             fail(c, K10S_ERR_CA_BUFFER);
             return;
         }
-        c.v.ca_act[nrem].up = 0;
-        c.v.ca_act[nrem].arg = n;
+        c.v.ca_act()[nrem].up = 0;
+        c.v.ca_act()[nrem].arg = n;
         nrem++;
     }
     for (uint32_t i = 0; i < nrem; i++) {
-        uint32_t n = c.v.ca_act[i].arg;
-        int32_t g = sc->def_ca_group[c.v.ps_def[n]];
+        uint32_t n = c.v.ca_act()[i].arg;
+        int32_t g = sc->def_ca_group[c.v.node(n).ps_def];
         if (g < 0) {
             fail(c, K10S_PANIC_CA_GROUP);
             return;
@@ -672,111 +672,111 @@ K10S_HD void ca_decide(Ctx& c) {
 
 // ---- persistent storage (persistent_storage.rs:185-490) --------------------------------------
 K10S_HD void ps_clean_up(Ctx& c, uint32_t p) {  // 173-182
-    int32_t n = c.v.ps_assigned[p];
+    int32_t n = c.v.pod(p).ps_assigned;
     if (n < 0) return;
-    if (c.v.node_flags[n] & NF_PS_PRESENT) {
-        c.v.ps_cpu[n] += c.v.preq_cpu[p];
-        c.v.ps_ram[n] += c.v.preq_ram[p];
-        if (c.v.ps_aepoch[p] == c.v.ps_epoch[n]) c.v.ps_aepoch[p] = 0;
+    if (c.v.node(n).flags & NF_PS_PRESENT) {
+        c.v.node(n).ps_cpu += c.v.pod(p).req_cpu;
+        c.v.node(n).ps_ram += c.v.pod(p).req_ram;
+        if (c.v.pod(p).ps_aepoch == c.v.node(n).ps_epoch) c.v.pod(p).ps_aepoch = 0;
     }
 }
 
 K10S_HD void on_ps(Ctx& c, const HeapEv& e) {
-    RepHdr* h = c.v.h;
+    RepHdr* h = c.v.h();
     const Params* pr = c.pr;
     switch (e.kind) {
     case K10S_EV_PS_CREATE_NODE_REQ: {
         uint32_t def = e.b, n = e.a;
-        if (c.v.node_flags[n] & NF_PS_PRESENT) {
+        if (c.v.node(n).flags & NF_PS_PRESENT) {
             fail(c, K10S_PANIC_DUPLICATE_NODE);
             return;
         }
-        c.v.node_flags[n] |= NF_PS_PRESENT;
-        c.v.ps_def[n] = def;
-        c.v.ps_cpu[n] = c.sc->def_cpu[def];
-        c.v.ps_ram[n] = c.sc->def_ram[def];
-        c.v.ps_epoch[n] += 1;
+        c.v.node(n).flags |= NF_PS_PRESENT;
+        c.v.node(n).ps_def = def;
+        c.v.node(n).ps_cpu = c.sc->def_cpu[def];
+        c.v.node(n).ps_ram = c.sc->def_ram[def];
+        c.v.node(n).ps_epoch += 1;
         h->ps_node_count += 1;
         emit(c, K10S_EV_AS_CREATE_NODE_RESP, pr->as_to_ps_network_delay, -1, n, 0, 0.0);
         break;
     }
     case K10S_EV_PS_NODE_ADDED: {
         uint32_t n = e.a;
-        if (!(c.v.node_flags[n] & NF_PS_PRESENT)) {
+        if (!(c.v.node(n).flags & NF_PS_PRESENT)) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
         }
-        emit(c, K10S_EV_S_ADD_NODE, pr->ps_to_sched_network_delay, -1, n, c.v.ps_cpu[n], u2f(c.v.ps_ram[n]));
+        emit(c, K10S_EV_S_ADD_NODE, pr->ps_to_sched_network_delay, -1, n, c.v.node(n).ps_cpu, u2f(c.v.node(n).ps_ram));
         h->counters[K10S_C_PROCESSED_NODES] += 1;
         break;
     }
     case K10S_EV_PS_CREATE_POD_REQ: {
         uint32_t p = e.a;
-        if (c.v.pflags[p] & PF_IN_PS) {
+        if (c.v.pod(p).flags & PF_IN_PS) {
             fail(c, K10S_PANIC_DUPLICATE_POD);
             return;
         }
-        c.v.pflags[p] |= PF_IN_PS;
-        c.v.ps_assigned[p] = -1;
-        if (c.v.prec) c.v.prec[p].state = 1;
+        c.v.pod(p).flags |= PF_IN_PS;
+        c.v.pod(p).ps_assigned = -1;
+        if (c.v.prec()) c.v.prec()[p].state = 1;
         emit(c, K10S_EV_S_POD_SCHEDULE_REQ, pr->ps_to_sched_network_delay, -1, p, 0, 0.0);
         break;
     }
     case K10S_EV_PS_ASSIGN_REQ: {
         uint32_t p = e.a, n = e.b;
-        if (!(c.v.pflags[p] & PF_IN_PS)) {
+        if (!(c.v.pod(p).flags & PF_IN_PS)) {
             fail(c, K10S_PANIC_MISSING_POD);
             return;
         }
-        c.v.ps_assigned[p] = (int32_t)n;
-        if (c.v.pflags[p] & PF_UNSCHED) {
-            c.v.pflags[p] &= (uint8_t)~PF_UNSCHED;
+        c.v.pod(p).ps_assigned = (int32_t)n;
+        if (c.v.pod(p).flags & PF_UNSCHED) {
+            c.v.pod(p).flags &= (uint8_t)~PF_UNSCHED;
             h->unsched_cache_count -= 1;
         }
-        if (!(c.v.node_flags[n] & NF_PS_PRESENT)) {
+        if (!(c.v.node(n).flags & NF_PS_PRESENT)) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
         }
-        c.v.ps_cpu[n] -= c.v.preq_cpu[p];
-        c.v.ps_ram[n] -= c.v.preq_ram[p];
-        c.v.ps_aepoch[p] = c.v.ps_epoch[n];
+        c.v.node(n).ps_cpu -= c.v.pod(p).req_cpu;
+        c.v.node(n).ps_ram -= c.v.pod(p).req_ram;
+        c.v.pod(p).ps_aepoch = c.v.node(n).ps_epoch;
         emit(c, K10S_EV_AS_ASSIGN_RESP, pr->as_to_ps_network_delay, -1, p, n, 0.0);
         break;
     }
     case K10S_EV_PS_POD_NOT_SCHEDULED: {
         uint32_t p = e.a;
-        if (!(c.v.pflags[p] & PF_IN_PS)) {
+        if (!(c.v.pod(p).flags & PF_IN_PS)) {
             fail(c, K10S_PANIC_MISSING_POD);
             return;
         }
-        if (!(c.v.pflags[p] & PF_UNSCHED)) {
-            c.v.pflags[p] |= PF_UNSCHED;
+        if (!(c.v.pod(p).flags & PF_UNSCHED)) {
+            c.v.pod(p).flags |= PF_UNSCHED;
             h->unsched_cache_count += 1;
         }
         break;
     }
     case K10S_EV_PS_POD_STARTED: {
         uint32_t p = e.a;
-        if (!(c.v.pflags[p] & PF_IN_PS)) {
+        if (!(c.v.pod(p).flags & PF_IN_PS)) {
             fail(c, K10S_PANIC_MISSING_POD);
             return;
         }
-        if (c.v.prec) c.v.prec[p].t_running = e.x;
+        if (c.v.prec()) c.v.prec()[p].t_running = e.x;
         break;
     }
     case K10S_EV_PS_POD_FINISHED: {
         uint32_t p = e.a;
-        if (c.v.pflags[p] & PF_IN_PS) {
-            c.v.pflags[p] &= (uint8_t)~PF_IN_PS;
+        if (c.v.pod(p).flags & PF_IN_PS) {
+            c.v.pod(p).flags &= (uint8_t)~PF_IN_PS;
             ps_clean_up(c, p);
             if (!(c.sc->pod_flags[p] & POD_HAS_DUR)) {
                 fail(c, K10S_PANIC_MISSING_POD);
                 return;
             }
-            est_add(h->est[K10S_EST_POD_DURATION], c.v.pdur[p]);
-            if (c.v.prec) {
-                c.v.prec[p].t_finished = e.x;
-                c.v.prec[p].state = 2;
+            est_add(h->est[K10S_EST_POD_DURATION], c.v.pod(p).dur);
+            if (c.v.prec()) {
+                c.v.prec()[p].t_finished = e.x;
+                c.v.prec()[p].state = 2;
             }
         }
         emit(c, K10S_EV_S_POD_FINISHED, pr->ps_to_sched_network_delay, -1, p, e.b, e.x);
@@ -784,11 +784,11 @@ K10S_HD void on_ps(Ctx& c, const HeapEv& e) {
     }
     case K10S_EV_PS_REMOVE_NODE_REQ: {
         uint32_t n = e.a;
-        if (!(c.v.node_flags[n] & NF_PS_PRESENT)) {
+        if (!(c.v.node(n).flags & NF_PS_PRESENT)) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
         }
-        c.v.node_flags[n] &= (uint8_t)~NF_PS_PRESENT;
+        c.v.node(n).flags &= (uint8_t)~NF_PS_PRESENT;
         h->ps_node_count -= 1;
         emit(c, K10S_EV_AS_REMOVE_NODE_RESP, pr->as_to_ps_network_delay, -1, n, 0, 0.0);
         break;
@@ -802,16 +802,16 @@ K10S_HD void on_ps(Ctx& c, const HeapEv& e) {
         break;
     case K10S_EV_PS_REMOVE_POD_REQ: {
         uint32_t p = e.a;
-        if (!(c.v.pflags[p] & PF_IN_PS)) {
+        if (!(c.v.pod(p).flags & PF_IN_PS)) {
             emit(c, K10S_EV_AS_REMOVE_POD_RESP, pr->as_to_ps_network_delay, -1, p, 0, 0.0);
             return;
         }
-        c.v.pflags[p] &= (uint8_t)~PF_IN_PS;
-        if (c.v.prec) {
-            c.v.prec[p].t_removed = e.time;
-            c.v.prec[p].state = 3;
+        c.v.pod(p).flags &= (uint8_t)~PF_IN_PS;
+        if (c.v.prec()) {
+            c.v.prec()[p].t_removed = e.time;
+            c.v.prec()[p].state = 3;
         }
-        int32_t n = c.v.ps_assigned[p];
+        int32_t n = c.v.pod(p).ps_assigned;
         uint32_t flag = 0;
         if (n >= 0) {
             ps_clean_up(c, p);
@@ -832,39 +832,39 @@ K10S_HD void on_ps(Ctx& c, const HeapEv& e) {
 
 // ---- api server (api_server.rs:127-457) --------------------------------------------------------
 K10S_HD void on_api_server(Ctx& c, const HeapEv& e) {
-    RepHdr* h = c.v.h;
+    RepHdr* h = c.v.h();
     const Params* pr = c.pr;
     const Scenario* sc = c.sc;
     switch (e.kind) {
     case K10S_EV_AS_CREATE_NODE_REQ: {
         uint32_t def = e.b;
         uint32_t n = sc->def_node[def];
-        c.v.pend_def[n] = (int32_t)def;
+        c.v.node(n).pend_def = (int32_t)def;
         emit(c, K10S_EV_PS_CREATE_NODE_REQ, pr->as_to_ps_network_delay, -1, n, def, 0.0);
         break;
     }
     case K10S_EV_AS_CREATE_NODE_RESP: {  // handle_create_node (96-115)
         uint32_t n = e.a;
-        int32_t def = c.v.pend_def[n];
+        int32_t def = c.v.node(n).pend_def;
         if (def < 0) {
             fail(c, K10S_PANIC_MISSING_PENDING);
             return;
         }
-        c.v.pend_def[n] = -1;
+        c.v.node(n).pend_def = -1;
         if (h->pool_count == 0) {
             fail(c, K10S_PANIC_POOL_EXHAUSTED);
             return;
         }
-        uint32_t slot = c.v.pool_ring[h->pool_head];
+        uint32_t slot = c.v.pool_ring()[h->pool_head];
         h->pool_head = (h->pool_head + 1) % sc->n_slots;
         h->pool_count -= 1;
-        c.v.slot_node[slot] = (int32_t)n;
-        c.v.slot_def[slot] = (uint32_t)def;
-        if (c.v.as_slot[n] >= 0) {
+        c.v.slot(slot).node = (int32_t)n;
+        c.v.slot(slot).def = (uint32_t)def;
+        if (c.v.node(n).as_slot >= 0) {
             fail(c, K10S_PANIC_DUPLICATE_NODE);
             return;
         }
-        c.v.as_slot[n] = (int32_t)slot;
+        c.v.node(n).as_slot = (int32_t)slot;
         h->as_node_count += 1;
         emit(c, K10S_EV_PS_NODE_ADDED, pr->as_to_ps_network_delay, -1, n, 0, e.time);
         break;
@@ -874,13 +874,13 @@ K10S_HD void on_api_server(Ctx& c, const HeapEv& e) {
         break;
     case K10S_EV_AS_ASSIGN_REQ: {
         uint32_t n = e.b;
-        if (bit_test(c.v.pend_rm, sc->node_uid[n]) || c.v.as_slot[n] < 0) return;
+        if (bit_test(c.v.pend_rm(), sc->node_uid[n]) || c.v.node(n).as_slot < 0) return;
         emit(c, K10S_EV_PS_ASSIGN_REQ, pr->as_to_ps_network_delay, -1, e.a, n, e.x);
         break;
     }
     case K10S_EV_AS_ASSIGN_RESP: {
         uint32_t n = e.b;
-        int32_t slot = c.v.as_slot[n];
+        int32_t slot = c.v.node(n).as_slot;
         if (slot < 0) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
@@ -900,11 +900,11 @@ K10S_HD void on_api_server(Ctx& c, const HeapEv& e) {
         emit(c, K10S_EV_PS_POD_FINISHED, pr->as_to_ps_network_delay, -1, e.a, e.b, e.x);
         break;
     case K10S_EV_AS_REMOVE_NODE_REQ:
-        bit_set(c.v.pend_rm, sc->node_uid[e.a]);
+        bit_set(c.v.pend_rm(), sc->node_uid[e.a]);
         emit(c, K10S_EV_PS_REMOVE_NODE_REQ, pr->as_to_ps_network_delay, -1, e.a, 0, 0.0);
         break;
     case K10S_EV_AS_REMOVE_NODE_RESP: {
-        int32_t slot = c.v.as_slot[e.a];
+        int32_t slot = c.v.node(e.a).as_slot;
         if (slot < 0) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
@@ -914,23 +914,23 @@ K10S_HD void on_api_server(Ctx& c, const HeapEv& e) {
     }
     case K10S_EV_AS_NODE_REMOVED: {
         uint32_t n = e.a;
-        int32_t slot = c.v.as_slot[n];
+        int32_t slot = c.v.node(n).as_slot;
         if (slot < 0) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
         }
-        c.v.as_slot[n] = -1;
+        c.v.node(n).as_slot = -1;
         h->as_node_count -= 1;
         // reclaim_component (node_component_pool.rs:68-77)
-        c.v.slot_node[slot] = -1;
-        c.v.slot_removed[slot] = 0;
-        c.v.slot_rtime[slot] = 0.0;
-        c.v.slot_gen[slot] += 1;
-        c.v.slot_head[slot] = -1;
+        c.v.slot(slot).node = -1;
+        c.v.slot(slot).removed = 0;
+        c.v.slot(slot).rtime = 0.0;
+        c.v.slot(slot).gen += 1;
+        c.v.slot(slot).head = -1;
         uint32_t tail = (h->pool_head + h->pool_count) % sc->n_slots;
-        c.v.pool_ring[tail] = (uint32_t)slot;
+        c.v.pool_ring()[tail] = (uint32_t)slot;
         h->pool_count += 1;
-        bit_clear(c.v.pend_rm, sc->node_uid[n]);
+        bit_clear(c.v.pend_rm(), sc->node_uid[n]);
         emit(c, K10S_EV_PS_NODE_REMOVED, pr->as_to_ps_network_delay, -1, n, 0, e.x);
         break;
     }
@@ -941,12 +941,12 @@ K10S_HD void on_api_server(Ctx& c, const HeapEv& e) {
         emit0(c, K10S_EV_CA_RESP, pr->as_to_ca_network_delay);
         break;
     case K10S_EV_AS_REMOVE_POD_REQ:
-        bit_set(c.v.pend_rm, sc->pod_uid[e.a]);  // quirk (api_server.rs:343): the NODE removal set
+        bit_set(c.v.pend_rm(), sc->pod_uid[e.a]);  // quirk (api_server.rs:343): the NODE removal set
         emit(c, K10S_EV_PS_REMOVE_POD_REQ, pr->as_to_ps_network_delay, -1, e.a, 0, 0.0);
         break;
     case K10S_EV_AS_REMOVE_POD_RESP: {
         if (f2u(e.x) != 0) {
-            int32_t slot = c.v.as_slot[e.b];
+            int32_t slot = c.v.node(e.b).as_slot;
             if (slot < 0) {
                 fail(c, K10S_PANIC_MISSING_NODE);
                 return;
@@ -968,7 +968,7 @@ K10S_HD void on_api_server(Ctx& c, const HeapEv& e) {
             fail(c, K10S_PANIC_GROUP_DURATION);
             return;
         }
-        GroupState& gs = c.v.grp[g];
+        GroupState& gs = c.v.grp()[g];
         gs.creation_time = e.time;
         gs.cpu_last_start = e.time;
         gs.ram_last_start = e.time;
@@ -997,33 +997,33 @@ K10S_HD void on_node(Ctx& c, const HeapEv& e) {
     switch (e.kind) {
     case K10S_EV_N_BIND: {
         uint32_t p = e.a, n = e.b;
-        if (c.v.slot_removed[slot]) {
+        if (c.v.slot(slot).removed) {
             fail(c, K10S_PANIC_BIND_REMOVED_NODE);
             return;
         }
-        if (c.v.slot_node[slot] != (int32_t)n) {
+        if (c.v.slot(slot).node != (int32_t)n) {
             fail(c, K10S_PANIC_BIND_REMOVED_NODE);
             return;
         }
-        if (c.v.run_slot[p] >= 0) {  // a second concurrent bind of one pod: not modelled
+        if (c.v.pod(p).run_slot >= 0) {  // a second concurrent bind of one pod: not modelled
             fail(c, K10S_PANIC_BIND_REMOVED_NODE);
             return;
         }
         uint32_t fseq = 0;
         if (c.sc->pod_flags[p] & POD_HAS_DUR) {  // simulate_pod_runtime (114-175)
-            double dur = c.v.pdur[p];
+            double dur = c.v.pod(p).dur;
             fseq = emit(c, K10S_EV_N_POD_FINISHED, dur + pr->as_to_node_network_delay, slot, p, n, e.time + dur);
         }
         run_insert(c, slot, p);
-        c.v.finish_seq[p] = fseq;
+        c.v.pod(p).finish_seq = fseq;
         int32_t g = c.sc->pod_group[p];
-        if (g >= 0) c.v.grp[g].running += 1;
+        if (g >= 0) c.v.grp()[g].running += 1;
         emit(c, K10S_EV_AS_POD_STARTED, pr->as_to_node_network_delay, -1, p, 0, e.time);
         break;
     }
     case K10S_EV_N_POD_FINISHED: {
         uint32_t p = e.a;
-        if (c.v.run_slot[p] != slot) {
+        if (c.v.pod(p).run_slot != slot) {
             fail(c, K10S_PANIC_MISSING_POD);
             return;
         }
@@ -1033,36 +1033,36 @@ K10S_HD void on_node(Ctx& c, const HeapEv& e) {
     }
     case K10S_EV_N_REMOVE_NODE: {
         uint32_t n = e.a;
-        if (c.v.slot_node[slot] != (int32_t)n) {
+        if (c.v.slot(slot).node != (int32_t)n) {
             fail(c, K10S_PANIC_REMOVE_OTHER_NODE);
             return;
         }
         // cancel_all_running_pods (95-112)
-        int32_t p = c.v.slot_head[slot];
-        uint32_t gen = c.v.slot_gen[slot];
+        int32_t p = c.v.slot(slot).head;
+        uint32_t gen = c.v.slot(slot).gen;
         while (p >= 0) {
-            int32_t nx = c.v.run_next[p];
-            c.v.cancel_slot[p] = slot;
-            c.v.cancel_gen[p] = gen;
+            int32_t nx = c.v.pod(p).run_next;
+            c.v.pod(p).cancel_slot = slot;
+            c.v.pod(p).cancel_gen = gen;
             run_remove(c, (uint32_t)p);
             p = nx;
         }
         emit(c, K10S_EV_AS_NODE_REMOVED, pr->as_to_node_network_delay, -1, n, 0, e.time);
-        c.v.slot_removed[slot] = 1;
-        c.v.slot_rtime[slot] = e.time;
+        c.v.slot(slot).removed = 1;
+        c.v.slot(slot).rtime = e.time;
         break;
     }
     case K10S_EV_N_REMOVE_POD: {
         uint32_t p = e.a;
-        if (c.v.slot_node[slot] < 0) {
+        if (c.v.slot(slot).node < 0) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
         }
-        if (c.v.run_slot[p] == slot) {
+        if (c.v.pod(p).run_slot == slot) {
             run_remove(c, p);
             emit(c, K10S_EV_AS_POD_REMOVED, pr->as_to_node_network_delay, -1, p, 1, e.time);
-        } else if (c.v.cancel_slot[p] == slot && c.v.cancel_gen[p] == c.v.slot_gen[slot]) {
-            emit(c, K10S_EV_AS_POD_REMOVED, pr->as_to_node_network_delay, -1, p, 1, c.v.slot_rtime[slot]);
+        } else if (c.v.pod(p).cancel_slot == slot && c.v.pod(p).cancel_gen == c.v.slot(slot).gen) {
+            emit(c, K10S_EV_AS_POD_REMOVED, pr->as_to_node_network_delay, -1, p, 1, c.v.slot(slot).rtime);
         } else {
             emit(c, K10S_EV_AS_POD_REMOVED, pr->as_to_node_network_delay, -1, p, 0, 0.0);
         }
@@ -1075,7 +1075,7 @@ K10S_HD void on_node(Ctx& c, const HeapEv& e) {
 
 // ---- cluster autoscaler proxy (cluster_autoscaler.rs:230-334) --------------------------------
 K10S_HD void on_ca(Ctx& c, const HeapEv& e) {
-    RepHdr* h = c.v.h;
+    RepHdr* h = c.v.h();
     const Params* pr = c.pr;
     if (e.kind == K10S_EV_CA_TICK) {
         h->ca_last_cycle_time = e.time;
@@ -1083,7 +1083,7 @@ K10S_HD void on_ca(Ctx& c, const HeapEv& e) {
         return;
     }
     for (uint32_t i = 0; i < h->ca_n_act && !c.err; i++) {
-        CAAct a = c.v.ca_act[i];
+        CAAct a = c.v.ca_act()[i];
         if (a.up) {
             emit(c, K10S_EV_AS_CREATE_NODE_REQ, pr->as_to_ca_network_delay, -1, c.sc->def_node[a.arg], a.arg, 0.0);
             h->counters[K10S_C_TOTAL_SCALED_UP_NODES] += 1;
@@ -1108,15 +1108,15 @@ K10S_HD uint32_t hpa_desired_by_metric(uint32_t cur, double value, double target
 }
 
 K10S_HD void on_hpa(Ctx& c, const HeapEv& e) {
-    RepHdr* h = c.v.h;
+    RepHdr* h = c.v.h();
     const Scenario* sc = c.sc;
     const uint32_t B = sc->group_bound;
     const uint32_t words = c.L->words_group;
     if (e.kind == K10S_EV_HPA_REGISTER_GROUP) {
         uint32_t g = e.a;
-        GroupState& gs = c.v.grp[g];
+        GroupState& gs = c.v.grp()[g];
         gs.registered = 1;
-        uint64_t* bits = c.v.grp_bits + (uint64_t)g * words;
+        uint64_t* bits = c.v.grp_bits() + (uint64_t)g * words;
         for (uint32_t i = 0; i < words; i++) bits[i] = 0;
         uint32_t init = sc->g_initial[g];
         for (uint32_t k = 0; k < init; k++) bit_set(bits, sc->g_pos[g * B + k]);
@@ -1125,7 +1125,7 @@ K10S_HD void on_hpa(Ctx& c, const HeapEv& e) {
         return;
     }
     for (uint32_t g = 0; g < sc->n_groups && !c.err; g++) {
-        GroupState& gs = c.v.grp[g];
+        GroupState& gs = c.v.grp()[g];
         if (!gs.has_metric) continue;
         if (!gs.registered) {
             fail(c, K10S_PANIC_HPA_UNREGISTERED);
@@ -1142,7 +1142,7 @@ K10S_HD void on_hpa(Ctx& c, const HeapEv& e) {
         else if (gf & GF_HAS_TCPU) desired = dc < mx ? dc : mx;
         else if (gf & GF_HAS_TRAM) desired = dr < mx ? dr : mx;
         else desired = cur;
-        uint64_t* bits = c.v.grp_bits + (uint64_t)g * words;
+        uint64_t* bits = c.v.grp_bits() + (uint64_t)g * words;
         if (cur < desired) {
             for (uint32_t i = 0; i < desired - cur && !c.err; i++) {
                 uint32_t k = gs.total_created;
@@ -1196,7 +1196,7 @@ K10S_HD void on_metrics(Ctx& c, const HeapEv& e) {
     }
     const Scenario* sc = c.sc;
     for (uint32_t g = 0; g < sc->n_groups; g++) {
-        GroupState& gs = c.v.grp[g];
+        GroupState& gs = c.v.grp()[g];
         gs.has_metric = gs.running > 0;
         if (!gs.has_metric) continue;
         // every pod of the group reports the same value (same model, creation time and count), so the
@@ -1236,66 +1236,65 @@ K10S_HD void init_replica(const Scenario* sc, const Params* pr, const Layout* L,
     Rep v = make_rep(base, *L, r);
     const int lane = lane_id();
     const uint32_t N = sc->n_nodes, P = sc->n_pods, S = sc->n_slots, G = sc->n_groups;
+    NodeState ns;
+    memset(&ns, 0, sizeof ns);
+    ns.as_slot = -1;
+    ns.pend_def = -1;
+    uint32_t* s_cpu = v.s_cpu();
+    uint64_t* s_ram = v.s_ram();
     for (uint32_t i = lane; i < N; i += K10S_LANES) {
-        v.s_cpu[i] = 0;
-        v.s_ram[i] = 0;
-        v.node_flags[i] = 0;
-        v.ps_cpu[i] = 0;
-        v.ps_ram[i] = 0;
-        v.ps_def[i] = 0;
-        v.ps_epoch[i] = 0;
-        v.as_slot[i] = -1;
-        v.pend_def[i] = -1;
+        s_cpu[i] = 0;
+        s_ram[i] = 0;
+        v.node(i) = ns;
     }
-    for (uint32_t i = lane; i < L->words_nodes; i += K10S_LANES) v.s_present[i] = 0;
-    for (uint32_t i = lane; i < L->words_uids; i += K10S_LANES) v.pend_rm[i] = 0;
+    for (uint32_t i = lane; i < L->words_nodes; i += K10S_LANES) v.s_present()[i] = 0;
+    for (uint32_t i = lane; i < L->words_uids; i += K10S_LANES) v.pend_rm()[i] = 0;
     const bool perturb = pr->perturb != 0;
+    k10s_pod_record* prec = v.prec();
     for (uint32_t p = lane; p < P; p += K10S_LANES) {
         uint32_t cpu = sc->pod_cpu[p];
         uint64_t ram = sc->pod_ram[p];
         double dur = sc->pod_dur[p];
         if (perturb && (sc->pod_flags[p] & POD_PERTURB)) perturb_pod(*pr, pod_key[p], cpu, ram, dur);
-        v.preq_cpu[p] = cpu;
-        v.preq_ram[p] = ram;
-        v.pdur[p] = dur;
-        v.pflags[p] = 0;
-        v.s_assigned[p] = -1;
-        v.ps_assigned[p] = -1;
-        v.ps_aepoch[p] = 0;
-        v.run_slot[p] = -1;
-        v.run_prev[p] = -1;
-        v.run_next[p] = -1;
-        v.finish_seq[p] = 0;
-        v.cancel_slot[p] = -1;
-        v.cancel_gen[p] = 0;
-        if (v.prec) {
-            v.prec[p].t_running = __builtin_nan("");
-            v.prec[p].t_finished = __builtin_nan("");
-            v.prec[p].t_removed = __builtin_nan("");
-            v.prec[p].state = 0;
-            v.prec[p].pad = 0;
+        PodState ps;
+        memset(&ps, 0, sizeof ps);
+        ps.req_cpu = cpu;
+        ps.req_ram = ram;
+        ps.dur = dur;
+        ps.s_assigned = -1;
+        ps.ps_assigned = -1;
+        ps.run_slot = -1;
+        ps.run_prev = -1;
+        ps.run_next = -1;
+        ps.cancel_slot = -1;
+        v.pod(p) = ps;
+        if (prec) {
+            prec[p].t_running = __builtin_nan("");
+            prec[p].t_finished = __builtin_nan("");
+            prec[p].t_removed = __builtin_nan("");
+            prec[p].state = 0;
+            prec[p].pad = 0;
         }
     }
+    SlotState ss;
+    memset(&ss, 0, sizeof ss);
+    ss.node = -1;
+    ss.head = -1;
     for (uint32_t s = lane; s < S; s += K10S_LANES) {
-        v.slot_node[s] = -1;
-        v.slot_def[s] = 0;
-        v.slot_removed[s] = 0;
-        v.slot_rtime[s] = 0.0;
-        v.slot_gen[s] = 0;
-        v.slot_head[s] = -1;
-        v.pool_ring[s] = s;  // pool contexts first (FIFO), default-node components after
+        v.slot((int32_t)s) = ss;
+        v.pool_ring()[s] = s;  // pool contexts first (FIFO), default-node components after
     }
     for (uint32_t g = lane; g < G; g += K10S_LANES) {
         GroupState gs;
         memset(&gs, 0, sizeof gs);
-        v.grp[g] = gs;
+        v.grp()[g] = gs;
     }
-    for (uint32_t i = lane; i < G * L->words_group; i += K10S_LANES) v.grp_bits[i] = 0;
-    for (uint32_t i = lane; i < 2 * sc->n_ca_groups; i += K10S_LANES) v.cag[i] = 0;
+    for (uint32_t i = lane; i < G * L->words_group; i += K10S_LANES) v.grp_bits()[i] = 0;
+    for (uint32_t i = lane; i < 2 * sc->n_ca_groups; i += K10S_LANES) v.cag()[i] = 0;
     wave_sync();
 
     // serial part (wave-uniform)
-    RepHdr* h = v.h;
+    RepHdr* h = v.h();
     RepHdr z;
     memset(&z, 0, sizeof z);
     *h = z;
@@ -1309,17 +1308,18 @@ K10S_HD void init_replica(const Scenario* sc, const Params* pr, const Layout* L,
         uint32_t def = sc->default_defs[j];
         uint32_t n = sc->def_node[def];
         uint32_t slot = sc->n_pool + j;
-        v.node_flags[n] |= NF_PS_PRESENT;
-        v.ps_def[n] = def;
-        v.ps_cpu[n] = sc->def_cpu[def];
-        v.ps_ram[n] = sc->def_ram[def];
-        v.ps_epoch[n] = 1;
-        v.as_slot[n] = (int32_t)slot;
-        v.slot_node[slot] = (int32_t)n;
-        v.slot_def[slot] = def;
-        v.s_cpu[n] = sc->def_cpu[def];
-        v.s_ram[n] = sc->def_ram[def];
-        bit_set(v.s_present, n);
+        NodeState& nd = v.node(n);
+        nd.flags |= NF_PS_PRESENT;
+        nd.ps_def = def;
+        nd.ps_cpu = sc->def_cpu[def];
+        nd.ps_ram = sc->def_ram[def];
+        nd.ps_epoch = 1;
+        nd.as_slot = (int32_t)slot;
+        v.slot((int32_t)slot).node = (int32_t)n;
+        v.slot((int32_t)slot).def = def;
+        s_cpu[n] = sc->def_cpu[def];
+        s_ram[n] = sc->def_ram[def];
+        bit_set(v.s_present(), n);
     }
     h->s_node_count = sc->n_default;
     h->ps_node_count = sc->n_default;
@@ -1361,7 +1361,7 @@ K10S_HD void init_replica(const Scenario* sc, const Params* pr, const Layout* L,
 K10S_HD int run_replica(const Scenario* sc, const Params* pr, const Layout* L, uint8_t* base, uint32_t r, int mode,
                         double until_time, double max_time, uint64_t budget) {
     Rep v = make_rep(base, *L, r);
-    RepHdr* h = v.h;
+    RepHdr* h = v.h();
     if (h->status != K10S_REPLICA_RUNNING) return 0;
     Ctx c;
     c.sc = sc;
@@ -1399,7 +1399,7 @@ K10S_HD int run_replica(const Scenario* sc, const Params* pr, const Layout* L, u
             if (!ht && !hh) break;
             if (ht) {
                 const TraceEv& te = tr[c.trace_cursor];
-                if (!hh || ev_before(te.time, te.seq, c.v.heap[0].time, c.v.heap[0].seq)) {
+                if (!hh || ev_before(te.time, te.seq, c.v.heap()[0].time, c.v.heap()[0].seq)) {
                     e.time = te.time;
                     e.seq = te.seq;
                     e.kind = (uint16_t)te.kind;
@@ -1416,8 +1416,8 @@ K10S_HD int run_replica(const Scenario* sc, const Params* pr, const Layout* L, u
                     break;
                 }
             }
-            e = c.v.heap[0];
-            if (e.kind == K10S_EV_N_POD_FINISHED && c.v.finish_seq[e.a] != e.seq) {  // canceled
+            e = c.v.heap()[0];
+            if (e.kind == K10S_EV_N_POD_FINISHED && c.v.pod(e.a).finish_seq != e.seq) {  // canceled
                 heap_pop(c);
                 continue;
             }
@@ -1448,7 +1448,7 @@ K10S_HD int run_replica(const Scenario* sc, const Params* pr, const Layout* L, u
         c.cur_seq = e.seq;
         done++;
         h->counters[K10S_C_EVENTS] += 1;
-        if (v.log) {
+        if (L->cap_log) {
             uint32_t k = h->log_n;
             if (k < L->cap_log) {
                 k10s_log_entry le;
@@ -1486,7 +1486,7 @@ K10S_HD int run_replica(const Scenario* sc, const Params* pr, const Layout* L, u
                 }
                 le.pod = pod;
                 le.node = node;
-                v.log[k] = le;
+                v.log()[k] = le;
                 h->log_n = k + 1;
             } else {
                 h->flags |= 1u;

@@ -177,15 +177,56 @@ struct CAAct {
 enum : uint8_t { NF_S_ASSIGN = 1, NF_PS_PRESENT = 2 };
 enum : uint8_t { PF_IN_S = 1, PF_IN_PS = 2, PF_UNSCHED = 4 };
 
+// Per-pod state: every field an event handler touches for one pod, in one 64-B line.
+struct PodState {
+    uint32_t req_cpu;       // requests (seed-perturbed per replica)
+    uint8_t flags;          // PF_*: in scheduler cache / in storage / in PS unscheduled cache
+    uint8_t pad0[3];
+    uint64_t req_ram;
+    double dur;
+    int32_t s_assigned;     // scheduler cache pod.status.assigned_node (node idx or -1)
+    int32_t ps_assigned;    // storage pod.status.assigned_node
+    uint32_t ps_aepoch;     // member of PS assignments[ps_assigned] iff == that node's epoch
+    int32_t run_slot;       // node component running it (running_pods), or -1
+    int32_t run_prev, run_next;   // intrusive list of running pods per component
+    uint32_t finish_seq;    // id of its pending PodFinishedRunning self-event (0 = none/canceled)
+    int32_t cancel_slot;    // canceled_pods membership: (slot, slot generation)
+    uint32_t cancel_gen;
+    uint32_t pad1;
+};
+static_assert(sizeof(PodState) == 64, "PodState must be one 64-B line");
+
+// Cold per-node state (persistent-storage copy, api-server maps): 32 B.
+struct NodeState {
+    uint8_t flags;          // NF_*
+    uint8_t pad0[3];
+    uint32_t ps_cpu;        // PS allocatable
+    uint64_t ps_ram;
+    uint32_t ps_def;        // node instance stored in PS
+    uint32_t ps_epoch;      // bumped by every PS add_node
+    int32_t as_slot;        // created_nodes: node component, or -1
+    int32_t pend_def;       // pending_node_creation_requests: def, or -1
+};
+static_assert(sizeof(NodeState) == 32, "NodeState must be 32 B");
+
+// Node component (pool context) state: 32 B.
+struct SlotState {
+    int32_t node;           // runtime node idx, -1 when back in the pool
+    uint32_t def;
+    uint32_t gen;           // bumped on reclaim (clears canceled_pods)
+    int32_t head;           // running-pod list head
+    double rtime;           // removal_time
+    uint32_t removed;
+    uint32_t pad;
+};
+static_assert(sizeof(SlotState) == 32, "SlotState must be 32 B");
+
 // Offsets (bytes) of per-replica arrays within one replica's region.
 struct Layout {
     uint64_t stride;
     uint64_t hdr;
-    uint64_t s_cpu, s_ram, s_present, node_flags, ps_cpu, ps_ram, ps_def, ps_epoch, as_slot, pend_def;
-    uint64_t pend_rm;
-    uint64_t preq_cpu, preq_ram, pdur, pflags, s_assigned, ps_assigned, ps_aepoch, run_slot, run_prev,
-        run_next, finish_seq, cancel_slot, cancel_gen, prec;
-    uint64_t slot_node, slot_def, slot_removed, slot_rtime, slot_gen, slot_head, pool_ring;
+    uint64_t s_cpu, s_ram, s_present;    // hot scheduler-cache SoA (scan target)
+    uint64_t node, pend_rm, pod, prec, slot, pool_ring;
     uint64_t grp, grp_bits;
     uint64_t cag, ca_act, ca_cpu, ca_ram, ca_undo;
     uint64_t heap, aq, uq, log, place;
@@ -194,102 +235,39 @@ struct Layout {
     uint32_t pad;
 };
 
-struct Rep {                // typed view of one replica's region
-    RepHdr* h;
-    uint32_t* s_cpu;
-    uint64_t* s_ram;
-    uint64_t* s_present;
-    uint8_t* node_flags;
-    uint32_t* ps_cpu;
-    uint64_t* ps_ram;
-    uint32_t* ps_def;
-    uint32_t* ps_epoch;
-    int32_t* as_slot;
-    int32_t* pend_def;
-    uint64_t* pend_rm;
-    uint32_t* preq_cpu;
-    uint64_t* preq_ram;
-    double* pdur;
-    uint8_t* pflags;
-    int32_t* s_assigned;
-    int32_t* ps_assigned;
-    uint32_t* ps_aepoch;
-    int32_t* run_slot;
-    int32_t* run_prev;
-    int32_t* run_next;
-    uint32_t* finish_seq;
-    int32_t* cancel_slot;
-    uint32_t* cancel_gen;
-    k10s_pod_record* prec;
-    int32_t* slot_node;
-    uint32_t* slot_def;
-    uint8_t* slot_removed;
-    double* slot_rtime;
-    uint32_t* slot_gen;
-    int32_t* slot_head;
-    uint32_t* pool_ring;
-    GroupState* grp;
-    uint64_t* grp_bits;
-    uint32_t* cag;          // [CG*2]: current_count, total_allocated
-    CAAct* ca_act;
-    uint32_t* ca_cpu;
-    uint64_t* ca_ram;
-    uint32_t* ca_undo;      // node indices modified during one all_pods_can_be_moved attempt
-    HeapEv* heap;
-    QInfo* aq;
-    QInfo* uq;
-    k10s_log_entry* log;
-    k10s_placement* place;
+// Typed accessors over one replica's region; bases are recomputed from the (constant) layout at
+// each use instead of being held live across the event loop.
+struct Rep {
+    uint8_t* b;
+    const Layout* L;
+    K10S_HD RepHdr* h() const { return (RepHdr*)(b + L->hdr); }
+    K10S_HD uint32_t* s_cpu() const { return (uint32_t*)(b + L->s_cpu); }
+    K10S_HD uint64_t* s_ram() const { return (uint64_t*)(b + L->s_ram); }
+    K10S_HD uint64_t* s_present() const { return (uint64_t*)(b + L->s_present); }
+    K10S_HD NodeState& node(uint32_t n) const { return ((NodeState*)(b + L->node))[n]; }
+    K10S_HD uint64_t* pend_rm() const { return (uint64_t*)(b + L->pend_rm); }
+    K10S_HD PodState& pod(uint32_t p) const { return ((PodState*)(b + L->pod))[p]; }
+    K10S_HD k10s_pod_record* prec() const { return L->rec_on ? (k10s_pod_record*)(b + L->prec) : nullptr; }
+    K10S_HD SlotState& slot(int32_t s) const { return ((SlotState*)(b + L->slot))[s]; }
+    K10S_HD uint32_t* pool_ring() const { return (uint32_t*)(b + L->pool_ring); }
+    K10S_HD GroupState* grp() const { return (GroupState*)(b + L->grp); }
+    K10S_HD uint64_t* grp_bits() const { return (uint64_t*)(b + L->grp_bits); }
+    K10S_HD uint32_t* cag() const { return (uint32_t*)(b + L->cag); }
+    K10S_HD CAAct* ca_act() const { return (CAAct*)(b + L->ca_act); }
+    K10S_HD uint32_t* ca_cpu() const { return (uint32_t*)(b + L->ca_cpu); }
+    K10S_HD uint64_t* ca_ram() const { return (uint64_t*)(b + L->ca_ram); }
+    K10S_HD uint32_t* ca_undo() const { return (uint32_t*)(b + L->ca_undo); }
+    K10S_HD HeapEv* heap() const { return (HeapEv*)(b + L->heap); }
+    K10S_HD QInfo* aq() const { return (QInfo*)(b + L->aq); }
+    K10S_HD QInfo* uq() const { return (QInfo*)(b + L->uq); }
+    K10S_HD k10s_log_entry* log() const { return L->cap_log ? (k10s_log_entry*)(b + L->log) : nullptr; }
+    K10S_HD k10s_placement* place() const { return L->cap_place ? (k10s_placement*)(b + L->place) : nullptr; }
 };
 
 K10S_HD Rep make_rep(uint8_t* base, const Layout& L, uint32_t r) {
-    uint8_t* b = base + (uint64_t)r * L.stride;
     Rep v;
-    v.h = (RepHdr*)(b + L.hdr);
-    v.s_cpu = (uint32_t*)(b + L.s_cpu);
-    v.s_ram = (uint64_t*)(b + L.s_ram);
-    v.s_present = (uint64_t*)(b + L.s_present);
-    v.node_flags = (uint8_t*)(b + L.node_flags);
-    v.ps_cpu = (uint32_t*)(b + L.ps_cpu);
-    v.ps_ram = (uint64_t*)(b + L.ps_ram);
-    v.ps_def = (uint32_t*)(b + L.ps_def);
-    v.ps_epoch = (uint32_t*)(b + L.ps_epoch);
-    v.as_slot = (int32_t*)(b + L.as_slot);
-    v.pend_def = (int32_t*)(b + L.pend_def);
-    v.pend_rm = (uint64_t*)(b + L.pend_rm);
-    v.preq_cpu = (uint32_t*)(b + L.preq_cpu);
-    v.preq_ram = (uint64_t*)(b + L.preq_ram);
-    v.pdur = (double*)(b + L.pdur);
-    v.pflags = (uint8_t*)(b + L.pflags);
-    v.s_assigned = (int32_t*)(b + L.s_assigned);
-    v.ps_assigned = (int32_t*)(b + L.ps_assigned);
-    v.ps_aepoch = (uint32_t*)(b + L.ps_aepoch);
-    v.run_slot = (int32_t*)(b + L.run_slot);
-    v.run_prev = (int32_t*)(b + L.run_prev);
-    v.run_next = (int32_t*)(b + L.run_next);
-    v.finish_seq = (uint32_t*)(b + L.finish_seq);
-    v.cancel_slot = (int32_t*)(b + L.cancel_slot);
-    v.cancel_gen = (uint32_t*)(b + L.cancel_gen);
-    v.prec = L.rec_on ? (k10s_pod_record*)(b + L.prec) : nullptr;
-    v.slot_node = (int32_t*)(b + L.slot_node);
-    v.slot_def = (uint32_t*)(b + L.slot_def);
-    v.slot_removed = (uint8_t*)(b + L.slot_removed);
-    v.slot_rtime = (double*)(b + L.slot_rtime);
-    v.slot_gen = (uint32_t*)(b + L.slot_gen);
-    v.slot_head = (int32_t*)(b + L.slot_head);
-    v.pool_ring = (uint32_t*)(b + L.pool_ring);
-    v.grp = (GroupState*)(b + L.grp);
-    v.grp_bits = (uint64_t*)(b + L.grp_bits);
-    v.cag = (uint32_t*)(b + L.cag);
-    v.ca_act = (CAAct*)(b + L.ca_act);
-    v.ca_cpu = (uint32_t*)(b + L.ca_cpu);
-    v.ca_ram = (uint64_t*)(b + L.ca_ram);
-    v.ca_undo = (uint32_t*)(b + L.ca_undo);
-    v.heap = (HeapEv*)(b + L.heap);
-    v.aq = (QInfo*)(b + L.aq);
-    v.uq = (QInfo*)(b + L.uq);
-    v.log = L.cap_log ? (k10s_log_entry*)(b + L.log) : nullptr;
-    v.place = L.cap_place ? (k10s_placement*)(b + L.place) : nullptr;
+    v.b = base + (uint64_t)r * L.stride;
+    v.L = &L;
     return v;
 }
 

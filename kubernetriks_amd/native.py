@@ -207,6 +207,12 @@ def lib():
     """Load build/libk10s.so (the HIP engine).  Raises if it is missing: no fallback."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch bundles its own libamdhip64 (same SONAME), and a
+        # process that also uses torch.cuda / RCCL must bind this library to that copy.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
         L = ctypes.CDLL(LIB_PATH)

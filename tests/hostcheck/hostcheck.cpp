@@ -75,32 +75,32 @@ int hc_results(void* p, k10s_replica_result* out) {
     HC* h = (HC*)p;
     for (uint32_t r = 0; r < h->R; r++) {
         Rep v = make_rep(h->state.data(), h->L, r);
-        hdr_to_result(*v.h, out[r]);
+        hdr_to_result(*v.h(), out[r]);
     }
     return 0;
 }
 int hc_event_log(void* p, uint32_t r, k10s_log_entry* out, uint32_t cap, uint32_t* n) {
     HC* h = (HC*)p;
     Rep v = make_rep(h->state.data(), h->L, r);
-    uint32_t k = v.h->log_n < cap ? v.h->log_n : cap;
-    if (v.log) std::memcpy(out, v.log, sizeof(k10s_log_entry) * k);
-    *n = v.log ? k : 0;
+    uint32_t k = v.h()->log_n < cap ? v.h()->log_n : cap;
+    if (v.log()) std::memcpy(out, v.log(), sizeof(k10s_log_entry) * k);
+    *n = v.log() ? k : 0;
     return 0;
 }
 int hc_placements(void* p, uint32_t r, k10s_placement* out, uint32_t cap, uint32_t* n) {
     HC* h = (HC*)p;
     Rep v = make_rep(h->state.data(), h->L, r);
-    uint32_t k = v.h->place_n < cap ? v.h->place_n : cap;
-    if (v.place) std::memcpy(out, v.place, sizeof(k10s_placement) * k);
-    *n = v.place ? k : 0;
+    uint32_t k = v.h()->place_n < cap ? v.h()->place_n : cap;
+    if (v.place()) std::memcpy(out, v.place(), sizeof(k10s_placement) * k);
+    *n = v.place() ? k : 0;
     return 0;
 }
 int hc_pod_records(void* p, uint32_t r, k10s_pod_record* out, uint32_t cap, uint32_t* n) {
     HC* h = (HC*)p;
     Rep v = make_rep(h->state.data(), h->L, r);
     uint32_t k = h->hs.n_pods < cap ? h->hs.n_pods : cap;
-    if (v.prec) std::memcpy(out, v.prec, sizeof(k10s_pod_record) * k);
-    *n = v.prec ? k : 0;
+    if (v.prec()) std::memcpy(out, v.prec(), sizeof(k10s_pod_record) * k);
+    *n = v.prec() ? k : 0;
     return 0;
 }
 int hc_group_sizes(void* p, uint32_t r, uint32_t* created, uint32_t* total, uint32_t cap, uint32_t* n) {
@@ -109,8 +109,8 @@ int hc_group_sizes(void* p, uint32_t r, uint32_t* created, uint32_t* total, uint
     uint32_t G = (uint32_t)h->hs.group_names.size();
     uint32_t k = G < cap ? G : cap;
     for (uint32_t g = 0; g < k; g++) {
-        created[g] = v.grp[g].registered ? v.grp[g].created_count : 0;
-        total[g] = v.grp[g].total_created;
+        created[g] = v.grp()[g].registered ? v.grp()[g].created_count : 0;
+        total[g] = v.grp()[g].total_created;
     }
     *n = k;
     return 0;
@@ -129,15 +129,15 @@ extern "C" int hc_debug_queues(void* p, uint32_t r, double* aq, uint32_t* aq_pod
                                uint32_t* uq_pod, uint32_t* nuq, uint32_t cap) {
     HC* h = (HC*)p;
     Rep v = make_rep(h->state.data(), h->L, r);
-    *naq = v.h->aq_size;
-    *nuq = v.h->uq_size;
-    for (uint32_t i = 0; i < v.h->aq_size && i < cap; i++) {
-        aq[i] = v.aq[i].timestamp;
-        aq_pod[i] = v.aq[i].pod;
+    *naq = v.h()->aq_size;
+    *nuq = v.h()->uq_size;
+    for (uint32_t i = 0; i < v.h()->aq_size && i < cap; i++) {
+        aq[i] = v.aq()[i].timestamp;
+        aq_pod[i] = v.aq()[i].pod;
     }
-    for (uint32_t i = 0; i < v.h->uq_size && i < cap; i++) {
-        uq[i] = v.uq[i].timestamp;
-        uq_pod[i] = v.uq[i].pod;
+    for (uint32_t i = 0; i < v.h()->uq_size && i < cap; i++) {
+        uq[i] = v.uq()[i].timestamp;
+        uq_pod[i] = v.uq()[i].pod;
     }
     return 0;
 }
