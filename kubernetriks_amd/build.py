@@ -36,14 +36,18 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False, extra=()) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, extra=(), out: str = None) -> str:
+    """Compile the engine.  `extra` adds compiler flags (e.g. tuning -D knobs) and `out` an
+    alternative output path (variant builds for A/B measurements; load them via K10S_LIB)."""
+    target = out or OUT
+    if not force and out is None and not _stale():
         return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    os.makedirs(os.path.dirname(target), exist_ok=True)
+    tag = os.path.basename(target).replace(".so", "")
     objs = []
     procs = []
     for src in SOURCES:
-        obj = os.path.join(REPO, "build", src + ".o")
+        obj = os.path.join(REPO, "build", f"{tag}.{src}.o")
         cmd = [hipcc(), *FLAGS, *extra, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
@@ -52,11 +56,11 @@ def build(force: bool = False, verbose: bool = False, extra=()) -> str:
     for p in procs:
         if p.wait() != 0:
             raise RuntimeError("hipcc failed")
-    link = [hipcc(), *FLAGS, "-shared", *objs, "-o", OUT]
+    link = [hipcc(), *FLAGS, "-shared", *objs, "-o", target]
     if verbose:
         print(" ".join(link), file=sys.stderr)
     subprocess.check_call(link)
-    return OUT
+    return target
 
 
 if __name__ == "__main__":

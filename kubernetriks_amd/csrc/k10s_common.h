@@ -17,9 +17,36 @@
 #include <hip/hip_runtime.h>
 #define K10S_HD __host__ __device__ __forceinline__
 #define K10S_D __device__ __forceinline__
+#define K10S_HD_NOINL __host__ __device__ __attribute__((noinline)) inline
+#define K10S_HD_FLEX __host__ __device__
 #else
 #define K10S_HD inline
 #define K10S_D inline
+#define K10S_HD_NOINL inline
+#define K10S_HD_FLEX inline
+#endif
+
+// Device-side inlining policy (tuning knob, semantics-neutral): K10S_SPLIT >= 1 keeps the cold
+// handlers (autoscalers, metrics) out of line, >= 2 also the api-server / storage / node handlers,
+// >= 3 also the queue/heap helpers, so the hot loop's register allocation is not sized by them.
+#ifndef K10S_SPLIT
+#define K10S_SPLIT 1
+#endif
+// K10S_COLD / K10S_WARM / K10S_HELPER: function qualifiers following K10S_SPLIT
+#if K10S_SPLIT >= 1
+#define K10S_COLD K10S_HD_NOINL
+#else
+#define K10S_COLD K10S_HD
+#endif
+#if K10S_SPLIT >= 2
+#define K10S_WARM K10S_HD_NOINL
+#else
+#define K10S_WARM K10S_HD
+#endif
+#if K10S_SPLIT >= 3
+#define K10S_HELPER K10S_HD_NOINL
+#else
+#define K10S_HELPER K10S_HD
 #endif
 
 #if defined(__HIP_DEVICE_COMPILE__)

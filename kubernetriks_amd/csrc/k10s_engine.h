@@ -67,7 +67,7 @@ K10S_HD bool ev_before(double ta, uint32_t sa, double tb, uint32_t sb) {
     return ka < kb || (ka == kb && sa < sb);
 }
 
-K10S_HD uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uint32_t a, uint32_t b, double x) {
+K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uint32_t a, uint32_t b, double x) {
     if (c.err) return 0;
     if (c.next_seq == 0xFFFFFFFFu) {
         fail(c, K10S_ERR_SEQ_OVERFLOW);
@@ -101,7 +101,7 @@ K10S_HD uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uint32_
 }
 K10S_HD uint32_t emit0(Ctx& c, uint32_t kind, double delay) { return emit(c, kind, delay, -1, 0, 0, 0.0); }
 
-K10S_HD void heap_pop(Ctx& c) {
+K10S_HELPER void heap_pop(Ctx& c) {
     HeapEv* hp = c.v.heap();
     uint32_t n = --c.heap_size;
     if (n == 0) return;
@@ -148,7 +148,7 @@ K10S_HD uint32_t aq_sift_up(QInfo* d, uint32_t start, uint32_t pos, const QInfo&
     d[pos] = elem;
     return pos;
 }
-K10S_HD void aq_push(Ctx& c, const QInfo& q) {
+K10S_HELPER void aq_push(Ctx& c, const QInfo& q) {
     if (c.aq_size >= c.L->cap_aq) {
         fail(c, K10S_ERR_QUEUE_FULL);
         return;
@@ -156,7 +156,7 @@ K10S_HD void aq_push(Ctx& c, const QInfo& q) {
     uint32_t old = c.aq_size++;
     aq_sift_up(c.v.aq(), 0, old, q);
 }
-K10S_HD QInfo aq_pop(Ctx& c) {
+K10S_HELPER QInfo aq_pop(Ctx& c) {
     QInfo* d = c.v.aq();
     QInfo item = d[--c.aq_size];
     uint32_t end = c.aq_size;
@@ -188,7 +188,7 @@ K10S_HD bool u_less(const QInfo& a, const QInfo& b) {
     int64_t ka = total_key(a.timestamp), kb = total_key(b.timestamp);
     return ka < kb || (ka == kb && a.pod < b.pod);
 }
-K10S_HD void uq_insert(Ctx& c, const QInfo& q) {
+K10S_HELPER void uq_insert(Ctx& c, const QInfo& q) {
     if (c.uq_size >= c.L->cap_uq) {
         fail(c, K10S_ERR_QUEUE_FULL);
         return;
@@ -218,7 +218,7 @@ K10S_HD bool pod_in_s(const Ctx& c, uint32_t p) { return (c.v.pod(p).flags & PF_
 // move_pods_to_active_queue over a selection, in key order (scheduler.rs:174-185)
 // mode 0: all (move_all_to_active_queue, 235-244); 1: flush (188-203, stay > 300 s);
 // 2: freed-resources conditional (366-379); 3: inverted add-node conditional (396-405).
-K10S_HD void s_move(Ctx& c, int mode, double t, uint32_t cpu, uint64_t ram) {
+K10S_HELPER void s_move(Ctx& c, int mode, double t, uint32_t cpu, uint64_t ram) {
     QInfo* d = c.v.uq();
     uint32_t n = c.uq_size;
     uint32_t w = 0;
@@ -527,7 +527,7 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
 // info is a snapshot of PS state at that instant, and the CA's node-group state is only touched
 // by autoscale() while exactly one request is in flight, so deciding at snapshot time and
 // emitting the actions at delivery time (cluster_autoscaler.rs:309-331) is equivalent.
-K10S_HD void ca_decide(Ctx& c) {
+K10S_COLD void ca_decide(Ctx& c) {
     RepHdr* h = c.v.h();
     const Scenario* sc = c.sc;
     h->ca_n_act = 0;
@@ -681,7 +681,7 @@ K10S_HD void ps_clean_up(Ctx& c, uint32_t p) {  // 173-182
     }
 }
 
-K10S_HD void on_ps(Ctx& c, const HeapEv& e) {
+K10S_WARM void on_ps(Ctx& c, const HeapEv& e) {
     RepHdr* h = c.v.h();
     const Params* pr = c.pr;
     switch (e.kind) {
@@ -831,7 +831,7 @@ K10S_HD void on_ps(Ctx& c, const HeapEv& e) {
 }
 
 // ---- api server (api_server.rs:127-457) --------------------------------------------------------
-K10S_HD void on_api_server(Ctx& c, const HeapEv& e) {
+K10S_WARM void on_api_server(Ctx& c, const HeapEv& e) {
     RepHdr* h = c.v.h();
     const Params* pr = c.pr;
     const Scenario* sc = c.sc;
@@ -991,7 +991,7 @@ K10S_HD void on_api_server(Ctx& c, const HeapEv& e) {
 }
 
 // ---- node components (node_component.rs:178-335) ------------------------------------------------
-K10S_HD void on_node(Ctx& c, const HeapEv& e) {
+K10S_WARM void on_node(Ctx& c, const HeapEv& e) {
     const Params* pr = c.pr;
     int32_t slot = e.slot;
     switch (e.kind) {
@@ -1074,7 +1074,7 @@ K10S_HD void on_node(Ctx& c, const HeapEv& e) {
 }
 
 // ---- cluster autoscaler proxy (cluster_autoscaler.rs:230-334) --------------------------------
-K10S_HD void on_ca(Ctx& c, const HeapEv& e) {
+K10S_COLD void on_ca(Ctx& c, const HeapEv& e) {
     RepHdr* h = c.v.h();
     const Params* pr = c.pr;
     if (e.kind == K10S_EV_CA_TICK) {
@@ -1107,7 +1107,7 @@ K10S_HD uint32_t hpa_desired_by_metric(uint32_t cur, double value, double target
     return d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
 }
 
-K10S_HD void on_hpa(Ctx& c, const HeapEv& e) {
+K10S_COLD void on_hpa(Ctx& c, const HeapEv& e) {
     RepHdr* h = c.v.h();
     const Scenario* sc = c.sc;
     const uint32_t B = sc->group_bound;
@@ -1189,7 +1189,7 @@ K10S_HD double usage_poll(const Scenario* sc, uint8_t kind, double usage, uint32
     return fmin_rs(1.0, sc->unit_load[uoff + idx] / (double)count);
 }
 
-K10S_HD void on_metrics(Ctx& c, const HeapEv& e) {
+K10S_COLD void on_metrics(Ctx& c, const HeapEv& e) {
     if (e.kind == K10S_EV_M_GAUGE_TICK) {  // CSV gauge record: no simulation state (collector.rs:392-407)
         emit0(c, K10S_EV_M_GAUGE_TICK, 5.0);
         return;

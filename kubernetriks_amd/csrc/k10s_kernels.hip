@@ -16,6 +16,17 @@
 
 using namespace k10s;
 
+// Occupancy knob for the event-loop kernel (0 = compiler default).  amdgpu_waves_per_eu(n) caps
+// the register allocation so that n waves fit per SIMD.
+#ifndef K10S_WAVES_PER_EU
+#define K10S_WAVES_PER_EU 0
+#endif
+#if K10S_WAVES_PER_EU > 0
+#define K10S_RUN_BOUNDS __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(K10S_WAVES_PER_EU)))
+#else
+#define K10S_RUN_BOUNDS __launch_bounds__(64)
+#endif
+
 __global__ __launch_bounds__(64) void k10s_init_kernel(Scenario sc, const Params* __restrict__ params, Layout L,
                                                          uint8_t* base, uint32_t n_replicas) {
     uint32_t r = blockIdx.x;
@@ -24,7 +35,7 @@ __global__ __launch_bounds__(64) void k10s_init_kernel(Scenario sc, const Params
     init_replica(&sc, &p, &L, base, r);
 }
 
-__global__ __launch_bounds__(64) void k10s_run_kernel(Scenario sc, const Params* __restrict__ params, Layout L,
+__global__ K10S_RUN_BOUNDS void k10s_run_kernel(Scenario sc, const Params* __restrict__ params, Layout L,
                                                         uint8_t* base, uint32_t n_replicas, int mode, double until_time,
                                                         double max_time, uint64_t budget, uint32_t* active) {
     uint32_t r = blockIdx.x;

@@ -101,7 +101,7 @@ K10S_HD void est_reset(Estimator& e) {
     e.avg = 0.0;
     e.sum2 = 0.0;
 }
-K10S_HD void est_add(Estimator& e, double x) {
+K10S_HELPER void est_add(Estimator& e, double x) {
     e.mn = fmin_rs(e.mn, x);
     e.mx = fmax_rs(e.mx, x);
     e.n += 1;

@@ -12,7 +12,7 @@ import os
 from typing import Dict, List, Optional, Sequence
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(REPO, "build", "libk10s.so")
+LIB_PATH = os.environ.get("K10S_LIB") or os.path.join(REPO, "build", "libk10s.so")
 
 NUM_COUNTERS = 16
 COUNTER_NAMES = [
