@@ -149,11 +149,14 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
-    statuses = {}
+    statuses, errors = {}, {}
     for r in eng.raw_results():
         statuses[r.status] = statuses.get(r.status, 0) + 1
+        if r.status == 2:
+            key = f"{r.error_code}@kind{r.error_kind}"
+            errors[key] = errors.get(key, 0) + 1
     if statuses.get(2):
-        log(f"[rank {rank}] WARNING: {statuses[2]} replicas ended in error")
+        log(f"[rank {rank}] WARNING: {statuses[2]} replicas ended in error: {errors}")
 
     tvec = torch.tensor([elapsed, sum(kernel_ms) / len(kernel_ms)], dtype=torch.float64, device="cuda")
     cvec = torch.tensor(counters, dtype=torch.float64, device="cuda")
@@ -200,7 +203,7 @@ def main():
                      "kernel": "k10s_run_kernel", "kernel_ms_per_launch": mean_kernel_ms,
                      "algorithmic_bytes_per_launch": per_launch_bytes},
         "totals": {"placements": placements, "attempts": attempts, "events": events, "nodes_scanned": scanned,
-                   "replica_status": {str(k): v for k, v in statuses.items()}},
+                   "replica_status": {str(k): v for k, v in statuses.items()}, "replica_errors": errors},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

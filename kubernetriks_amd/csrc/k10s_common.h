@@ -30,7 +30,7 @@
 // handlers (autoscalers, metrics) out of line, >= 2 also the api-server / storage / node handlers,
 // >= 3 also the queue/heap helpers, so the hot loop's register allocation is not sized by them.
 #ifndef K10S_SPLIT
-#define K10S_SPLIT 1
+#define K10S_SPLIT 2
 #endif
 // K10S_COLD / K10S_WARM / K10S_HELPER: function qualifiers following K10S_SPLIT
 #if K10S_SPLIT >= 1

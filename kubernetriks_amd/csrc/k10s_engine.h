@@ -23,6 +23,7 @@ namespace k10s {
 struct Ctx {
     const Scenario* sc;
     const Params* pr;
+    RepHdr* h;   // working copy of the replica header (LDS on the device for the launch)
     Rep v;
     const Layout* L;
     double clock;
@@ -34,10 +35,10 @@ struct Ctx {
 K10S_HD void fail(Ctx& c, uint32_t code) {
     if (c.err == 0) {
         c.err = code;
-        c.v.h()->error_code = code;
-        c.v.h()->error_kind = c.cur_kind;
-        c.v.h()->error_seq = c.cur_seq;
-        c.v.h()->error_time = c.clock;
+        c.h->error_code = code;
+        c.h->error_kind = c.cur_kind;
+        c.h->error_seq = c.cur_seq;
+        c.h->error_time = c.clock;
     }
 }
 
@@ -67,6 +68,11 @@ K10S_HD bool ev_before(double ta, uint32_t sa, double tb, uint32_t sb) {
     return ka < kb || (ka == kb && sa < sb);
 }
 
+// The dslab queue as an 8-ary min-heap of 32-B events.  Ids are unique, so every arity pops the
+// same (time, id) order; 8-ary cuts the dependent load chain of a pop to ~log8(n) levels, and the
+// 8 children of a level (256 contiguous bytes) are loaded and compared by 8 lanes at once.
+#define K10S_HEAP_D 8
+
 K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uint32_t a, uint32_t b, double x) {
     if (c.err) return 0;
     if (c.next_seq == 0xFFFFFFFFu) {
@@ -89,7 +95,7 @@ K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uin
     uint32_t pos = c.heap_size++;
     int64_t k = total_key(e.time);
     while (pos > 0) {
-        uint32_t parent = (pos - 1) >> 1;
+        uint32_t parent = (pos - 1) / K10S_HEAP_D;
         HeapEv p = hp[parent];
         int64_t kp = total_key(p.time);
         if (!(k < kp || (k == kp && e.seq < p.seq))) break;
@@ -101,6 +107,52 @@ K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uin
 }
 K10S_HD uint32_t emit0(Ctx& c, uint32_t kind, double delay) { return emit(c, kind, delay, -1, 0, 0, 0.0); }
 
+// Smallest (time, id) among children [first, min(first + D, n)); returns its index.
+K10S_HD uint32_t heap_min_child(const HeapEv* hp, uint32_t first, uint32_t n, int64_t& kmin, uint32_t& smin) {
+#if K10S_DEVICE
+    const int lane = lane_id();
+    uint32_t i = first + (uint32_t)(lane & (K10S_HEAP_D - 1));
+    int64_t k = 0x7FFFFFFFFFFFFFFFll;
+    uint32_t sq = 0xFFFFFFFFu;
+    if (lane < K10S_HEAP_D && i < n) {
+        k = total_key(hp[i].time);
+        sq = hp[i].seq;
+    }
+#pragma unroll
+    for (int m = K10S_HEAP_D / 2; m >= 1; m >>= 1) {
+        int64_t ok = (int64_t)shfl_xor_u64((uint64_t)k, m);
+        uint32_t os = (uint32_t)__shfl_xor((int)sq, m, 64);
+        uint32_t oi = (uint32_t)__shfl_xor((int)i, m, 64);
+        if (ok < k || (ok == k && os < sq)) {
+            k = ok;
+            sq = os;
+            i = oi;
+        }
+    }
+    // lanes 0..D-1 now agree; broadcast lane 0's result to the whole wave
+    kmin = (int64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)k) |
+           ((int64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)k >> 32)) << 32);
+    smin = (uint32_t)__builtin_amdgcn_readfirstlane((int)sq);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
+#else
+    uint32_t best = first;
+    int64_t kb = total_key(hp[first].time);
+    uint32_t sb = hp[first].seq;
+    uint32_t end = first + K10S_HEAP_D < n ? first + K10S_HEAP_D : n;
+    for (uint32_t i = first + 1; i < end; i++) {
+        int64_t k = total_key(hp[i].time);
+        if (k < kb || (k == kb && hp[i].seq < sb)) {
+            kb = k;
+            sb = hp[i].seq;
+            best = i;
+        }
+    }
+    kmin = kb;
+    smin = sb;
+    return best;
+#endif
+}
+
 K10S_HELPER void heap_pop(Ctx& c) {
     HeapEv* hp = c.v.heap();
     uint32_t n = --c.heap_size;
@@ -109,25 +161,13 @@ K10S_HELPER void heap_pop(Ctx& c) {
     int64_t kl = total_key(last.time);
     uint32_t pos = 0;
     for (;;) {
-        uint32_t l = 2 * pos + 1;
-        if (l >= n) break;
-        uint32_t r = l + 1;
-        uint32_t m = l;
-        HeapEv cl = hp[l];
-        int64_t km = total_key(cl.time);
-        uint32_t sm = cl.seq;
-        if (r < n) {
-            HeapEv cr = hp[r];
-            int64_t kr = total_key(cr.time);
-            if (kr < km || (kr == km && cr.seq < sm)) {
-                m = r;
-                km = kr;
-                sm = cr.seq;
-                cl = cr;
-            }
-        }
+        uint32_t first = K10S_HEAP_D * pos + 1;
+        if (first >= n) break;
+        int64_t km;
+        uint32_t sm;
+        uint32_t m = heap_min_child(hp, first, n, km, sm);
         if (!(km < kl || (km == kl && sm < last.seq))) break;
-        hp[pos] = cl;
+        hp[pos] = hp[m];
         pos = m;
     }
     hp[pos] = last;
@@ -295,33 +335,57 @@ K10S_HD double la_score(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr) {
     return (cpu_score + ram_score) / 2.0;
 }
 
-// Returns K10S_SCHED_* and writes the chosen node index.  Wave-parallel over node indices
-// (name order): lane l visits n = l, l+64, ...; per-lane "score >= best" keeps the last
-// maximum; the cross-lane (key, n) max reproduces the reference's left-to-right argmax.
+// Returns K10S_SCHED_* and writes the chosen node index.  Wave-parallel over node indices (name
+// order): each lane owns 4 consecutive nodes per 256-node step (one 16-B cpu load + two 16-B ram
+// loads), keeps "score >= best" (the last maximum) over its nodes in ascending order, and the
+// cross-lane (key, n) max reproduces the reference's left-to-right argmax.
+// Requires s_cpu / s_ram 16-B aligned (node arrays start on 256-B boundaries).
+K10S_HD void scan_node(uint32_t n, uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr, double weight, int32_t& first,
+                       uint64_t& best_key, int32_t& best_n) {
+    if (rc <= ac && rr <= ar) {
+        if ((int32_t)n < first) first = (int32_t)n;
+        double s = 0.0 + la_score(ac, ar, rc, rr) * weight;
+        if (!is_nan(s)) {
+            uint64_t k = score_key(s);
+            if (k >= best_key) {
+                best_key = k;
+                best_n = (int32_t)n;
+            }
+        }
+    }
+}
+
 K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
                           uint32_t rc, uint64_t rr, double weight, int32_t* chosen) {
-    const int lane = lane_id();
     uint64_t best_key = 0;
     int32_t best_n = -1;
     int32_t first = 0x7fffffff;
-    for (uint32_t base = 0; base < n_nodes; base += K10S_LANES) {
-        uint32_t n = base + (uint32_t)lane;
-        if (n < n_nodes && ((present[n >> 6] >> (n & 63)) & 1ull)) {
-            uint32_t ac = s_cpu[n];
-            uint64_t ar = s_ram[n];
-            if (rc <= ac && rr <= ar) {
-                if ((int32_t)n < first) first = (int32_t)n;
-                double s = 0.0 + la_score(ac, ar, rc, rr) * weight;
-                if (!is_nan(s)) {
-                    uint64_t k = score_key(s);
-                    if (k >= best_key) {
-                        best_key = k;
-                        best_n = (int32_t)n;
-                    }
+#if K10S_DEVICE
+    const uint32_t lane = (uint32_t)lane_id();
+    for (uint32_t base = 0; base < n_nodes; base += 256) {
+        uint32_t n0 = base + 4 * lane;
+        if (n0 < n_nodes) {
+            uint32_t bits = (uint32_t)(present[n0 >> 6] >> (n0 & 63)) & 0xFu;
+            if (bits) {
+                if (n0 + 4 <= n_nodes) {
+                    uint4 cv = *reinterpret_cast<const uint4*>(s_cpu + n0);
+                    ulonglong2 r01 = *reinterpret_cast<const ulonglong2*>(s_ram + n0);
+                    ulonglong2 r23 = *reinterpret_cast<const ulonglong2*>(s_ram + n0 + 2);
+                    if (bits & 1u) scan_node(n0, cv.x, r01.x, rc, rr, weight, first, best_key, best_n);
+                    if (bits & 2u) scan_node(n0 + 1, cv.y, r01.y, rc, rr, weight, first, best_key, best_n);
+                    if (bits & 4u) scan_node(n0 + 2, cv.z, r23.x, rc, rr, weight, first, best_key, best_n);
+                    if (bits & 8u) scan_node(n0 + 3, cv.w, r23.y, rc, rr, weight, first, best_key, best_n);
+                } else {
+                    for (uint32_t j = 0; j < 4 && n0 + j < n_nodes; j++)
+                        if (bits & (1u << j)) scan_node(n0 + j, s_cpu[n0 + j], s_ram[n0 + j], rc, rr, weight, first, best_key, best_n);
                 }
             }
         }
     }
+#else
+    for (uint32_t n = 0; n < n_nodes; n++)
+        if ((present[n >> 6] >> (n & 63)) & 1ull) scan_node(n, s_cpu[n], s_ram[n], rc, rr, weight, first, best_key, best_n);
+#endif
     first = wave_min_i32(first);
     wave_argmax(best_key, best_n);
     if (first == 0x7fffffff) return K10S_SCHED_NO_SUFFICIENT_RESOURCES;
@@ -334,7 +398,7 @@ K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const ui
 // ---- scheduling cycle (scheduler.rs:246-334) ----------------------------------------------------
 K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
     double cycle_dur = 0.0;
-    RepHdr* h = c.v.h();
+    RepHdr* h = c.h;
     const double w = c.pr->score_weight;
     while (c.aq_size > 0 && !c.err) {
         QInfo q = aq_pop(c);
@@ -425,7 +489,7 @@ K10S_HD void s_release(Ctx& c, uint32_t p) {  // release_node_resources (153-162
 }
 
 K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
-    RepHdr* h = c.v.h();
+    RepHdr* h = c.h;
     switch (e.kind) {
     case K10S_EV_S_RUN_CYCLE:
         run_scheduling_cycle(c, e.time);
@@ -528,7 +592,7 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
 // by autoscale() while exactly one request is in flight, so deciding at snapshot time and
 // emitting the actions at delivery time (cluster_autoscaler.rs:309-331) is equivalent.
 K10S_COLD void ca_decide(Ctx& c) {
-    RepHdr* h = c.v.h();
+    RepHdr* h = c.h;
     const Scenario* sc = c.sc;
     h->ca_n_act = 0;
     uint32_t* cag = c.v.cag();
@@ -682,7 +746,7 @@ K10S_HD void ps_clean_up(Ctx& c, uint32_t p) {  // 173-182
 }
 
 K10S_WARM void on_ps(Ctx& c, const HeapEv& e) {
-    RepHdr* h = c.v.h();
+    RepHdr* h = c.h;
     const Params* pr = c.pr;
     switch (e.kind) {
     case K10S_EV_PS_CREATE_NODE_REQ: {
@@ -832,7 +896,7 @@ K10S_WARM void on_ps(Ctx& c, const HeapEv& e) {
 
 // ---- api server (api_server.rs:127-457) --------------------------------------------------------
 K10S_WARM void on_api_server(Ctx& c, const HeapEv& e) {
-    RepHdr* h = c.v.h();
+    RepHdr* h = c.h;
     const Params* pr = c.pr;
     const Scenario* sc = c.sc;
     switch (e.kind) {
@@ -1075,7 +1139,7 @@ K10S_WARM void on_node(Ctx& c, const HeapEv& e) {
 
 // ---- cluster autoscaler proxy (cluster_autoscaler.rs:230-334) --------------------------------
 K10S_COLD void on_ca(Ctx& c, const HeapEv& e) {
-    RepHdr* h = c.v.h();
+    RepHdr* h = c.h;
     const Params* pr = c.pr;
     if (e.kind == K10S_EV_CA_TICK) {
         h->ca_last_cycle_time = e.time;
@@ -1108,7 +1172,7 @@ K10S_HD uint32_t hpa_desired_by_metric(uint32_t cur, double value, double target
 }
 
 K10S_COLD void on_hpa(Ctx& c, const HeapEv& e) {
-    RepHdr* h = c.v.h();
+    RepHdr* h = c.h;
     const Scenario* sc = c.sc;
     const uint32_t B = sc->group_bound;
     const uint32_t words = c.L->words_group;
@@ -1328,6 +1392,7 @@ K10S_HD void init_replica(const Scenario* sc, const Params* pr, const Layout* L,
     Ctx c;
     c.sc = sc;
     c.pr = pr;
+    c.h = h;
     c.v = v;
     c.L = L;
     c.clock = 0.0;
@@ -1358,14 +1423,17 @@ K10S_HD void init_replica(const Scenario* sc, const Params* pr, const Layout* L,
 
 // ---- the event loop -----------------------------------------------------------------------------
 // Returns 1 if the replica still has work (event budget exhausted), else 0.
+// `h` is the working copy of replica r's header: the device kernel stages it in LDS for the
+// launch (every counter / estimator / queue-size update on the serial path is then an LDS access)
+// and writes it back afterwards; the host check build passes the header in place.
 K10S_HD int run_replica(const Scenario* sc, const Params* pr, const Layout* L, uint8_t* base, uint32_t r, int mode,
-                        double until_time, double max_time, uint64_t budget) {
+                        double until_time, double max_time, uint64_t budget, RepHdr* h) {
     Rep v = make_rep(base, *L, r);
-    RepHdr* h = v.h();
     if (h->status != K10S_REPLICA_RUNNING) return 0;
     Ctx c;
     c.sc = sc;
     c.pr = pr;
+    c.h = h;
     c.v = v;
     c.L = L;
     c.clock = h->clock;

@@ -41,7 +41,17 @@ __global__ K10S_RUN_BOUNDS void k10s_run_kernel(Scenario sc, const Params* __res
     uint32_t r = blockIdx.x;
     if (r >= n_replicas) return;
     Params p = params[r];
-    int more = run_replica(&sc, &p, &L, base, r, mode, until_time, max_time, budget);
+    // stage the replica header in LDS for the whole launch
+    __shared__ RepHdr hdr;
+    constexpr uint32_t W = sizeof(RepHdr) / 4;
+    static_assert(sizeof(RepHdr) % 4 == 0, "RepHdr must be a whole number of dwords");
+    uint32_t* g = reinterpret_cast<uint32_t*>(base + (uint64_t)r * L.stride + L.hdr);
+    uint32_t* s = reinterpret_cast<uint32_t*>(&hdr);
+    for (uint32_t i = threadIdx.x; i < W; i += 64) s[i] = g[i];
+    __syncthreads();
+    int more = run_replica(&sc, &p, &L, base, r, mode, until_time, max_time, budget, &hdr);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < W; i += 64) g[i] = s[i];
     if (more && threadIdx.x == 0) atomicAdd(active, 1u);
 }
 

@@ -66,7 +66,8 @@ int hc_run(void* p, int mode, double until, double max_time, uint64_t budget) {
     HC* h = (HC*)p;
     int active = 0;
     for (uint32_t r = 0; r < h->R; r++) {
-        while (run_replica(&h->sc, &h->params[r], &h->L, h->state.data(), r, mode, until, max_time, budget)) {
+        Rep v = make_rep(h->state.data(), h->L, r);
+        while (run_replica(&h->sc, &h->params[r], &h->L, h->state.data(), r, mode, until, max_time, budget, v.h())) {
         }
     }
     return active;
