@@ -180,6 +180,21 @@ int32_t k10s_schedule_one_batch(const uint32_t* alloc_cpu, const uint64_t* alloc
                                 uint32_t n_problems, int32_t* out_node, int32_t* out_status,
                                 void* stream);
 
+/* (1') Host-buffer form of (1) for hosts without HIP bindings (the Rust PodSchedulingAlgorithm
+ * adapter in INTEGRATION.md): a handle owns device buffers for up to max_problems problems of up
+ * to max_nodes nodes.  k10s_scheduler_schedule takes HOST arrays — problem r's nodes are
+ * alloc_cpu/alloc_ram[r*n_nodes .. r*n_nodes + n_nodes) in name order; present_bits (may be NULL
+ * = every node present) holds ceil(n_nodes/64) words per problem — copies them to the device,
+ * runs the same kernel as (1) and blocks until out_node/out_status (host, [n_problems]) are
+ * written.  PCIe-inclusive; meant for one cycle's worth of pods, not for throughput. */
+typedef struct k10s_scheduler k10s_scheduler;
+k10s_scheduler* k10s_scheduler_create(uint32_t max_nodes, uint32_t max_problems, int32_t device);
+void k10s_scheduler_destroy(k10s_scheduler* s);
+int32_t k10s_scheduler_schedule(k10s_scheduler* s, const uint32_t* alloc_cpu, const uint64_t* alloc_ram,
+                                const uint64_t* present_bits, uint32_t n_nodes, const uint32_t* req_cpu,
+                                const uint64_t* req_ram, double weight, uint32_t n_problems, int32_t* out_node,
+                                int32_t* out_status);
+
 /* (2) -------------------------------------------------------------------------------------- */
 typedef struct k10s_engine k10s_engine;
 

@@ -95,6 +95,108 @@ int32_t k10s_schedule_one_batch(const uint32_t* alloc_cpu, const uint64_t* alloc
     return K10S_OK;
 }
 
+}  // extern "C"
+
+struct k10s_scheduler {
+    int device = 0;
+    uint32_t max_nodes = 0, max_problems = 0, stride = 0;
+    hipStream_t stream = nullptr;
+    uint32_t* d_cpu = nullptr;
+    uint64_t* d_ram = nullptr;
+    uint64_t* d_bits = nullptr;
+    uint32_t* d_rc = nullptr;
+    uint64_t* d_rr = nullptr;
+    int32_t* d_out = nullptr;  // [2 * max_problems]: node, status
+};
+
+static void scheduler_free(k10s_scheduler* s) {
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    for (void* p : {(void*)s->d_cpu, (void*)s->d_ram, (void*)s->d_bits, (void*)s->d_rc, (void*)s->d_rr, (void*)s->d_out})
+        if (p) (void)hipFree(p);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    delete s;
+}
+
+static int32_t scheduler_alloc(k10s_scheduler* s) {
+    HIPCHK(hipSetDevice(s->device));
+    HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    const uint64_t cells = (uint64_t)s->stride * s->max_problems;
+    HIPCHK(hipMalloc(&s->d_cpu, 4 * cells));
+    HIPCHK(hipMalloc(&s->d_ram, 8 * cells));
+    HIPCHK(hipMalloc(&s->d_bits, cells / 8));
+    HIPCHK(hipMalloc(&s->d_rc, 4ull * s->max_problems));
+    HIPCHK(hipMalloc(&s->d_rr, 8ull * s->max_problems));
+    HIPCHK(hipMalloc(&s->d_out, 8ull * s->max_problems));
+    return K10S_OK;
+}
+
+extern "C" {
+
+k10s_scheduler* k10s_scheduler_create(uint32_t max_nodes, uint32_t max_problems, int32_t device) {
+    if (max_nodes == 0 || max_problems == 0) {
+        set_err(K10S_E_INVALID, "max_nodes and max_problems must be > 0");
+        return nullptr;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        set_err(K10S_E_NO_DEVICE, "no HIP device: the k10s scheduler runs only on the GPU");
+        return nullptr;
+    }
+    if (device < 0 || device >= ndev) {
+        set_err(K10S_E_INVALID, "device index out of range");
+        return nullptr;
+    }
+    auto* s = new k10s_scheduler();
+    s->device = device;
+    s->max_nodes = max_nodes;
+    s->max_problems = max_problems;
+    s->stride = (max_nodes + 63) / 64 * 64;
+    if (scheduler_alloc(s) != K10S_OK) {
+        std::string m = g_err;
+        scheduler_free(s);
+        set_err(K10S_E_CAPACITY, m);
+        return nullptr;
+    }
+    return s;
+}
+
+void k10s_scheduler_destroy(k10s_scheduler* s) { scheduler_free(s); }
+
+int32_t k10s_scheduler_schedule(k10s_scheduler* s, const uint32_t* alloc_cpu, const uint64_t* alloc_ram,
+                                const uint64_t* present_bits, uint32_t n_nodes, const uint32_t* req_cpu,
+                                const uint64_t* req_ram, double weight, uint32_t n_problems, int32_t* out_node,
+                                int32_t* out_status) {
+    if (!s) return set_err(K10S_E_INVALID, "null scheduler");
+    if (n_problems == 0) return K10S_OK;
+    if (!alloc_cpu || !alloc_ram || !req_cpu || !req_ram || !out_node || !out_status)
+        return set_err(K10S_E_INVALID, "null pointer");
+    if (n_nodes > s->max_nodes || n_problems > s->max_problems)
+        return set_err(K10S_E_CAPACITY, "n_nodes/n_problems exceed the scheduler's capacity");
+    HIPCHK(hipSetDevice(s->device));
+    const uint32_t words = (n_nodes + 63) / 64, dwords = s->stride / 64;
+    if (n_nodes > 0) {
+        HIPCHK(hipMemcpy2DAsync(s->d_cpu, 4ull * s->stride, alloc_cpu, 4ull * n_nodes, 4ull * n_nodes, n_problems,
+                                hipMemcpyHostToDevice, s->stream));
+        HIPCHK(hipMemcpy2DAsync(s->d_ram, 8ull * s->stride, alloc_ram, 8ull * n_nodes, 8ull * n_nodes, n_problems,
+                                hipMemcpyHostToDevice, s->stream));
+        if (present_bits) {
+            HIPCHK(hipMemcpy2DAsync(s->d_bits, 8ull * dwords, present_bits, 8ull * words, 8ull * words, n_problems,
+                                    hipMemcpyHostToDevice, s->stream));
+        } else {
+            HIPCHK(hipMemsetAsync(s->d_bits, 0xFF, 8ull * dwords * n_problems, s->stream));
+        }
+    }
+    HIPCHK(hipMemcpyAsync(s->d_rc, req_cpu, 4ull * n_problems, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(hipMemcpyAsync(s->d_rr, req_ram, 8ull * n_problems, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(k10s_launch_schedule(s->d_cpu, s->d_ram, s->d_bits, n_nodes, s->stride, s->d_rc, s->d_rr, weight, n_problems,
+                                s->d_out, s->d_out + s->max_problems, s->stream));
+    HIPCHK(hipMemcpyAsync(out_node, s->d_out, 4ull * n_problems, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipMemcpyAsync(out_status, s->d_out + s->max_problems, 4ull * n_problems, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return K10S_OK;
+}
+
 k10s_engine* k10s_engine_create(const char* scenario_text, const k10s_replica_params* params, uint32_t n_replicas,
                                 const k10s_capacities* caps, int32_t device) {
     if (!scenario_text || n_replicas == 0) {

@@ -235,6 +235,12 @@ def lib():
         L.k10s_schedule_one_batch.restype = ctypes.c_int32
         L.k10s_schedule_one_batch.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint32, ctypes.c_uint32] + \
             [ctypes.c_void_p] * 2 + [ctypes.c_double, ctypes.c_uint32] + [ctypes.c_void_p] * 3
+        L.k10s_scheduler_create.restype = ctypes.c_void_p
+        L.k10s_scheduler_create.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int32]
+        L.k10s_scheduler_destroy.argtypes = [ctypes.c_void_p]
+        L.k10s_scheduler_schedule.restype = ctypes.c_int32
+        L.k10s_scheduler_schedule.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint32] + [ctypes.c_void_p] * 2 + \
+            [ctypes.c_double, ctypes.c_uint32] + [ctypes.c_void_p] * 2
         _lib = L
     return _lib
 
@@ -288,6 +294,50 @@ class Engine(EngineBase):
 
     def sync(self):
         self._check(self._L.k10s_engine_sync(self._h))
+
+
+class Scheduler:
+    """Host-buffer schedule_one surface (k10s_scheduler_*): R problems of n_nodes name-ordered
+    nodes each, numpy in / numpy out.  Mirrors PodSchedulingAlgorithm::schedule_one
+    (src/core/scheduler/interface.rs:14-23) with node indices instead of names."""
+
+    def __init__(self, max_nodes: int, max_problems: int, device: int = 0):
+        L = lib()
+        self._L = L
+        h = L.k10s_scheduler_create(max_nodes, max_problems, device)
+        if not h:
+            raise RuntimeError("k10s_scheduler_create failed: " + L.k10s_last_error().decode())
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.k10s_scheduler_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def schedule(self, alloc_cpu, alloc_ram, req_cpu, req_ram, present_bits=None, weight: float = 1.0):
+        """alloc_cpu u32[R, N], alloc_ram u64[R, N], req_* [R], present_bits u64[R, ceil(N/64)] or None.
+        Returns (node_idx i32[R] (-1 on error), status i32[R] = K10S_SCHED_*)."""
+        import numpy as np
+        cpu = np.ascontiguousarray(alloc_cpu, dtype=np.uint32)
+        ram = np.ascontiguousarray(alloc_ram, dtype=np.uint64)
+        R, N = cpu.shape
+        rc = np.ascontiguousarray(req_cpu, dtype=np.uint32)
+        rr = np.ascontiguousarray(req_ram, dtype=np.uint64)
+        bits = None if present_bits is None else np.ascontiguousarray(present_bits, dtype=np.uint64)
+        if ram.shape != (R, N) or rc.shape != (R,) or rr.shape != (R,) or \
+                (bits is not None and bits.shape != (R, (N + 63) // 64)):
+            raise ValueError("shape mismatch")
+        out_n = np.empty(R, dtype=np.int32)
+        out_s = np.empty(R, dtype=np.int32)
+        rcode = self._L.k10s_scheduler_schedule(self._h, cpu.ctypes.data, ram.ctypes.data,
+                                                None if bits is None else bits.ctypes.data, N, rc.ctypes.data,
+                                                rr.ctypes.data, weight, R, out_n.ctypes.data, out_s.ctypes.data)
+        if rcode != 0:
+            raise RuntimeError(f"k10s_scheduler_schedule: {rcode}: " + self._L.k10s_last_error().decode())
+        return out_n, out_s
 
 
 def version() -> str:

@@ -180,3 +180,40 @@ def test_schedule_one_batch_matches_oracle():
         assert got_s[r] == st, r
         if st == 0:
             assert nodes[got_n[r]][0] == name, r
+
+
+@pytest.mark.gpu
+def test_host_buffer_scheduler_matches_oracle():
+    """k10s_scheduler_schedule (host arrays, the Rust adapter's surface) vs the oracle."""
+    import numpy as np
+    from kubernetriks_amd.native import Scheduler
+    rng = random.Random(23)
+    R, N = 257, 130
+    cpu = np.zeros((R, N), np.uint32)
+    ram = np.zeros((R, N), np.uint64)
+    bits = np.zeros((R, (N + 63) // 64), np.uint64)
+    rc = np.zeros(R, np.uint32)
+    rr = np.zeros(R, np.uint64)
+    problems = []
+    for r in range(R):
+        nodes, pc, pr = _random_problem(rng, N if r % 5 else rng.randint(0, 3))
+        problems.append((nodes, pc, pr))
+        for i, (_, c_, r_, p_) in enumerate(nodes):
+            cpu[r, i], ram[r, i] = c_, r_
+            if p_:
+                bits[r, i // 64] |= np.uint64(1 << (i % 64))
+        rc[r], rr[r] = pc, pr
+    s = Scheduler(N, R)
+    got_n, got_s = s.schedule(cpu, ram, rc, rr, bits)
+    for r, (nodes, pc, pr) in enumerate(problems):
+        present = [(nm, c_, r_) for nm, c_, r_, p_ in nodes if p_]
+        st, name = ob.schedule_one(present, pc, pr)
+        assert got_s[r] == st, r
+        if st == 0:
+            assert nodes[got_n[r]][0] == name, r
+    # present_bits=None: every node in the cache
+    nodes, pc, pr = problems[1]
+    n1, s1 = s.schedule(cpu[1:2], ram[1:2], rc[1:2], rr[1:2], None)
+    st, name = ob.schedule_one([(nm, c_, r_) for nm, c_, r_, _ in nodes], pc, pr)
+    assert s1[0] == st and (st != 0 or nodes[n1[0]][0] == name)
+    s.close()
