@@ -130,8 +130,9 @@ K10S_HD uint32_t heap_min_child(const HeapEv* hp, uint32_t first, uint32_t n, in
         }
     }
     // lanes 0..D-1 now agree; broadcast lane 0's result to the whole wave
-    kmin = (int64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)k) |
-           ((int64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)k >> 32)) << 32);
+    const uint64_t klo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)k);
+    const uint64_t khi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)k >> 32));
+    kmin = (int64_t)(klo | (khi << 32));
     smin = (uint32_t)__builtin_amdgcn_readfirstlane((int)sq);
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
 #else
