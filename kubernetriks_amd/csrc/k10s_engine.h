@@ -20,26 +20,117 @@
 
 namespace k10s {
 
+// ---- where a replica's inputs and working header live ------------------------------------------
+// Device: the compiled scenario, the layout and the parameter/state base pointers of a launch sit
+// in __constant__ memory (k10s_dc; scalar loads, no pointer chains through scratch), and the
+// working replica header — clock, id counter, queue sizes, counters, estimators — is staged in LDS
+// (k10s_hdr) for the whole launch: one workgroup = one replica.  Host (test-only check build): the
+// same code reads them through the pointers held in Ctx.
+#if defined(__HIP__)
+__constant__ DevConst k10s_dc;
+__shared__ RepHdr k10s_hdr;
+#endif
+
+// Typed accessors over one replica's region; section bases are recomputed from the (constant)
+// layout at each use instead of being held live across the event loop.
+struct Rep {
+#if K10S_DEVICE
+    K10S_GB(uint8_t) b;
+    K10S_D const Layout& L() const { return k10s_dc.L; }
+#else
+    uint8_t* b;
+    const Layout* Lp;
+    const Layout& L() const { return *Lp; }
+#endif
+    template <typename T>
+    K10S_HD T* at(uint64_t off) const { return (T*)(b + off); }
+    K10S_HD RepHdr* h() const { return at<RepHdr>(L().hdr); }
+    K10S_HD uint32_t* s_cpu() const { return at<uint32_t>(L().s_cpu); }
+    K10S_HD uint64_t* s_ram() const { return at<uint64_t>(L().s_ram); }
+    K10S_HD uint64_t* s_present() const { return at<uint64_t>(L().s_present); }
+    K10S_HD NodeState& node(uint32_t n) const { return at<NodeState>(L().node)[n]; }
+    K10S_HD uint64_t* pend_rm() const { return at<uint64_t>(L().pend_rm); }
+    K10S_HD PodState& pod(uint32_t p) const { return at<PodState>(L().pod)[p]; }
+    K10S_HD k10s_pod_record* prec() const { return L().rec_on ? at<k10s_pod_record>(L().prec) : nullptr; }
+    K10S_HD SlotState& slot(int32_t s) const { return at<SlotState>(L().slot)[s]; }
+    K10S_HD uint32_t* pool_ring() const { return at<uint32_t>(L().pool_ring); }
+    K10S_HD GroupState* grp() const { return at<GroupState>(L().grp); }
+    K10S_HD uint64_t* grp_bits() const { return at<uint64_t>(L().grp_bits); }
+    K10S_HD uint32_t* cag() const { return at<uint32_t>(L().cag); }
+    K10S_HD CAAct* ca_act() const { return at<CAAct>(L().ca_act); }
+    K10S_HD uint32_t* ca_cpu() const { return at<uint32_t>(L().ca_cpu); }
+    K10S_HD uint64_t* ca_ram() const { return at<uint64_t>(L().ca_ram); }
+    K10S_HD uint32_t* ca_undo() const { return at<uint32_t>(L().ca_undo); }
+    K10S_HD HeapEv* heap() const { return at<HeapEv>(L().heap); }
+    K10S_HD QInfo* aq() const { return at<QInfo>(L().aq); }
+    K10S_HD QInfo* uq() const { return at<QInfo>(L().uq); }
+    K10S_HD k10s_log_entry* log() const { return L().cap_log ? at<k10s_log_entry>(L().log) : nullptr; }
+    K10S_HD k10s_placement* place() const { return L().cap_place ? at<k10s_placement>(L().place) : nullptr; }
+};
+
+#if !K10S_DEVICE
+inline Rep make_rep(uint8_t* base, const Layout& L, uint32_t r) {
+    Rep v;
+    v.b = base + (uint64_t)r * L.stride;
+    v.Lp = &L;
+    return v;
+}
+#endif
+
+// The handlers' view of the current replica.  Mutable simulation registers (clock, next id, queue
+// sizes, trace cursor, sticky error) are fields of the working header H().
 struct Ctx {
+#if K10S_DEVICE
+    K10S_D const Scenario& S() const { return k10s_dc.sc; }
+    K10S_D const Params& P() const { return *(const Params*)(k10s_dc.params + blockIdx.x); }
+    K10S_D const Layout& Ly() const { return k10s_dc.L; }
+    K10S_D RepHdr& H() const { return k10s_hdr; }
+    K10S_D Rep V() const {
+        Rep v;
+        v.b = k10s_dc.base + (uint64_t)blockIdx.x * k10s_dc.L.stride;
+        return v;
+    }
+#else
     const Scenario* sc;
     const Params* pr;
-    RepHdr* h;   // working copy of the replica header (LDS on the device for the launch)
+    RepHdr* h;
     Rep v;
-    const Layout* L;
-    double clock;
-    uint32_t next_seq, heap_size, aq_size, uq_size, trace_cursor;
-    uint32_t err;
-    uint32_t cur_kind, cur_seq;
+    const Layout* Lp;
+    const Scenario& S() const { return *sc; }
+    const Params& P() const { return *pr; }
+    const Layout& Ly() const { return *Lp; }
+    RepHdr& H() const { return *h; }
+    Rep V() const { return v; }
+#endif
 };
 
 K10S_HD void fail(Ctx& c, uint32_t code) {
-    if (c.err == 0) {
-        c.err = code;
-        c.h->error_code = code;
-        c.h->error_kind = c.cur_kind;
-        c.h->error_seq = c.cur_seq;
-        c.h->error_time = c.clock;
+    RepHdr& h = c.H();
+    if (h.error_code == 0) {
+        h.error_code = code;
+        h.error_kind = h.cur_kind;
+        h.error_seq = h.cur_seq;
+        h.error_time = h.clock;
     }
+}
+
+// Broadcast an event loaded by vector loads to scalar registers: every field is wave-uniform by
+// construction, and saying so lets every address derived from it be computed on the scalar unit.
+K10S_HD void uniform_event(HeapEv& e) {
+#if K10S_DEVICE
+    uint64_t tb = f2u(e.time);
+    e.time = u2f(((uint64_t)uniform_u32((uint32_t)(tb >> 32)) << 32) | uniform_u32((uint32_t)tb));
+    e.seq = uniform_u32(e.seq);
+    uint32_t ks = uniform_u32((uint32_t)e.kind | ((uint32_t)(uint16_t)e.slot << 16));
+    e.kind = (uint16_t)ks;
+    e.slot = (int16_t)(ks >> 16);
+    e.a = uniform_u32(e.a);
+    e.b = uniform_u32(e.b);
+    uint64_t xb = f2u(e.x);
+    e.x = u2f(((uint64_t)uniform_u32((uint32_t)(xb >> 32)) << 32) | uniform_u32((uint32_t)xb));
+#else
+    (void)e;
+#endif
 }
 
 // ---- small helpers ---------------------------------------------------------------------------
@@ -74,25 +165,25 @@ K10S_HD bool ev_before(double ta, uint32_t sa, double tb, uint32_t sb) {
 #define K10S_HEAP_D 8
 
 K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uint32_t a, uint32_t b, double x) {
-    if (c.err) return 0;
-    if (c.next_seq == 0xFFFFFFFFu) {
+    if (c.H().error_code) return 0;
+    if (c.H().next_seq == 0xFFFFFFFFu) {
         fail(c, K10S_ERR_SEQ_OVERFLOW);
         return 0;
     }
-    if (c.heap_size >= c.L->cap_heap) {
+    if (c.H().heap_size >= c.Ly().cap_heap) {
         fail(c, K10S_ERR_HEAP_FULL);
         return 0;
     }
     HeapEv e;
-    e.time = c.clock + delay;
-    e.seq = c.next_seq++;
+    e.time = c.H().clock + delay;
+    e.seq = c.H().next_seq++;
     e.kind = (uint16_t)kind;
     e.slot = (int16_t)slot;
     e.a = a;
     e.b = b;
     e.x = x;
-    HeapEv* hp = c.v.heap();
-    uint32_t pos = c.heap_size++;
+    HeapEv* hp = c.V().heap();
+    uint32_t pos = c.H().heap_size++;
     int64_t k = total_key(e.time);
     while (pos > 0) {
         uint32_t parent = (pos - 1) / K10S_HEAP_D;
@@ -155,8 +246,8 @@ K10S_HD uint32_t heap_min_child(const HeapEv* hp, uint32_t first, uint32_t n, in
 }
 
 K10S_HELPER void heap_pop(Ctx& c) {
-    HeapEv* hp = c.v.heap();
-    uint32_t n = --c.heap_size;
+    HeapEv* hp = c.V().heap();
+    uint32_t n = --c.H().heap_size;
     if (n == 0) return;
     HeapEv last = hp[n];
     int64_t kl = total_key(last.time);
@@ -190,17 +281,17 @@ K10S_HD uint32_t aq_sift_up(QInfo* d, uint32_t start, uint32_t pos, const QInfo&
     return pos;
 }
 K10S_HELPER void aq_push(Ctx& c, const QInfo& q) {
-    if (c.aq_size >= c.L->cap_aq) {
+    if (c.H().aq_size >= c.Ly().cap_aq) {
         fail(c, K10S_ERR_QUEUE_FULL);
         return;
     }
-    uint32_t old = c.aq_size++;
-    aq_sift_up(c.v.aq(), 0, old, q);
+    uint32_t old = c.H().aq_size++;
+    aq_sift_up(c.V().aq(), 0, old, q);
 }
 K10S_HELPER QInfo aq_pop(Ctx& c) {
-    QInfo* d = c.v.aq();
-    QInfo item = d[--c.aq_size];
-    uint32_t end = c.aq_size;
+    QInfo* d = c.V().aq();
+    QInfo item = d[--c.H().aq_size];
+    uint32_t end = c.H().aq_size;
     if (end == 0) return item;
     QInfo top = d[0];
     // sift_down_to_bottom(0) with `item` in the hole, then sift_up(0, pos)
@@ -230,20 +321,20 @@ K10S_HD bool u_less(const QInfo& a, const QInfo& b) {
     return ka < kb || (ka == kb && a.pod < b.pod);
 }
 K10S_HELPER void uq_insert(Ctx& c, const QInfo& q) {
-    if (c.uq_size >= c.L->cap_uq) {
+    if (c.H().uq_size >= c.Ly().cap_uq) {
         fail(c, K10S_ERR_QUEUE_FULL);
         return;
     }
-    QInfo* d = c.v.uq();
-    uint32_t pos = c.uq_size++;
+    QInfo* d = c.V().uq();
+    uint32_t pos = c.H().uq_size++;
     while (pos > 0) {  // timestamps are almost always >= the tail: short backward walk
         QInfo prev = d[pos - 1];
         if (!u_less(q, prev)) {
             if (prev.pod == q.pod && total_key(prev.timestamp) == total_key(q.timestamp)) {
                 // BTreeMap::insert on an existing key replaces the value
                 d[pos - 1] = q;
-                for (uint32_t i = pos; i + 1 < c.uq_size; i++) d[i] = d[i + 1];
-                c.uq_size--;
+                for (uint32_t i = pos; i + 1 < c.H().uq_size; i++) d[i] = d[i + 1];
+                c.H().uq_size--;
                 return;
             }
             break;
@@ -254,14 +345,14 @@ K10S_HELPER void uq_insert(Ctx& c, const QInfo& q) {
     d[pos] = q;
 }
 
-K10S_HD bool pod_in_s(const Ctx& c, uint32_t p) { return (c.v.pod(p).flags & PF_IN_S) != 0; }
+K10S_HD bool pod_in_s(const Ctx& c, uint32_t p) { return (c.V().pod(p).flags & PF_IN_S) != 0; }
 
 // move_pods_to_active_queue over a selection, in key order (scheduler.rs:174-185)
 // mode 0: all (move_all_to_active_queue, 235-244); 1: flush (188-203, stay > 300 s);
 // 2: freed-resources conditional (366-379); 3: inverted add-node conditional (396-405).
 K10S_HELPER void s_move(Ctx& c, int mode, double t, uint32_t cpu, uint64_t ram) {
-    QInfo* d = c.v.uq();
-    uint32_t n = c.uq_size;
+    QInfo* d = c.V().uq();
+    uint32_t n = c.H().uq_size;
     uint32_t w = 0;
     uint32_t fc = cpu;
     uint64_t fr = ram;
@@ -283,8 +374,8 @@ K10S_HELPER void s_move(Ctx& c, int mode, double t, uint32_t cpu, uint64_t ram) 
         } else if (mode == 1) {
             sel = (t - q.timestamp) > 5.0 * 60.0;
         } else {
-            uint32_t rc = c.v.pod(q.pod).req_cpu;
-            uint64_t rr = c.v.pod(q.pod).req_ram;
+            uint32_t rc = c.V().pod(q.pod).req_cpu;
+            uint64_t rr = c.V().pod(q.pod).req_ram;
             if (rc <= fc && rr <= fr) {
                 fc -= rc;
                 fr -= rr;
@@ -296,37 +387,37 @@ K10S_HELPER void s_move(Ctx& c, int mode, double t, uint32_t cpu, uint64_t ram) 
         if (sel && pod_in_s(c, q.pod)) {
             q.attempts += 1;
             aq_push(c, q);
-            if (c.err) return;
+            if (c.H().error_code) return;
         } else {
             d[w++] = q;  // kept (not selected, or stale entry of a deleted pod)
         }
     }
-    c.uq_size = w;
+    c.H().uq_size = w;
 }
 K10S_HD void s_move_after_free(Ctx& c, uint32_t cpu, uint64_t ram) {
-    if (c.pr->enable_unscheduled_pods_conditional_move) s_move(c, 2, 0.0, cpu, ram);
+    if (c.P().enable_unscheduled_pods_conditional_move) s_move(c, 2, 0.0, cpu, ram);
     else s_move(c, 0, 0.0, 0, 0);
 }
 
 // ---- running-pod lists of node components ----------------------------------------------------
 K10S_HD void run_insert(Ctx& c, int32_t slot, uint32_t p) {
-    int32_t h = c.v.slot(slot).head;
-    c.v.pod(p).run_prev = -1;
-    c.v.pod(p).run_next = h;
-    if (h >= 0) c.v.pod(h).run_prev = (int32_t)p;
-    c.v.slot(slot).head = (int32_t)p;
-    c.v.pod(p).run_slot = slot;
+    int32_t h = c.V().slot(slot).head;
+    c.V().pod(p).run_prev = -1;
+    c.V().pod(p).run_next = h;
+    if (h >= 0) c.V().pod(h).run_prev = (int32_t)p;
+    c.V().slot(slot).head = (int32_t)p;
+    c.V().pod(p).run_slot = slot;
 }
 K10S_HD void run_remove(Ctx& c, uint32_t p) {
-    int32_t slot = c.v.pod(p).run_slot;
-    int32_t pr = c.v.pod(p).run_prev, nx = c.v.pod(p).run_next;
-    if (pr >= 0) c.v.pod(pr).run_next = nx;
-    else c.v.slot(slot).head = nx;
-    if (nx >= 0) c.v.pod(nx).run_prev = pr;
-    c.v.pod(p).run_slot = -1;
-    c.v.pod(p).finish_seq = 0;  // cancels a pending finish event (dslab cancel_event)
-    int32_t g = c.sc->pod_group[p];
-    if (g >= 0) c.v.grp()[g].running -= 1;
+    int32_t slot = c.V().pod(p).run_slot;
+    int32_t pr = c.V().pod(p).run_prev, nx = c.V().pod(p).run_next;
+    if (pr >= 0) c.V().pod(pr).run_next = nx;
+    else c.V().slot(slot).head = nx;
+    if (nx >= 0) c.V().pod(nx).run_prev = pr;
+    c.V().pod(p).run_slot = -1;
+    c.V().pod(p).finish_seq = 0;  // cancels a pending finish event (dslab cancel_event)
+    int32_t g = c.S().pod_group[p];
+    if (g >= 0) c.V().grp()[g].running -= 1;
 }
 
 // ---- schedule_one: Fit filter + LeastAllocated score + argmax (the hot scan) -------------------
@@ -399,9 +490,9 @@ K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const ui
 // ---- scheduling cycle (scheduler.rs:246-334) ----------------------------------------------------
 K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
     double cycle_dur = 0.0;
-    RepHdr* h = c.h;
-    const double w = c.pr->score_weight;
-    while (c.aq_size > 0 && !c.err) {
+    RepHdr* h = &c.H();
+    const double w = c.P().score_weight;
+    while (c.H().aq_size > 0 && !c.H().error_code) {
         QInfo q = aq_pop(c);
         uint32_t p = q.pod;
         if (!pod_in_s(c, p)) continue;
@@ -409,8 +500,8 @@ K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
         uint32_t nn = h->s_node_count;
         double sched_time = 0.000001 * (double)nn;  // ConstantTimePerNodeModel (model.rs:24-26)
         cycle_dur += sched_time;
-        uint32_t rc = c.v.pod(p).req_cpu;
-        uint64_t rr = c.v.pod(p).req_ram;
+        uint32_t rc = c.V().pod(p).req_cpu;
+        uint64_t rr = c.V().pod(p).req_ram;
         int st;
         int32_t chosen = -1;
         if (rc == 0 && rr == 0) {
@@ -420,27 +511,27 @@ K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
         } else {
             h->counters[K10S_C_ATTEMPTS] += 1;
             h->counters[K10S_C_NODES_SCANNED] += nn;
-            st = schedule_scan(c.v.s_cpu(), c.v.s_ram(), c.v.s_present(), c.sc->n_nodes, rc, rr, w, &chosen);
+            st = schedule_scan(c.V().s_cpu(), c.V().s_ram(), c.V().s_present(), c.S().n_nodes, rc, rr, w, &chosen);
         }
         if (st != K10S_SCHED_OK) {
             q.timestamp = t + cycle_dur;
             uq_insert(c, q);
-            emit(c, K10S_EV_AS_POD_NOT_SCHEDULED, c.pr->sched_to_as_network_delay, -1, p, 0, t + cycle_dur);
+            emit(c, K10S_EV_AS_POD_NOT_SCHEDULED, c.P().sched_to_as_network_delay, -1, p, 0, t + cycle_dur);
             continue;
         }
         uint32_t n = (uint32_t)chosen;
-        c.v.s_cpu()[n] -= rc;  // reserve_node_resources (118-123)
-        c.v.s_ram()[n] -= rr;
-        c.v.node(n).flags |= NF_S_ASSIGN;  // assign_node_to_pod (125-151)
-        c.v.pod(p).s_assigned = (int32_t)n;
-        emit(c, K10S_EV_AS_ASSIGN_REQ, cycle_dur + c.pr->sched_to_as_network_delay, -1, p, n, t + cycle_dur);
+        c.V().s_cpu()[n] -= rc;  // reserve_node_resources (118-123)
+        c.V().s_ram()[n] -= rr;
+        c.V().node(n).flags |= NF_S_ASSIGN;  // assign_node_to_pod (125-151)
+        c.V().pod(p).s_assigned = (int32_t)n;
+        emit(c, K10S_EV_AS_ASSIGN_REQ, cycle_dur + c.P().sched_to_as_network_delay, -1, p, n, t + cycle_dur);
         h->counters[K10S_C_PLACEMENTS] += 1;
-        if (c.v.place()) {
+        if (c.V().place()) {
             uint32_t k = h->place_n;
-            if (k < c.L->cap_place) {
-                c.v.place()[k].assign_time = t + cycle_dur;
-                c.v.place()[k].pod = (int32_t)p;
-                c.v.place()[k].node = (int32_t)n;
+            if (k < c.Ly().cap_place) {
+                c.V().place()[k].assign_time = t + cycle_dur;
+                c.V().place()[k].pod = (int32_t)p;
+                c.V().place()[k].node = (int32_t)n;
                 h->place_n = k + 1;
             } else {
                 h->flags |= 2u;
@@ -449,15 +540,15 @@ K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
         est_add(h->est[K10S_EST_POD_SCHEDULE_TIME], sched_time);
         est_add(h->est[K10S_EST_POD_QUEUE_TIME], queue_t);
     }
-    double next = fmax_rs(cycle_dur, c.pr->scheduling_cycle_interval);
+    double next = fmax_rs(cycle_dur, c.P().scheduling_cycle_interval);
     emit0(c, K10S_EV_S_RUN_CYCLE, next);
 }
 
 // ---- pods of a node in name order (wave ballot over pod indices) ---------------------------------
-// Calls f(p) for every pod p (ascending) with pred(p); stops early if c.err.
+// Calls f(p) for every pod p (ascending) with pred(p); stops early if c.H().error_code.
 template <typename Pred, typename F>
 K10S_HD void for_each_pod_in_order(Ctx& c, Pred pred, F f) {
-    const uint32_t P = c.sc->n_pods;
+    const uint32_t P = c.S().n_pods;
     for (uint32_t base = 0; base < P; base += K10S_LANES) {
         uint32_t p = base + (uint32_t)lane_id();
         bool m = p < P && pred(p);
@@ -467,12 +558,12 @@ K10S_HD void for_each_pod_in_order(Ctx& c, Pred pred, F f) {
             uint32_t b = (uint32_t)__builtin_ctzll(mask);
             mask &= mask - 1;
             f(base + b);
-            if (c.err) return;
+            if (c.H().error_code) return;
         }
 #else
         if (m) {
             f(p);
-            if (c.err) return;
+            if (c.H().error_code) return;
         }
 #endif
     }
@@ -480,17 +571,17 @@ K10S_HD void for_each_pod_in_order(Ctx& c, Pred pred, F f) {
 
 // ---- scheduler handlers (scheduler.rs:382-477) ---------------------------------------------------
 K10S_HD void s_release(Ctx& c, uint32_t p) {  // release_node_resources (153-162)
-    int32_t n = c.v.pod(p).s_assigned;
-    if (n < 0 || !bit_test(c.v.s_present(), (uint32_t)n)) {
+    int32_t n = c.V().pod(p).s_assigned;
+    if (n < 0 || !bit_test(c.V().s_present(), (uint32_t)n)) {
         fail(c, K10S_PANIC_MISSING_NODE);
         return;
     }
-    c.v.s_cpu()[n] += c.v.pod(p).req_cpu;
-    c.v.s_ram()[n] += c.v.pod(p).req_ram;
+    c.V().s_cpu()[n] += c.V().pod(p).req_cpu;
+    c.V().s_ram()[n] += c.V().pod(p).req_ram;
 }
 
 K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
-    RepHdr* h = c.h;
+    RepHdr* h = &c.H();
     switch (e.kind) {
     case K10S_EV_S_RUN_CYCLE:
         run_scheduling_cycle(c, e.time);
@@ -503,20 +594,20 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
         uint32_t n = e.a;
         uint32_t ac = e.b;
         uint64_t ar = f2u(e.x);
-        c.v.s_cpu()[n] = ac;
-        c.v.s_ram()[n] = ar;
-        if (!bit_test(c.v.s_present(), n)) {
-            bit_set(c.v.s_present(), n);
+        c.V().s_cpu()[n] = ac;
+        c.V().s_ram()[n] = ar;
+        if (!bit_test(c.V().s_present(), n)) {
+            bit_set(c.V().s_present(), n);
             h->s_node_count += 1;
         }
-        if (c.pr->enable_unscheduled_pods_conditional_move) s_move(c, 3, 0.0, ac, ar);
+        if (c.P().enable_unscheduled_pods_conditional_move) s_move(c, 3, 0.0, ac, ar);
         else s_move(c, 0, 0.0, 0, 0);
         break;
     }
     case K10S_EV_S_POD_SCHEDULE_REQ: {
         uint32_t p = e.a;
-        c.v.pod(p).flags |= PF_IN_S;
-        c.v.pod(p).s_assigned = -1;
+        c.V().pod(p).flags |= PF_IN_S;
+        c.V().pod(p).s_assigned = -1;
         QInfo q;
         q.timestamp = e.time;
         q.initial = e.time;
@@ -531,31 +622,31 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
             fail(c, K10S_PANIC_MISSING_POD);
             return;
         }
-        c.v.pod(p).flags &= (uint8_t)~PF_IN_S;
-        if (!(c.v.node(n).flags & NF_S_ASSIGN)) {
+        c.V().pod(p).flags &= (uint8_t)~PF_IN_S;
+        if (!(c.V().node(n).flags & NF_S_ASSIGN)) {
             fail(c, K10S_PANIC_MISSING_ASSIGNMENTS);
             return;
         }
         s_release(c, p);
-        if (c.err) return;
-        s_move_after_free(c, c.v.pod(p).req_cpu, c.v.pod(p).req_ram);
+        if (c.H().error_code) return;
+        s_move_after_free(c, c.V().pod(p).req_cpu, c.V().pod(p).req_ram);
         break;
     }
     case K10S_EV_S_REMOVE_NODE: {
         uint32_t n = e.a;
-        if (!bit_test(c.v.s_present(), n)) {
+        if (!bit_test(c.V().s_present(), n)) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
         }
-        bit_clear(c.v.s_present(), n);
+        bit_clear(c.V().s_present(), n);
         h->s_node_count -= 1;
-        if (c.v.node(n).flags & NF_S_ASSIGN) {  // reschedule_unfinished_pods (352-364), name order
-            c.v.node(n).flags &= (uint8_t)~NF_S_ASSIGN;
+        if (c.V().node(n).flags & NF_S_ASSIGN) {  // reschedule_unfinished_pods (352-364), name order
+            c.V().node(n).flags &= (uint8_t)~NF_S_ASSIGN;
             double t = e.time;
             for_each_pod_in_order(
-                c, [&](uint32_t p) { return pod_in_s(c, p) && c.v.pod(p).s_assigned == (int32_t)n; },
+                c, [&](uint32_t p) { return pod_in_s(c, p) && c.V().pod(p).s_assigned == (int32_t)n; },
                 [&](uint32_t p) {
-                    c.v.pod(p).s_assigned = -1;
+                    c.V().pod(p).s_assigned = -1;
                     QInfo q;
                     q.timestamp = t;
                     q.initial = t;
@@ -569,16 +660,16 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
     case K10S_EV_S_REMOVE_POD: {
         uint32_t p = e.a;
         if (!pod_in_s(c, p)) return;
-        c.v.pod(p).flags &= (uint8_t)~PF_IN_S;
-        int32_t n = c.v.pod(p).s_assigned;
+        c.V().pod(p).flags &= (uint8_t)~PF_IN_S;
+        int32_t n = c.V().pod(p).s_assigned;
         if (n >= 0) {
             s_release(c, p);
-            if (c.err) return;
-            if (!(c.v.node(n).flags & NF_S_ASSIGN)) {
+            if (c.H().error_code) return;
+            if (!(c.V().node(n).flags & NF_S_ASSIGN)) {
                 fail(c, K10S_PANIC_MISSING_ASSIGNMENTS);
                 return;
             }
-            s_move_after_free(c, c.v.pod(p).req_cpu, c.v.pod(p).req_ram);
+            s_move_after_free(c, c.V().pod(p).req_cpu, c.V().pod(p).req_ram);
         }
         break;
     }
@@ -593,16 +684,16 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
 // by autoscale() while exactly one request is in flight, so deciding at snapshot time and
 // emitting the actions at delivery time (cluster_autoscaler.rs:309-331) is equivalent.
 K10S_COLD void ca_decide(Ctx& c) {
-    RepHdr* h = c.h;
-    const Scenario* sc = c.sc;
+    RepHdr* h = &c.H();
+    const Scenario* sc = &c.S();
     h->ca_n_act = 0;
-    uint32_t* cag = c.v.cag();
-    const uint64_t max_nodes = c.pr->ca_max_node_count;
+    uint32_t* cag = c.V().cag();
+    const uint64_t max_nodes = c.P().ca_max_node_count;
     if (h->unsched_cache_count > 0) {
         // scale_up_info (persistent_storage.rs:137-145) looks every cached unscheduled pod up in
         // storage before the algorithm runs: a removed one panics (the cache is never cleaned, A.5)
         for (uint32_t p = 0; p < sc->n_pods; p++) {
-            if ((c.v.pod(p).flags & PF_UNSCHED) && !(c.v.pod(p).flags & PF_IN_PS)) {
+            if ((c.V().pod(p).flags & PF_UNSCHED) && !(c.V().pod(p).flags & PF_IN_PS)) {
                 fail(c, K10S_PANIC_MISSING_POD);
                 return;
             }
@@ -621,15 +712,15 @@ K10S_COLD void ca_decide(Ctx& c) {
         }
         if (over) return;
         uint32_t nalloc = 0;
-        for (uint32_t p = 0; p < sc->n_pods && !c.err; p++) {
-            if (!(c.v.pod(p).flags & PF_UNSCHED)) continue;
-            uint32_t rc = c.v.pod(p).req_cpu;
-            uint64_t rr = c.v.pod(p).req_ram;
+        for (uint32_t p = 0; p < sc->n_pods && !c.H().error_code; p++) {
+            if (!(c.V().pod(p).flags & PF_UNSCHED)) continue;
+            uint32_t rc = c.V().pod(p).req_cpu;
+            uint64_t rr = c.V().pod(p).req_ram;
             bool fit = false;
             for (uint32_t i = 0; i < nalloc; i++) {  // try_fit_in_allocated_nodes (114-123)
-                if (rc <= c.v.ca_cpu()[i] && rr <= c.v.ca_ram()[i]) {
-                    c.v.ca_cpu()[i] -= rc;
-                    c.v.ca_ram()[i] -= rr;
+                if (rc <= c.V().ca_cpu()[i] && rr <= c.V().ca_ram()[i]) {
+                    c.V().ca_cpu()[i] -= rc;
+                    c.V().ca_ram()[i] -= rr;
                     fit = true;
                     break;
                 }
@@ -646,14 +737,14 @@ K10S_COLD void ca_decide(Ctx& c) {
                         fail(c, K10S_ERR_NAME_BOUND);
                         return;
                     }
-                    if (nalloc >= c.L->cap_act) {
+                    if (nalloc >= c.Ly().cap_act) {
                         fail(c, K10S_ERR_CA_BUFFER);
                         return;
                     }
-                    c.v.ca_act()[nalloc].up = 1;
-                    c.v.ca_act()[nalloc].arg = sc->ca_def[g * sc->ca_bound + (k - 1)];
-                    c.v.ca_cpu()[nalloc] = sc->ca_cpu[g];
-                    c.v.ca_ram()[nalloc] = sc->ca_ram[g];
+                    c.V().ca_act()[nalloc].up = 1;
+                    c.V().ca_act()[nalloc].arg = sc->ca_def[g * sc->ca_bound + (k - 1)];
+                    c.V().ca_cpu()[nalloc] = sc->ca_cpu[g];
+                    c.V().ca_ram()[nalloc] = sc->ca_ram[g];
                     nalloc++;
                     cur++;
                     break;
@@ -666,40 +757,40 @@ K10S_COLD void ca_decide(Ctx& c) {
     // scale_down (247-306) over PS nodes in name order with a mutable copy of their allocatable
     const uint32_t N = sc->n_nodes;
     for (uint32_t n = 0; n < N; n++) {
-        c.v.ca_cpu()[n] = c.v.node(n).ps_cpu;
-        c.v.ca_ram()[n] = c.v.node(n).ps_ram;
+        c.V().ca_cpu()[n] = c.V().node(n).ps_cpu;
+        c.V().ca_ram()[n] = c.V().node(n).ps_ram;
     }
     uint32_t nrem = 0;
-    for (uint32_t n = 0; n < N && !c.err; n++) {
-        if (!(c.v.node(n).flags & NF_PS_PRESENT)) continue;
-        uint32_t def = c.v.node(n).ps_def;
+    for (uint32_t n = 0; n < N && !c.H().error_code; n++) {
+        if (!(c.V().node(n).flags & NF_PS_PRESENT)) continue;
+        uint32_t def = c.V().node(n).ps_def;
         if (!sc->def_ca_origin[def]) continue;
         uint32_t cap_c = sc->def_cpu[def];
         uint64_t cap_r = sc->def_ram[def];
-        double cu = (double)(uint32_t)(cap_c - c.v.ca_cpu()[n]) / (double)cap_c;
-        double ru = (double)(uint64_t)(cap_r - c.v.ca_ram()[n]) / (double)cap_r;
+        double cu = (double)(uint32_t)(cap_c - c.V().ca_cpu()[n]) / (double)cap_c;
+        double ru = (double)(uint64_t)(cap_r - c.V().ca_ram()[n]) / (double)cap_r;
         double util = cu > ru ? cu : ru;
-        if (!(util < c.pr->ca_scale_down_utilization_threshold)) continue;
+        if (!(util < c.P().ca_scale_down_utilization_threshold)) continue;
         // all_pods_can_be_moved_to_other_nodes (148-181): pods in PS assignments[n], name order
         uint32_t nundo = 0;
         bool ok = true;
-        uint32_t ep = c.v.node(n).ps_epoch;
+        uint32_t ep = c.V().node(n).ps_epoch;
         for (uint32_t p = 0; p < sc->n_pods && ok; p++) {
-            if (c.v.pod(p).ps_assigned != (int32_t)n || c.v.pod(p).ps_aepoch != ep || ep == 0) continue;
-            uint32_t rc = c.v.pod(p).req_cpu;
-            uint64_t rr = c.v.pod(p).req_ram;
+            if (c.V().pod(p).ps_assigned != (int32_t)n || c.V().pod(p).ps_aepoch != ep || ep == 0) continue;
+            uint32_t rc = c.V().pod(p).req_cpu;
+            uint64_t rr = c.V().pod(p).req_ram;
             bool placed = false;
             for (uint32_t m = 0; m < N; m++) {
-                if (m == n || !(c.v.node(m).flags & NF_PS_PRESENT)) continue;
-                if (rc <= c.v.ca_cpu()[m] && rr <= c.v.ca_ram()[m]) {
-                    c.v.ca_cpu()[m] -= rc;
-                    c.v.ca_ram()[m] -= rr;
-                    if (nundo >= c.L->cap_undo) {
+                if (m == n || !(c.V().node(m).flags & NF_PS_PRESENT)) continue;
+                if (rc <= c.V().ca_cpu()[m] && rr <= c.V().ca_ram()[m]) {
+                    c.V().ca_cpu()[m] -= rc;
+                    c.V().ca_ram()[m] -= rr;
+                    if (nundo >= c.Ly().cap_undo) {
                         fail(c, K10S_ERR_CA_BUFFER);
                         return;
                     }
-                    c.v.ca_undo()[2 * nundo] = m;
-                    c.v.ca_undo()[2 * nundo + 1] = p;
+                    c.V().ca_undo()[2 * nundo] = m;
+                    c.V().ca_undo()[2 * nundo + 1] = p;
                     nundo++;
                     placed = true;
                     break;
@@ -709,23 +800,23 @@ K10S_COLD void ca_decide(Ctx& c) {
         }
         if (!ok) {
             for (uint32_t i = 0; i < nundo; i++) {  // *nodes = original
-                uint32_t m = c.v.ca_undo()[2 * i], p = c.v.ca_undo()[2 * i + 1];
-                c.v.ca_cpu()[m] += c.v.pod(p).req_cpu;
-                c.v.ca_ram()[m] += c.v.pod(p).req_ram;
+                uint32_t m = c.V().ca_undo()[2 * i], p = c.V().ca_undo()[2 * i + 1];
+                c.V().ca_cpu()[m] += c.V().pod(p).req_cpu;
+                c.V().ca_ram()[m] += c.V().pod(p).req_ram;
             }
             continue;
         }
-        if (nrem >= c.L->cap_act) {
+        if (nrem >= c.Ly().cap_act) {
             fail(c, K10S_ERR_CA_BUFFER);
             return;
         }
-        c.v.ca_act()[nrem].up = 0;
-        c.v.ca_act()[nrem].arg = n;
+        c.V().ca_act()[nrem].up = 0;
+        c.V().ca_act()[nrem].arg = n;
         nrem++;
     }
     for (uint32_t i = 0; i < nrem; i++) {
-        uint32_t n = c.v.ca_act()[i].arg;
-        int32_t g = sc->def_ca_group[c.v.node(n).ps_def];
+        uint32_t n = c.V().ca_act()[i].arg;
+        int32_t g = sc->def_ca_group[c.V().node(n).ps_def];
         if (g < 0) {
             fail(c, K10S_PANIC_CA_GROUP);
             return;
@@ -737,111 +828,112 @@ K10S_COLD void ca_decide(Ctx& c) {
 
 // ---- persistent storage (persistent_storage.rs:185-490) --------------------------------------
 K10S_HD void ps_clean_up(Ctx& c, uint32_t p) {  // 173-182
-    int32_t n = c.v.pod(p).ps_assigned;
+    int32_t n = c.V().pod(p).ps_assigned;
     if (n < 0) return;
-    if (c.v.node(n).flags & NF_PS_PRESENT) {
-        c.v.node(n).ps_cpu += c.v.pod(p).req_cpu;
-        c.v.node(n).ps_ram += c.v.pod(p).req_ram;
-        if (c.v.pod(p).ps_aepoch == c.v.node(n).ps_epoch) c.v.pod(p).ps_aepoch = 0;
+    if (c.V().node(n).flags & NF_PS_PRESENT) {
+        c.V().node(n).ps_cpu += c.V().pod(p).req_cpu;
+        c.V().node(n).ps_ram += c.V().pod(p).req_ram;
+        if (c.V().pod(p).ps_aepoch == c.V().node(n).ps_epoch) c.V().pod(p).ps_aepoch = 0;
     }
 }
 
-K10S_WARM void on_ps(Ctx& c, const HeapEv& e) {
-    RepHdr* h = c.h;
-    const Params* pr = c.pr;
+K10S_WARM void on_ps(Ctx& c, HeapEv e) {
+    uniform_event(e);
+    RepHdr* h = &c.H();
+    const Params* pr = &c.P();
     switch (e.kind) {
     case K10S_EV_PS_CREATE_NODE_REQ: {
         uint32_t def = e.b, n = e.a;
-        if (c.v.node(n).flags & NF_PS_PRESENT) {
+        if (c.V().node(n).flags & NF_PS_PRESENT) {
             fail(c, K10S_PANIC_DUPLICATE_NODE);
             return;
         }
-        c.v.node(n).flags |= NF_PS_PRESENT;
-        c.v.node(n).ps_def = def;
-        c.v.node(n).ps_cpu = c.sc->def_cpu[def];
-        c.v.node(n).ps_ram = c.sc->def_ram[def];
-        c.v.node(n).ps_epoch += 1;
+        c.V().node(n).flags |= NF_PS_PRESENT;
+        c.V().node(n).ps_def = def;
+        c.V().node(n).ps_cpu = c.S().def_cpu[def];
+        c.V().node(n).ps_ram = c.S().def_ram[def];
+        c.V().node(n).ps_epoch += 1;
         h->ps_node_count += 1;
         emit(c, K10S_EV_AS_CREATE_NODE_RESP, pr->as_to_ps_network_delay, -1, n, 0, 0.0);
         break;
     }
     case K10S_EV_PS_NODE_ADDED: {
         uint32_t n = e.a;
-        if (!(c.v.node(n).flags & NF_PS_PRESENT)) {
+        if (!(c.V().node(n).flags & NF_PS_PRESENT)) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
         }
-        emit(c, K10S_EV_S_ADD_NODE, pr->ps_to_sched_network_delay, -1, n, c.v.node(n).ps_cpu, u2f(c.v.node(n).ps_ram));
+        emit(c, K10S_EV_S_ADD_NODE, pr->ps_to_sched_network_delay, -1, n, c.V().node(n).ps_cpu, u2f(c.V().node(n).ps_ram));
         h->counters[K10S_C_PROCESSED_NODES] += 1;
         break;
     }
     case K10S_EV_PS_CREATE_POD_REQ: {
         uint32_t p = e.a;
-        if (c.v.pod(p).flags & PF_IN_PS) {
+        if (c.V().pod(p).flags & PF_IN_PS) {
             fail(c, K10S_PANIC_DUPLICATE_POD);
             return;
         }
-        c.v.pod(p).flags |= PF_IN_PS;
-        c.v.pod(p).ps_assigned = -1;
-        if (c.v.prec()) c.v.prec()[p].state = 1;
+        c.V().pod(p).flags |= PF_IN_PS;
+        c.V().pod(p).ps_assigned = -1;
+        if (c.V().prec()) c.V().prec()[p].state = 1;
         emit(c, K10S_EV_S_POD_SCHEDULE_REQ, pr->ps_to_sched_network_delay, -1, p, 0, 0.0);
         break;
     }
     case K10S_EV_PS_ASSIGN_REQ: {
         uint32_t p = e.a, n = e.b;
-        if (!(c.v.pod(p).flags & PF_IN_PS)) {
+        if (!(c.V().pod(p).flags & PF_IN_PS)) {
             fail(c, K10S_PANIC_MISSING_POD);
             return;
         }
-        c.v.pod(p).ps_assigned = (int32_t)n;
-        if (c.v.pod(p).flags & PF_UNSCHED) {
-            c.v.pod(p).flags &= (uint8_t)~PF_UNSCHED;
+        c.V().pod(p).ps_assigned = (int32_t)n;
+        if (c.V().pod(p).flags & PF_UNSCHED) {
+            c.V().pod(p).flags &= (uint8_t)~PF_UNSCHED;
             h->unsched_cache_count -= 1;
         }
-        if (!(c.v.node(n).flags & NF_PS_PRESENT)) {
+        if (!(c.V().node(n).flags & NF_PS_PRESENT)) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
         }
-        c.v.node(n).ps_cpu -= c.v.pod(p).req_cpu;
-        c.v.node(n).ps_ram -= c.v.pod(p).req_ram;
-        c.v.pod(p).ps_aepoch = c.v.node(n).ps_epoch;
+        c.V().node(n).ps_cpu -= c.V().pod(p).req_cpu;
+        c.V().node(n).ps_ram -= c.V().pod(p).req_ram;
+        c.V().pod(p).ps_aepoch = c.V().node(n).ps_epoch;
         emit(c, K10S_EV_AS_ASSIGN_RESP, pr->as_to_ps_network_delay, -1, p, n, 0.0);
         break;
     }
     case K10S_EV_PS_POD_NOT_SCHEDULED: {
         uint32_t p = e.a;
-        if (!(c.v.pod(p).flags & PF_IN_PS)) {
+        if (!(c.V().pod(p).flags & PF_IN_PS)) {
             fail(c, K10S_PANIC_MISSING_POD);
             return;
         }
-        if (!(c.v.pod(p).flags & PF_UNSCHED)) {
-            c.v.pod(p).flags |= PF_UNSCHED;
+        if (!(c.V().pod(p).flags & PF_UNSCHED)) {
+            c.V().pod(p).flags |= PF_UNSCHED;
             h->unsched_cache_count += 1;
         }
         break;
     }
     case K10S_EV_PS_POD_STARTED: {
         uint32_t p = e.a;
-        if (!(c.v.pod(p).flags & PF_IN_PS)) {
+        if (!(c.V().pod(p).flags & PF_IN_PS)) {
             fail(c, K10S_PANIC_MISSING_POD);
             return;
         }
-        if (c.v.prec()) c.v.prec()[p].t_running = e.x;
+        if (c.V().prec()) c.V().prec()[p].t_running = e.x;
         break;
     }
     case K10S_EV_PS_POD_FINISHED: {
         uint32_t p = e.a;
-        if (c.v.pod(p).flags & PF_IN_PS) {
-            c.v.pod(p).flags &= (uint8_t)~PF_IN_PS;
+        if (c.V().pod(p).flags & PF_IN_PS) {
+            c.V().pod(p).flags &= (uint8_t)~PF_IN_PS;
             ps_clean_up(c, p);
-            if (!(c.sc->pod_flags[p] & POD_HAS_DUR)) {
+            if (!(c.S().pod_flags[p] & POD_HAS_DUR)) {
                 fail(c, K10S_PANIC_MISSING_POD);
                 return;
             }
-            est_add(h->est[K10S_EST_POD_DURATION], c.v.pod(p).dur);
-            if (c.v.prec()) {
-                c.v.prec()[p].t_finished = e.x;
-                c.v.prec()[p].state = 2;
+            est_add(h->est[K10S_EST_POD_DURATION], c.V().pod(p).dur);
+            if (c.V().prec()) {
+                c.V().prec()[p].t_finished = e.x;
+                c.V().prec()[p].state = 2;
             }
         }
         emit(c, K10S_EV_S_POD_FINISHED, pr->ps_to_sched_network_delay, -1, p, e.b, e.x);
@@ -849,11 +941,11 @@ K10S_WARM void on_ps(Ctx& c, const HeapEv& e) {
     }
     case K10S_EV_PS_REMOVE_NODE_REQ: {
         uint32_t n = e.a;
-        if (!(c.v.node(n).flags & NF_PS_PRESENT)) {
+        if (!(c.V().node(n).flags & NF_PS_PRESENT)) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
         }
-        c.v.node(n).flags &= (uint8_t)~NF_PS_PRESENT;
+        c.V().node(n).flags &= (uint8_t)~NF_PS_PRESENT;
         h->ps_node_count -= 1;
         emit(c, K10S_EV_AS_REMOVE_NODE_RESP, pr->as_to_ps_network_delay, -1, n, 0, 0.0);
         break;
@@ -867,16 +959,16 @@ K10S_WARM void on_ps(Ctx& c, const HeapEv& e) {
         break;
     case K10S_EV_PS_REMOVE_POD_REQ: {
         uint32_t p = e.a;
-        if (!(c.v.pod(p).flags & PF_IN_PS)) {
+        if (!(c.V().pod(p).flags & PF_IN_PS)) {
             emit(c, K10S_EV_AS_REMOVE_POD_RESP, pr->as_to_ps_network_delay, -1, p, 0, 0.0);
             return;
         }
-        c.v.pod(p).flags &= (uint8_t)~PF_IN_PS;
-        if (c.v.prec()) {
-            c.v.prec()[p].t_removed = e.time;
-            c.v.prec()[p].state = 3;
+        c.V().pod(p).flags &= (uint8_t)~PF_IN_PS;
+        if (c.V().prec()) {
+            c.V().prec()[p].t_removed = e.time;
+            c.V().prec()[p].state = 3;
         }
-        int32_t n = c.v.pod(p).ps_assigned;
+        int32_t n = c.V().pod(p).ps_assigned;
         uint32_t flag = 0;
         if (n >= 0) {
             ps_clean_up(c, p);
@@ -896,40 +988,41 @@ K10S_WARM void on_ps(Ctx& c, const HeapEv& e) {
 }
 
 // ---- api server (api_server.rs:127-457) --------------------------------------------------------
-K10S_WARM void on_api_server(Ctx& c, const HeapEv& e) {
-    RepHdr* h = c.h;
-    const Params* pr = c.pr;
-    const Scenario* sc = c.sc;
+K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
+    uniform_event(e);
+    RepHdr* h = &c.H();
+    const Params* pr = &c.P();
+    const Scenario* sc = &c.S();
     switch (e.kind) {
     case K10S_EV_AS_CREATE_NODE_REQ: {
         uint32_t def = e.b;
         uint32_t n = sc->def_node[def];
-        c.v.node(n).pend_def = (int32_t)def;
+        c.V().node(n).pend_def = (int32_t)def;
         emit(c, K10S_EV_PS_CREATE_NODE_REQ, pr->as_to_ps_network_delay, -1, n, def, 0.0);
         break;
     }
     case K10S_EV_AS_CREATE_NODE_RESP: {  // handle_create_node (96-115)
         uint32_t n = e.a;
-        int32_t def = c.v.node(n).pend_def;
+        int32_t def = c.V().node(n).pend_def;
         if (def < 0) {
             fail(c, K10S_PANIC_MISSING_PENDING);
             return;
         }
-        c.v.node(n).pend_def = -1;
+        c.V().node(n).pend_def = -1;
         if (h->pool_count == 0) {
             fail(c, K10S_PANIC_POOL_EXHAUSTED);
             return;
         }
-        uint32_t slot = c.v.pool_ring()[h->pool_head];
+        uint32_t slot = c.V().pool_ring()[h->pool_head];
         h->pool_head = (h->pool_head + 1) % sc->n_slots;
         h->pool_count -= 1;
-        c.v.slot(slot).node = (int32_t)n;
-        c.v.slot(slot).def = (uint32_t)def;
-        if (c.v.node(n).as_slot >= 0) {
+        c.V().slot(slot).node = (int32_t)n;
+        c.V().slot(slot).def = (uint32_t)def;
+        if (c.V().node(n).as_slot >= 0) {
             fail(c, K10S_PANIC_DUPLICATE_NODE);
             return;
         }
-        c.v.node(n).as_slot = (int32_t)slot;
+        c.V().node(n).as_slot = (int32_t)slot;
         h->as_node_count += 1;
         emit(c, K10S_EV_PS_NODE_ADDED, pr->as_to_ps_network_delay, -1, n, 0, e.time);
         break;
@@ -939,13 +1032,13 @@ K10S_WARM void on_api_server(Ctx& c, const HeapEv& e) {
         break;
     case K10S_EV_AS_ASSIGN_REQ: {
         uint32_t n = e.b;
-        if (bit_test(c.v.pend_rm(), sc->node_uid[n]) || c.v.node(n).as_slot < 0) return;
+        if (bit_test(c.V().pend_rm(), sc->node_uid[n]) || c.V().node(n).as_slot < 0) return;
         emit(c, K10S_EV_PS_ASSIGN_REQ, pr->as_to_ps_network_delay, -1, e.a, n, e.x);
         break;
     }
     case K10S_EV_AS_ASSIGN_RESP: {
         uint32_t n = e.b;
-        int32_t slot = c.v.node(n).as_slot;
+        int32_t slot = c.V().node(n).as_slot;
         if (slot < 0) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
@@ -965,11 +1058,11 @@ K10S_WARM void on_api_server(Ctx& c, const HeapEv& e) {
         emit(c, K10S_EV_PS_POD_FINISHED, pr->as_to_ps_network_delay, -1, e.a, e.b, e.x);
         break;
     case K10S_EV_AS_REMOVE_NODE_REQ:
-        bit_set(c.v.pend_rm(), sc->node_uid[e.a]);
+        bit_set(c.V().pend_rm(), sc->node_uid[e.a]);
         emit(c, K10S_EV_PS_REMOVE_NODE_REQ, pr->as_to_ps_network_delay, -1, e.a, 0, 0.0);
         break;
     case K10S_EV_AS_REMOVE_NODE_RESP: {
-        int32_t slot = c.v.node(e.a).as_slot;
+        int32_t slot = c.V().node(e.a).as_slot;
         if (slot < 0) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
@@ -979,23 +1072,23 @@ K10S_WARM void on_api_server(Ctx& c, const HeapEv& e) {
     }
     case K10S_EV_AS_NODE_REMOVED: {
         uint32_t n = e.a;
-        int32_t slot = c.v.node(n).as_slot;
+        int32_t slot = c.V().node(n).as_slot;
         if (slot < 0) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
         }
-        c.v.node(n).as_slot = -1;
+        c.V().node(n).as_slot = -1;
         h->as_node_count -= 1;
         // reclaim_component (node_component_pool.rs:68-77)
-        c.v.slot(slot).node = -1;
-        c.v.slot(slot).removed = 0;
-        c.v.slot(slot).rtime = 0.0;
-        c.v.slot(slot).gen += 1;
-        c.v.slot(slot).head = -1;
+        c.V().slot(slot).node = -1;
+        c.V().slot(slot).removed = 0;
+        c.V().slot(slot).rtime = 0.0;
+        c.V().slot(slot).gen += 1;
+        c.V().slot(slot).head = -1;
         uint32_t tail = (h->pool_head + h->pool_count) % sc->n_slots;
-        c.v.pool_ring()[tail] = (uint32_t)slot;
+        c.V().pool_ring()[tail] = (uint32_t)slot;
         h->pool_count += 1;
-        bit_clear(c.v.pend_rm(), sc->node_uid[n]);
+        bit_clear(c.V().pend_rm(), sc->node_uid[n]);
         emit(c, K10S_EV_PS_NODE_REMOVED, pr->as_to_ps_network_delay, -1, n, 0, e.x);
         break;
     }
@@ -1006,12 +1099,12 @@ K10S_WARM void on_api_server(Ctx& c, const HeapEv& e) {
         emit0(c, K10S_EV_CA_RESP, pr->as_to_ca_network_delay);
         break;
     case K10S_EV_AS_REMOVE_POD_REQ:
-        bit_set(c.v.pend_rm(), sc->pod_uid[e.a]);  // quirk (api_server.rs:343): the NODE removal set
+        bit_set(c.V().pend_rm(), sc->pod_uid[e.a]);  // quirk (api_server.rs:343): the NODE removal set
         emit(c, K10S_EV_PS_REMOVE_POD_REQ, pr->as_to_ps_network_delay, -1, e.a, 0, 0.0);
         break;
     case K10S_EV_AS_REMOVE_POD_RESP: {
         if (f2u(e.x) != 0) {
-            int32_t slot = c.v.node(e.b).as_slot;
+            int32_t slot = c.V().node(e.b).as_slot;
             if (slot < 0) {
                 fail(c, K10S_PANIC_MISSING_NODE);
                 return;
@@ -1033,7 +1126,7 @@ K10S_WARM void on_api_server(Ctx& c, const HeapEv& e) {
             fail(c, K10S_PANIC_GROUP_DURATION);
             return;
         }
-        GroupState& gs = c.v.grp()[g];
+        GroupState& gs = c.V().grp()[g];
         gs.creation_time = e.time;
         gs.cpu_last_start = e.time;
         gs.ram_last_start = e.time;
@@ -1045,7 +1138,7 @@ K10S_WARM void on_api_server(Ctx& c, const HeapEv& e) {
             fail(c, K10S_ERR_NAME_BOUND);
             return;
         }
-        for (uint32_t k = 0; k < init && !c.err; k++)
+        for (uint32_t k = 0; k < init && !c.H().error_code; k++)
             emit(c, K10S_EV_PS_CREATE_POD_REQ, pr->as_to_ps_network_delay, -1, sc->g_pod[g * sc->group_bound + k], 0, 0.0);
         if (sc->hpa_enabled) emit(c, K10S_EV_HPA_REGISTER_GROUP, pr->as_to_hpa_network_delay, -1, g, 0, e.time);
         break;
@@ -1056,39 +1149,40 @@ K10S_WARM void on_api_server(Ctx& c, const HeapEv& e) {
 }
 
 // ---- node components (node_component.rs:178-335) ------------------------------------------------
-K10S_WARM void on_node(Ctx& c, const HeapEv& e) {
-    const Params* pr = c.pr;
+K10S_WARM void on_node(Ctx& c, HeapEv e) {
+    uniform_event(e);
+    const Params* pr = &c.P();
     int32_t slot = e.slot;
     switch (e.kind) {
     case K10S_EV_N_BIND: {
         uint32_t p = e.a, n = e.b;
-        if (c.v.slot(slot).removed) {
+        if (c.V().slot(slot).removed) {
             fail(c, K10S_PANIC_BIND_REMOVED_NODE);
             return;
         }
-        if (c.v.slot(slot).node != (int32_t)n) {
+        if (c.V().slot(slot).node != (int32_t)n) {
             fail(c, K10S_PANIC_BIND_REMOVED_NODE);
             return;
         }
-        if (c.v.pod(p).run_slot >= 0) {  // a second concurrent bind of one pod: not modelled
+        if (c.V().pod(p).run_slot >= 0) {  // a second concurrent bind of one pod: not modelled
             fail(c, K10S_PANIC_BIND_REMOVED_NODE);
             return;
         }
         uint32_t fseq = 0;
-        if (c.sc->pod_flags[p] & POD_HAS_DUR) {  // simulate_pod_runtime (114-175)
-            double dur = c.v.pod(p).dur;
+        if (c.S().pod_flags[p] & POD_HAS_DUR) {  // simulate_pod_runtime (114-175)
+            double dur = c.V().pod(p).dur;
             fseq = emit(c, K10S_EV_N_POD_FINISHED, dur + pr->as_to_node_network_delay, slot, p, n, e.time + dur);
         }
         run_insert(c, slot, p);
-        c.v.pod(p).finish_seq = fseq;
-        int32_t g = c.sc->pod_group[p];
-        if (g >= 0) c.v.grp()[g].running += 1;
+        c.V().pod(p).finish_seq = fseq;
+        int32_t g = c.S().pod_group[p];
+        if (g >= 0) c.V().grp()[g].running += 1;
         emit(c, K10S_EV_AS_POD_STARTED, pr->as_to_node_network_delay, -1, p, 0, e.time);
         break;
     }
     case K10S_EV_N_POD_FINISHED: {
         uint32_t p = e.a;
-        if (c.v.pod(p).run_slot != slot) {
+        if (c.V().pod(p).run_slot != slot) {
             fail(c, K10S_PANIC_MISSING_POD);
             return;
         }
@@ -1098,36 +1192,36 @@ K10S_WARM void on_node(Ctx& c, const HeapEv& e) {
     }
     case K10S_EV_N_REMOVE_NODE: {
         uint32_t n = e.a;
-        if (c.v.slot(slot).node != (int32_t)n) {
+        if (c.V().slot(slot).node != (int32_t)n) {
             fail(c, K10S_PANIC_REMOVE_OTHER_NODE);
             return;
         }
         // cancel_all_running_pods (95-112)
-        int32_t p = c.v.slot(slot).head;
-        uint32_t gen = c.v.slot(slot).gen;
+        int32_t p = c.V().slot(slot).head;
+        uint32_t gen = c.V().slot(slot).gen;
         while (p >= 0) {
-            int32_t nx = c.v.pod(p).run_next;
-            c.v.pod(p).cancel_slot = slot;
-            c.v.pod(p).cancel_gen = gen;
+            int32_t nx = c.V().pod(p).run_next;
+            c.V().pod(p).cancel_slot = slot;
+            c.V().pod(p).cancel_gen = gen;
             run_remove(c, (uint32_t)p);
             p = nx;
         }
         emit(c, K10S_EV_AS_NODE_REMOVED, pr->as_to_node_network_delay, -1, n, 0, e.time);
-        c.v.slot(slot).removed = 1;
-        c.v.slot(slot).rtime = e.time;
+        c.V().slot(slot).removed = 1;
+        c.V().slot(slot).rtime = e.time;
         break;
     }
     case K10S_EV_N_REMOVE_POD: {
         uint32_t p = e.a;
-        if (c.v.slot(slot).node < 0) {
+        if (c.V().slot(slot).node < 0) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
         }
-        if (c.v.pod(p).run_slot == slot) {
+        if (c.V().pod(p).run_slot == slot) {
             run_remove(c, p);
             emit(c, K10S_EV_AS_POD_REMOVED, pr->as_to_node_network_delay, -1, p, 1, e.time);
-        } else if (c.v.pod(p).cancel_slot == slot && c.v.pod(p).cancel_gen == c.v.slot(slot).gen) {
-            emit(c, K10S_EV_AS_POD_REMOVED, pr->as_to_node_network_delay, -1, p, 1, c.v.slot(slot).rtime);
+        } else if (c.V().pod(p).cancel_slot == slot && c.V().pod(p).cancel_gen == c.V().slot(slot).gen) {
+            emit(c, K10S_EV_AS_POD_REMOVED, pr->as_to_node_network_delay, -1, p, 1, c.V().slot(slot).rtime);
         } else {
             emit(c, K10S_EV_AS_POD_REMOVED, pr->as_to_node_network_delay, -1, p, 0, 0.0);
         }
@@ -1139,18 +1233,19 @@ K10S_WARM void on_node(Ctx& c, const HeapEv& e) {
 }
 
 // ---- cluster autoscaler proxy (cluster_autoscaler.rs:230-334) --------------------------------
-K10S_COLD void on_ca(Ctx& c, const HeapEv& e) {
-    RepHdr* h = c.h;
-    const Params* pr = c.pr;
+K10S_COLD void on_ca(Ctx& c, HeapEv e) {
+    uniform_event(e);
+    RepHdr* h = &c.H();
+    const Params* pr = &c.P();
     if (e.kind == K10S_EV_CA_TICK) {
         h->ca_last_cycle_time = e.time;
         emit0(c, K10S_EV_AS_CA_REQ, pr->as_to_ca_network_delay);
         return;
     }
-    for (uint32_t i = 0; i < h->ca_n_act && !c.err; i++) {
-        CAAct a = c.v.ca_act()[i];
+    for (uint32_t i = 0; i < h->ca_n_act && !c.H().error_code; i++) {
+        CAAct a = c.V().ca_act()[i];
         if (a.up) {
-            emit(c, K10S_EV_AS_CREATE_NODE_REQ, pr->as_to_ca_network_delay, -1, c.sc->def_node[a.arg], a.arg, 0.0);
+            emit(c, K10S_EV_AS_CREATE_NODE_REQ, pr->as_to_ca_network_delay, -1, c.S().def_node[a.arg], a.arg, 0.0);
             h->counters[K10S_C_TOTAL_SCALED_UP_NODES] += 1;
         } else {
             emit(c, K10S_EV_AS_REMOVE_NODE_REQ, pr->as_to_ca_network_delay, -1, a.arg, 0, 0.0);
@@ -1172,16 +1267,17 @@ K10S_HD uint32_t hpa_desired_by_metric(uint32_t cur, double value, double target
     return d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
 }
 
-K10S_COLD void on_hpa(Ctx& c, const HeapEv& e) {
-    RepHdr* h = c.h;
-    const Scenario* sc = c.sc;
+K10S_COLD void on_hpa(Ctx& c, HeapEv e) {
+    uniform_event(e);
+    RepHdr* h = &c.H();
+    const Scenario* sc = &c.S();
     const uint32_t B = sc->group_bound;
-    const uint32_t words = c.L->words_group;
+    const uint32_t words = c.Ly().words_group;
     if (e.kind == K10S_EV_HPA_REGISTER_GROUP) {
         uint32_t g = e.a;
-        GroupState& gs = c.v.grp()[g];
+        GroupState& gs = c.V().grp()[g];
         gs.registered = 1;
-        uint64_t* bits = c.v.grp_bits() + (uint64_t)g * words;
+        uint64_t* bits = c.V().grp_bits() + (uint64_t)g * words;
         for (uint32_t i = 0; i < words; i++) bits[i] = 0;
         uint32_t init = sc->g_initial[g];
         for (uint32_t k = 0; k < init; k++) bit_set(bits, sc->g_pos[g * B + k]);
@@ -1189,8 +1285,8 @@ K10S_COLD void on_hpa(Ctx& c, const HeapEv& e) {
         gs.total_created = init;
         return;
     }
-    for (uint32_t g = 0; g < sc->n_groups && !c.err; g++) {
-        GroupState& gs = c.v.grp()[g];
+    for (uint32_t g = 0; g < sc->n_groups && !c.H().error_code; g++) {
+        GroupState& gs = c.V().grp()[g];
         if (!gs.has_metric) continue;
         if (!gs.registered) {
             fail(c, K10S_PANIC_HPA_UNREGISTERED);
@@ -1198,7 +1294,7 @@ K10S_COLD void on_hpa(Ctx& c, const HeapEv& e) {
         }
         uint8_t gf = sc->g_flags[g];
         uint32_t cur = gs.created_count;
-        const double tol = c.pr->hpa_target_threshold_tolerance;
+        const double tol = c.P().hpa_target_threshold_tolerance;
         uint32_t dc = (gf & GF_HAS_TCPU) ? hpa_desired_by_metric(cur, gs.util_cpu, sc->g_tcpu[g], tol) : 0;
         uint32_t dr = (gf & GF_HAS_TRAM) ? hpa_desired_by_metric(cur, gs.util_ram, sc->g_tram[g], tol) : 0;
         uint32_t mx = sc->g_max[g];
@@ -1207,9 +1303,9 @@ K10S_COLD void on_hpa(Ctx& c, const HeapEv& e) {
         else if (gf & GF_HAS_TCPU) desired = dc < mx ? dc : mx;
         else if (gf & GF_HAS_TRAM) desired = dr < mx ? dr : mx;
         else desired = cur;
-        uint64_t* bits = c.v.grp_bits() + (uint64_t)g * words;
+        uint64_t* bits = c.V().grp_bits() + (uint64_t)g * words;
         if (cur < desired) {
-            for (uint32_t i = 0; i < desired - cur && !c.err; i++) {
+            for (uint32_t i = 0; i < desired - cur && !c.H().error_code; i++) {
                 uint32_t k = gs.total_created;
                 if (k >= B) {
                     fail(c, K10S_ERR_NAME_BOUND);
@@ -1218,11 +1314,11 @@ K10S_COLD void on_hpa(Ctx& c, const HeapEv& e) {
                 bit_set(bits, sc->g_pos[g * B + k]);
                 gs.created_count += 1;
                 gs.total_created += 1;
-                emit(c, K10S_EV_AS_CREATE_POD_REQ, c.pr->as_to_ca_network_delay, -1, sc->g_pod[g * B + k], 0, 0.0);
+                emit(c, K10S_EV_AS_CREATE_POD_REQ, c.P().as_to_ca_network_delay, -1, sc->g_pod[g * B + k], 0, 0.0);
                 h->counters[K10S_C_TOTAL_SCALED_UP_PODS] += 1;
             }
         } else if (cur > desired) {
-            for (uint32_t i = 0; i < cur - desired && !c.err; i++) {
+            for (uint32_t i = 0; i < cur - desired && !c.H().error_code; i++) {
                 uint32_t j = 0;  // created_pods.pop_first(): smallest name
                 for (uint32_t w = 0; w < words; w++) {
                     if (bits[w]) {
@@ -1233,12 +1329,12 @@ K10S_COLD void on_hpa(Ctx& c, const HeapEv& e) {
                 bit_clear(bits, j);
                 gs.created_count -= 1;
                 uint32_t k = sc->g_sorted_k[g * B + j];
-                emit(c, K10S_EV_AS_REMOVE_POD_REQ, c.pr->as_to_ca_network_delay, -1, sc->g_pod[g * B + k], 0, 0.0);
+                emit(c, K10S_EV_AS_REMOVE_POD_REQ, c.P().as_to_ca_network_delay, -1, sc->g_pod[g * B + k], 0, 0.0);
                 h->counters[K10S_C_TOTAL_SCALED_DOWN_PODS] += 1;
             }
         }
     }
-    emit0(c, K10S_EV_HPA_TICK, c.pr->hpa_scan_interval);
+    emit0(c, K10S_EV_HPA_TICK, c.P().hpa_scan_interval);
 }
 
 // ---- metrics collector (collector.rs:263-337, 410-431) -----------------------------------------
@@ -1254,14 +1350,15 @@ K10S_HD double usage_poll(const Scenario* sc, uint8_t kind, double usage, uint32
     return fmin_rs(1.0, sc->unit_load[uoff + idx] / (double)count);
 }
 
-K10S_COLD void on_metrics(Ctx& c, const HeapEv& e) {
+K10S_COLD void on_metrics(Ctx& c, HeapEv e) {
+    uniform_event(e);
     if (e.kind == K10S_EV_M_GAUGE_TICK) {  // CSV gauge record: no simulation state (collector.rs:392-407)
         emit0(c, K10S_EV_M_GAUGE_TICK, 5.0);
         return;
     }
-    const Scenario* sc = c.sc;
+    const Scenario* sc = &c.S();
     for (uint32_t g = 0; g < sc->n_groups; g++) {
-        GroupState& gs = c.v.grp()[g];
+        GroupState& gs = c.V().grp()[g];
         gs.has_metric = gs.running > 0;
         if (!gs.has_metric) continue;
         // every pod of the group reports the same value (same model, creation time and count), so the
@@ -1296,9 +1393,11 @@ K10S_HD void perturb_pod(const Params& pr, uint32_t key, uint32_t& cpu, uint64_t
     ram = (ram >> 4) * kr;
 }
 
-K10S_HD void init_replica(const Scenario* sc, const Params* pr, const Layout* L, uint8_t* base, uint32_t r) {
-    const uint32_t* pod_key = sc->pod_key;
-    Rep v = make_rep(base, *L, r);
+K10S_HD void init_replica(Ctx& c) {
+    const Scenario* sc = &c.S();
+    const Params* pr = &c.P();
+    const Layout* L = &c.Ly();
+    Rep v = c.V();
     const int lane = lane_id();
     const uint32_t N = sc->n_nodes, P = sc->n_pods, S = sc->n_slots, G = sc->n_groups;
     NodeState ns;
@@ -1320,7 +1419,7 @@ K10S_HD void init_replica(const Scenario* sc, const Params* pr, const Layout* L,
         uint32_t cpu = sc->pod_cpu[p];
         uint64_t ram = sc->pod_ram[p];
         double dur = sc->pod_dur[p];
-        if (perturb && (sc->pod_flags[p] & POD_PERTURB)) perturb_pod(*pr, pod_key[p], cpu, ram, dur);
+        if (perturb && (sc->pod_flags[p] & POD_PERTURB)) perturb_pod(*pr, sc->pod_key[p], cpu, ram, dur);
         PodState ps;
         memset(&ps, 0, sizeof ps);
         ps.req_cpu = cpu;
@@ -1358,8 +1457,8 @@ K10S_HD void init_replica(const Scenario* sc, const Params* pr, const Layout* L,
     for (uint32_t i = lane; i < 2 * sc->n_ca_groups; i += K10S_LANES) v.cag()[i] = 0;
     wave_sync();
 
-    // serial part (wave-uniform)
-    RepHdr* h = v.h();
+    // serial part (wave-uniform) on the working header
+    RepHdr* h = &c.H();
     RepHdr z;
     memset(&z, 0, sizeof z);
     *h = z;
@@ -1389,71 +1488,34 @@ K10S_HD void init_replica(const Scenario* sc, const Params* pr, const Layout* L,
     h->s_node_count = sc->n_default;
     h->ps_node_count = sc->n_default;
     h->as_node_count = sc->n_default;
-
-    Ctx c;
-    c.sc = sc;
-    c.pr = pr;
-    c.h = h;
-    c.v = v;
-    c.L = L;
-    c.clock = 0.0;
-    c.next_seq = 0;
-    c.heap_size = 0;
-    c.aq_size = 0;
-    c.uq_size = 0;
-    c.trace_cursor = 0;
-    c.err = 0;
-    c.cur_kind = 0xFFFF;
-    c.cur_seq = 0;
+    h->cur_kind = 0xFFFF;
     emit0(c, K10S_EV_M_POD_METRICS_TICK, 0.0);  // id 0 (simulator.rs:156-158)
     emit0(c, K10S_EV_M_GAUGE_TICK, 0.0);        // id 1 (simulator.rs:159-161)
-    c.next_seq = sc->first_dynamic_seq;         // trace events hold ids 2 .. 2 + n_trace - 1
-    emit0(c, K10S_EV_S_RUN_CYCLE, 0.0);         // Scheduler::start (scheduler.rs:78-81)
+    h->next_seq = sc->first_dynamic_seq;         // trace events hold ids 2 .. 2 + n_trace - 1
+    emit0(c, K10S_EV_S_RUN_CYCLE, 0.0);          // Scheduler::start (scheduler.rs:78-81)
     emit0(c, K10S_EV_S_FLUSH, 0.0);
     if (sc->ca_enabled) emit0(c, K10S_EV_CA_TICK, 0.0);
     if (sc->hpa_enabled) emit0(c, K10S_EV_HPA_TICK, 0.0);
-    h->clock = c.clock;
-    h->next_seq = c.next_seq;
-    h->heap_size = c.heap_size;
-    h->aq_size = 0;
-    h->uq_size = 0;
-    h->trace_cursor = 0;
     h->status = K10S_REPLICA_RUNNING;
-    h->error_code = c.err;
 }
 
 // ---- the event loop -----------------------------------------------------------------------------
-// Returns 1 if the replica still has work (event budget exhausted), else 0.
-// `h` is the working copy of replica r's header: the device kernel stages it in LDS for the
-// launch (every counter / estimator / queue-size update on the serial path is then an LDS access)
-// and writes it back afterwards; the host check build passes the header in place.
-K10S_HD int run_replica(const Scenario* sc, const Params* pr, const Layout* L, uint8_t* base, uint32_t r, int mode,
-                        double until_time, double max_time, uint64_t budget, RepHdr* h) {
-    Rep v = make_rep(base, *L, r);
+// Returns 1 if the replica still has work (event budget exhausted), else 0.  The working header
+// c.H() is LDS on the device (staged by the kernel) and the replica's header in place on the host.
+K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, uint64_t budget) {
+    RepHdr* h = &c.H();
     if (h->status != K10S_REPLICA_RUNNING) return 0;
-    Ctx c;
-    c.sc = sc;
-    c.pr = pr;
-    c.h = h;
-    c.v = v;
-    c.L = L;
-    c.clock = h->clock;
-    c.next_seq = h->next_seq;
-    c.heap_size = h->heap_size;
-    c.aq_size = h->aq_size;
-    c.uq_size = h->uq_size;
-    c.trace_cursor = h->trace_cursor;
-    c.err = h->error_code;
-    c.cur_kind = 0xFFFF;
-    c.cur_seq = 0;
+    const Scenario* sc = &c.S();
+    h->cur_kind = 0xFFFF;
+    h->cur_seq = 0;
     const uint64_t total_pods = sc->total_pods_in_trace;
-    const TraceEv* tr = sc->trace;
     const uint32_t ntr = sc->n_trace;
+    const uint32_t cap_log = c.Ly().cap_log;
     uint64_t done = 0;
     int more = 0;
     uint32_t status = K10S_REPLICA_RUNNING;
-    while (!c.err) {
-        if (mode == K10S_RUN_UNTIL_ALL_FINISHED && is_multiple_of_1000(c.clock) &&
+    while (!h->error_code) {
+        if (mode == K10S_RUN_UNTIL_ALL_FINISHED && is_multiple_of_1000(h->clock) &&
             h->counters[K10S_C_TERMINATED_PODS] >= total_pods) {
             status = K10S_REPLICA_FINISHED;
             break;
@@ -1463,30 +1525,36 @@ K10S_HD int run_replica(const Scenario* sc, const Params* pr, const Layout* L, u
         bool from_trace = false;
         bool have = false;
         for (;;) {
-            bool ht = c.trace_cursor < ntr;
-            bool hh = c.heap_size > 0;
+            const uint32_t cur = h->trace_cursor;
+            bool ht = cur < ntr;
+            bool hh = h->heap_size > 0;
             if (!ht && !hh) break;
+            if (hh) {
+                e = c.V().heap()[0];
+                uniform_event(e);
+            }
             if (ht) {
-                const TraceEv& te = tr[c.trace_cursor];
-                if (!hh || ev_before(te.time, te.seq, c.v.heap()[0].time, c.v.heap()[0].seq)) {
-                    e.time = te.time;
-                    e.seq = te.seq;
-                    e.kind = (uint16_t)te.kind;
+                const double tt = sc->trace[cur].time;
+                const uint32_t ts = sc->trace[cur].seq;
+                if (!hh || ev_before(tt, ts, e.time, e.seq)) {
+                    const uint32_t tk = sc->trace[cur].kind, ta = sc->trace[cur].arg;
+                    e.time = tt;
+                    e.seq = ts;
+                    e.kind = (uint16_t)tk;
                     e.slot = -1;
                     e.x = 0.0;
-                    e.a = te.arg;
+                    e.a = ta;
                     e.b = 0;
-                    if (te.kind == K10S_EV_AS_CREATE_NODE_REQ) {
-                        e.a = sc->def_node[te.arg];
-                        e.b = te.arg;
+                    if (tk == K10S_EV_AS_CREATE_NODE_REQ) {
+                        e.a = sc->def_node[ta];
+                        e.b = ta;
                     }
                     from_trace = true;
                     have = true;
                     break;
                 }
             }
-            e = c.v.heap()[0];
-            if (e.kind == K10S_EV_N_POD_FINISHED && c.v.pod(e.a).finish_seq != e.seq) {  // canceled
+            if (e.kind == K10S_EV_N_POD_FINISHED && c.V().pod(e.a).finish_seq != e.seq) {  // canceled
                 heap_pop(c);
                 continue;
             }
@@ -1494,12 +1562,12 @@ K10S_HD int run_replica(const Scenario* sc, const Params* pr, const Layout* L, u
             break;
         }
         if (!have) {
-            if (mode == K10S_RUN_UNTIL_TIME) c.clock = until_time;
+            if (mode == K10S_RUN_UNTIL_TIME) h->clock = until_time;
             status = mode == K10S_RUN_UNTIL_TIME ? K10S_REPLICA_RUNNING : K10S_REPLICA_FINISHED;
             break;
         }
         if (mode == K10S_RUN_UNTIL_TIME && e.time > until_time) {
-            c.clock = until_time;
+            h->clock = until_time;
             break;
         }
         if (mode == K10S_RUN_UNTIL_ALL_FINISHED && e.time > max_time) {
@@ -1510,16 +1578,16 @@ K10S_HD int run_replica(const Scenario* sc, const Params* pr, const Layout* L, u
             more = 1;
             break;
         }
-        if (from_trace) c.trace_cursor++;
+        if (from_trace) h->trace_cursor += 1;
         else heap_pop(c);
-        c.clock = e.time;
-        c.cur_kind = e.kind;
-        c.cur_seq = e.seq;
+        h->clock = e.time;
+        h->cur_kind = e.kind;
+        h->cur_seq = e.seq;
         done++;
         h->counters[K10S_C_EVENTS] += 1;
-        if (L->cap_log) {
+        if (cap_log) {
             uint32_t k = h->log_n;
-            if (k < L->cap_log) {
+            if (k < cap_log) {
                 k10s_log_entry le;
                 le.time = e.time;
                 le.seq = e.seq;
@@ -1555,7 +1623,7 @@ K10S_HD int run_replica(const Scenario* sc, const Params* pr, const Layout* L, u
                 }
                 le.pod = pod;
                 le.node = node;
-                v.log()[k] = le;
+                c.V().log()[k] = le;
                 h->log_n = k + 1;
             } else {
                 h->flags |= 1u;
@@ -1563,13 +1631,7 @@ K10S_HD int run_replica(const Scenario* sc, const Params* pr, const Layout* L, u
         }
         dispatch(c, e);
     }
-    if (c.err) status = K10S_REPLICA_ERROR;
-    h->clock = c.clock;
-    h->next_seq = c.next_seq;
-    h->heap_size = c.heap_size;
-    h->aq_size = c.aq_size;
-    h->uq_size = c.uq_size;
-    h->trace_cursor = c.trace_cursor;
+    if (h->error_code) status = K10S_REPLICA_ERROR;
     h->status = status;
     return more;
 }

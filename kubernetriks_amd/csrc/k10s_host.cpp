@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -14,11 +15,9 @@
 
 using namespace k10s;
 
-hipError_t k10s_launch_init(const Scenario& sc, const Params* d_params, const Layout& L, uint8_t* d_state,
-                            uint32_t n_replicas, hipStream_t s);
-hipError_t k10s_launch_run(const Scenario& sc, const Params* d_params, const Layout& L, uint8_t* d_state,
-                           uint32_t n_replicas, int mode, double until_time, double max_time, uint64_t budget,
-                           uint32_t* d_active, hipStream_t s);
+hipError_t k10s_launch_init(const DevConst* h_dc, uint32_t n_replicas, hipStream_t s);
+hipError_t k10s_launch_run(const DevConst* h_dc, uint32_t n_replicas, int mode, double until_time, double max_time,
+                           uint64_t budget, uint32_t* d_active, hipStream_t s);
 hipError_t k10s_launch_schedule(const uint32_t* alloc_cpu, const uint64_t* alloc_ram, const uint64_t* present,
                                 uint32_t n_nodes, uint32_t node_stride, const uint32_t* req_cpu, const uint64_t* req_ram,
                                 double weight, uint32_t n_problems, int32_t* out_node, int32_t* out_status,
@@ -50,9 +49,22 @@ struct k10s_engine {
     Params* d_params = nullptr;
     uint32_t* d_active = nullptr;
     uint32_t* h_active = nullptr;  // pinned
+    DevConst* h_dc = nullptr;      // pinned launch constants
     std::vector<Params> params;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
+
+// All engines of a device launch on one stream: the launch constants are one __constant__ block per
+// device (k10s_kernels.hip), so launches of different engines must not overlap.
+static hipStream_t engine_stream(int device) {
+    static std::mutex mu;
+    static std::vector<hipStream_t> streams;
+    std::lock_guard<std::mutex> g(mu);
+    if ((int)streams.size() <= device) streams.resize(device + 1, nullptr);
+    if (!streams[device] && hipStreamCreateWithFlags(&streams[device], hipStreamNonBlocking) != hipSuccess)
+        streams[device] = nullptr;
+    return streams[device];
+}
 
 static void engine_free(k10s_engine* e) {
     if (!e) return;
@@ -62,15 +74,15 @@ static void engine_free(k10s_engine* e) {
     if (e->d_params) (void)hipFree(e->d_params);
     if (e->d_active) (void)hipFree(e->d_active);
     if (e->h_active) (void)hipHostFree(e->h_active);
+    if (e->h_dc) (void)hipHostFree(e->h_dc);
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
-    if (e->stream) (void)hipStreamDestroy(e->stream);
-    delete e;
+    delete e;  // e->stream is the device's shared engine stream: not destroyed
 }
 
 static int32_t engine_init(k10s_engine* e) {
     HIPCHK(hipSetDevice(e->device));
-    HIPCHK(k10s_launch_init(e->dsc, e->d_params, e->L, e->d_state, e->R, e->stream));
+    HIPCHK(k10s_launch_init(e->h_dc, e->R, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     return K10S_OK;
 }
@@ -241,7 +253,7 @@ k10s_engine* k10s_engine_create(const char* scenario_text, const k10s_replica_pa
         return nullptr;
     };
     if (hipSetDevice(device) != hipSuccess) return fail("hipSetDevice");
-    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return fail("hipStreamCreate");
+    if (!(e->stream = engine_stream(device))) return fail("hipStreamCreate");
     (void)hipEventCreate(&e->ev0);
     (void)hipEventCreate(&e->ev1);
     Scenario offs;
@@ -263,6 +275,12 @@ k10s_engine* k10s_engine_create(const char* scenario_text, const k10s_replica_pa
         return fail("upload params");
     if (hipMalloc(&e->d_active, 64) != hipSuccess) return fail("hipMalloc active");
     if (hipHostMalloc(&e->h_active, 64) != hipSuccess) return fail("hipHostMalloc");
+    if (hipHostMalloc(&e->h_dc, sizeof(DevConst)) != hipSuccess) return fail("hipHostMalloc");
+    std::memset(e->h_dc, 0, sizeof(DevConst));
+    e->h_dc->sc = e->dsc;
+    e->h_dc->L = e->L;
+    e->h_dc->params = e->d_params;
+    e->h_dc->base = e->d_state;
     if (engine_init(e) != K10S_OK) {
         std::string m = g_err;
         engine_free(e);
@@ -291,8 +309,8 @@ int32_t k10s_engine_step_async(k10s_engine* e, int32_t mode, double until_time, 
     if (mode != K10S_RUN_UNTIL_ALL_FINISHED && mode != K10S_RUN_UNTIL_TIME) return set_err(K10S_E_INVALID, "bad mode");
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipMemsetAsync(e->d_active, 0, 4, e->stream));
-    HIPCHK(k10s_launch_run(e->dsc, e->d_params, e->L, e->d_state, e->R, mode, until_time, max_time,
-                           max_events_per_launch, e->d_active, e->stream));
+    HIPCHK(k10s_launch_run(e->h_dc, e->R, mode, until_time, max_time, max_events_per_launch, e->d_active,
+                           e->stream));
     HIPCHK(hipMemcpyAsync(e->h_active, e->d_active, 4, hipMemcpyDeviceToHost, e->stream));
     return K10S_OK;
 }

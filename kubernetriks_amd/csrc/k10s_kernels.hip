@@ -12,6 +12,9 @@
 // like the Rust reference (correctly rounded division, no FMA contraction).
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
+#define K10S_KERNEL_TU 1
 #include "k10s_engine.h"
 
 using namespace k10s;
@@ -19,7 +22,7 @@ using namespace k10s;
 // Occupancy knob for the event-loop kernel (0 = compiler default).  amdgpu_waves_per_eu(n) caps
 // the register allocation so that n waves fit per SIMD.
 #ifndef K10S_WAVES_PER_EU
-#define K10S_WAVES_PER_EU 0
+#define K10S_WAVES_PER_EU 4
 #endif
 #if K10S_WAVES_PER_EU > 0
 #define K10S_RUN_BOUNDS __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(K10S_WAVES_PER_EU)))
@@ -27,31 +30,35 @@ using namespace k10s;
 #define K10S_RUN_BOUNDS __launch_bounds__(64)
 #endif
 
-__global__ __launch_bounds__(64) void k10s_init_kernel(Scenario sc, const Params* __restrict__ params, Layout L,
-                                                         uint8_t* base, uint32_t n_replicas) {
-    uint32_t r = blockIdx.x;
-    if (r >= n_replicas) return;
-    Params p = params[r];
-    init_replica(&sc, &p, &L, base, r);
-}
-
-__global__ K10S_RUN_BOUNDS void k10s_run_kernel(Scenario sc, const Params* __restrict__ params, Layout L,
-                                                        uint8_t* base, uint32_t n_replicas, int mode, double until_time,
-                                                        double max_time, uint64_t budget, uint32_t* active) {
-    uint32_t r = blockIdx.x;
-    if (r >= n_replicas) return;
-    Params p = params[r];
-    // stage the replica header in LDS for the whole launch
-    __shared__ RepHdr hdr;
+// Stage replica r's header between HBM and the LDS working copy k10s_hdr (dword-wise, 64 lanes).
+__device__ __forceinline__ void hdr_copy(uint32_t* dst, const uint32_t* src) {
     constexpr uint32_t W = sizeof(RepHdr) / 4;
     static_assert(sizeof(RepHdr) % 4 == 0, "RepHdr must be a whole number of dwords");
-    uint32_t* g = reinterpret_cast<uint32_t*>(base + (uint64_t)r * L.stride + L.hdr);
-    uint32_t* s = reinterpret_cast<uint32_t*>(&hdr);
-    for (uint32_t i = threadIdx.x; i < W; i += 64) s[i] = g[i];
+    for (uint32_t i = threadIdx.x; i < W; i += 64) dst[i] = src[i];
     __syncthreads();
-    int more = run_replica(&sc, &p, &L, base, r, mode, until_time, max_time, budget, &hdr);
+}
+__device__ __forceinline__ uint32_t* hdr_global(uint32_t r) {
+    return (uint32_t*)(k10s_dc.base + (uint64_t)r * k10s_dc.L.stride + k10s_dc.L.hdr);
+}
+
+__global__ __launch_bounds__(64) void k10s_init_kernel(uint32_t n_replicas) {
+    uint32_t r = blockIdx.x;
+    if (r >= n_replicas) return;
+    Ctx c;
+    init_replica(c);
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < W; i += 64) g[i] = s[i];
+    hdr_copy(hdr_global(r), (const uint32_t*)&k10s_hdr);
+}
+
+__global__ K10S_RUN_BOUNDS void k10s_run_kernel(uint32_t n_replicas, int mode, double until_time, double max_time,
+                                                uint64_t budget, uint32_t* active) {
+    uint32_t r = blockIdx.x;
+    if (r >= n_replicas) return;
+    hdr_copy((uint32_t*)&k10s_hdr, hdr_global(r));
+    Ctx c;
+    int more = run_replica(c, mode, until_time, max_time, budget);
+    __syncthreads();
+    hdr_copy(hdr_global(r), (const uint32_t*)&k10s_hdr);
     if (more && threadIdx.x == 0) atomicAdd(active, 1u);
 }
 
@@ -85,17 +92,30 @@ __global__ __launch_bounds__(64) void k10s_schedule_kernel(const uint32_t* __res
 }
 
 // ---- launchers (called from k10s_host.cpp) -------------------------------------------------------
-hipError_t k10s_launch_init(const Scenario& sc, const Params* d_params, const Layout& L, uint8_t* d_state,
-                            uint32_t n_replicas, hipStream_t s) {
-    hipLaunchKernelGGL(k10s_init_kernel, dim3(n_replicas), dim3(64), 0, s, sc, d_params, L, d_state, n_replicas);
+// The launch constants live in the one __constant__ block k10s_dc, so every engine launch first
+// copies its block (from pinned host memory, stream-ordered) and then launches; engines of a device
+// share one stream (k10s_host.cpp), and the mutex keeps each (copy, launch) pair adjacent in it.
+static std::mutex g_launch_mu;
+
+static hipError_t upload(const DevConst* h_dc, hipStream_t s) {
+    return hipMemcpyToSymbolAsync(HIP_SYMBOL(k10s_dc), h_dc, sizeof(DevConst), 0, hipMemcpyHostToDevice, s);
+}
+
+hipError_t k10s_launch_init(const DevConst* h_dc, uint32_t n_replicas, hipStream_t s) {
+    std::lock_guard<std::mutex> g(g_launch_mu);
+    hipError_t e = upload(h_dc, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k10s_init_kernel, dim3(n_replicas), dim3(64), 0, s, n_replicas);
     return hipGetLastError();
 }
 
-hipError_t k10s_launch_run(const Scenario& sc, const Params* d_params, const Layout& L, uint8_t* d_state,
-                           uint32_t n_replicas, int mode, double until_time, double max_time, uint64_t budget,
-                           uint32_t* d_active, hipStream_t s) {
-    hipLaunchKernelGGL(k10s_run_kernel, dim3(n_replicas), dim3(64), 0, s, sc, d_params, L, d_state, n_replicas, mode,
-                       until_time, max_time, budget, d_active);
+hipError_t k10s_launch_run(const DevConst* h_dc, uint32_t n_replicas, int mode, double until_time, double max_time,
+                           uint64_t budget, uint32_t* d_active, hipStream_t s) {
+    std::lock_guard<std::mutex> g(g_launch_mu);
+    hipError_t e = upload(h_dc, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k10s_run_kernel, dim3(n_replicas), dim3(64), 0, s, n_replicas, mode, until_time, max_time,
+                       budget, d_active);
     return hipGetLastError();
 }
 

@@ -16,6 +16,18 @@
 #include "../../include/k10s_events.h"
 #include "k10s_common.h"
 
+// Device address spaces (gfx950): the compiled scenario is immutable for a launch, so its tables
+// are read through constant-address-space pointers (scalar loads through the scalar cache when
+// the index is wave-uniform); per-replica state is global memory.  Host code (and the device pass
+// of the host-only translation units) sees plain pointers of the same size.
+#if K10S_DEVICE && defined(K10S_KERNEL_TU)
+#define K10S_RO(T) const __attribute__((address_space(4))) T*
+#define K10S_GB(T) __attribute__((address_space(1))) T*
+#else
+#define K10S_RO(T) const T*
+#define K10S_GB(T) T*
+#endif
+
 namespace k10s {
 
 struct TraceEv {          // one client-emitted trace event (simulator.rs:234-253)
@@ -41,50 +53,50 @@ struct Scenario {
     uint32_t first_dynamic_seq;
     uint64_t total_pods_in_trace, total_nodes_in_trace;
 
-    const uint32_t* node_uid;      // [N]
-    const uint32_t* def_node;      // [D] node idx of node instance def
-    const uint32_t* def_cpu;       // [D] capacity
-    const uint64_t* def_ram;
-    const int32_t* def_ca_group;   // [D] "node_group" label -> CA group idx (-1 none, -2 unknown)
-    const uint8_t* def_ca_origin;  // [D] label origin == "cluster autoscaler"
-    const uint32_t* pod_uid;       // [P]
-    const uint32_t* pod_cpu;       // [P] requests
-    const uint64_t* pod_ram;
-    const double* pod_dur;
-    const uint8_t* pod_flags;
-    const int32_t* pod_group;      // [P] pod group idx or -1
-    const uint32_t* pod_key;       // [P] perturbation key (workload-trace position)
-    const uint32_t* default_defs;  // [n_default] defs of default-cluster nodes, slot order
-    const TraceEv* trace;          // [n_trace] merged (time, seq) order
+    K10S_RO(uint32_t) node_uid;      // [N]
+    K10S_RO(uint32_t) def_node;      // [D] node idx of node instance def
+    K10S_RO(uint32_t) def_cpu;       // [D] capacity
+    K10S_RO(uint64_t) def_ram;
+    K10S_RO(int32_t) def_ca_group;   // [D] "node_group" label -> CA group idx (-1 none, -2 unknown)
+    K10S_RO(uint8_t) def_ca_origin;  // [D] label origin == "cluster autoscaler"
+    K10S_RO(uint32_t) pod_uid;       // [P]
+    K10S_RO(uint32_t) pod_cpu;       // [P] requests
+    K10S_RO(uint64_t) pod_ram;
+    K10S_RO(double) pod_dur;
+    K10S_RO(uint8_t) pod_flags;
+    K10S_RO(int32_t) pod_group;      // [P] pod group idx or -1
+    K10S_RO(uint32_t) pod_key;       // [P] perturbation key (workload-trace position)
+    K10S_RO(uint32_t) default_defs;  // [n_default] defs of default-cluster nodes, slot order
+    K10S_RO(TraceEv) trace;          // [n_trace] merged (time, seq) order
 
     // pod groups (name order)
-    const uint32_t* g_initial;
-    const uint32_t* g_max;
-    const uint32_t* g_cpu;
-    const uint64_t* g_ram;
-    const uint8_t* g_flags;
-    const double* g_tcpu;
-    const double* g_tram;
-    const uint8_t* g_cpu_kind;
-    const uint8_t* g_ram_kind;
-    const double* g_cpu_usage;
-    const double* g_ram_usage;
-    const uint32_t* g_cpu_uoff;
-    const uint32_t* g_cpu_ucnt;
-    const uint32_t* g_ram_uoff;
-    const uint32_t* g_ram_ucnt;
-    const uint32_t* g_pod;         // [G*group_bound] pod idx of "{g}_{k}"
-    const uint32_t* g_pos;         // [G*group_bound] name-order position of k within the group
-    const uint32_t* g_sorted_k;    // [G*group_bound] k at name-order position j
-    const double* unit_dur;
-    const double* unit_load;
+    K10S_RO(uint32_t) g_initial;
+    K10S_RO(uint32_t) g_max;
+    K10S_RO(uint32_t) g_cpu;
+    K10S_RO(uint64_t) g_ram;
+    K10S_RO(uint8_t) g_flags;
+    K10S_RO(double) g_tcpu;
+    K10S_RO(double) g_tram;
+    K10S_RO(uint8_t) g_cpu_kind;
+    K10S_RO(uint8_t) g_ram_kind;
+    K10S_RO(double) g_cpu_usage;
+    K10S_RO(double) g_ram_usage;
+    K10S_RO(uint32_t) g_cpu_uoff;
+    K10S_RO(uint32_t) g_cpu_ucnt;
+    K10S_RO(uint32_t) g_ram_uoff;
+    K10S_RO(uint32_t) g_ram_ucnt;
+    K10S_RO(uint32_t) g_pod;         // [G*group_bound] pod idx of "{g}_{k}"
+    K10S_RO(uint32_t) g_pos;         // [G*group_bound] name-order position of k within the group
+    K10S_RO(uint32_t) g_sorted_k;    // [G*group_bound] k at name-order position j
+    K10S_RO(double) unit_dur;
+    K10S_RO(double) unit_load;
 
     // cluster-autoscaler node groups (name order; cluster_autoscaler.rs:175-200)
-    const uint8_t* ca_has_max;
-    const uint64_t* ca_max;
-    const uint32_t* ca_def;        // [CG*ca_bound] def of "{group}_{k}", k = 1..ca_bound
-    const uint32_t* ca_cpu;
-    const uint64_t* ca_ram;
+    K10S_RO(uint8_t) ca_has_max;
+    K10S_RO(uint64_t) ca_max;
+    K10S_RO(uint32_t) ca_def;        // [CG*ca_bound] def of "{group}_{k}", k = 1..ca_bound
+    K10S_RO(uint32_t) ca_cpu;
+    K10S_RO(uint64_t) ca_ram;
 };
 
 // Replica parameters as consumed by the device (k10s_replica_params with derived fields).
@@ -136,7 +148,8 @@ struct RepHdr {
     uint32_t place_n;
     uint32_t flags;
     uint32_t unsched_cache_count;
-    uint32_t pad[3];
+    uint32_t cur_kind, cur_seq;   // event being handled (panic attribution)
+    uint32_t pad;
 };
 
 struct HeapEv {             // dslab Event {id, time, dst, data}, 32 B
@@ -235,40 +248,12 @@ struct Layout {
     uint32_t pad;
 };
 
-// Typed accessors over one replica's region; bases are recomputed from the (constant) layout at
-// each use instead of being held live across the event loop.
-struct Rep {
-    uint8_t* b;
-    const Layout* L;
-    K10S_HD RepHdr* h() const { return (RepHdr*)(b + L->hdr); }
-    K10S_HD uint32_t* s_cpu() const { return (uint32_t*)(b + L->s_cpu); }
-    K10S_HD uint64_t* s_ram() const { return (uint64_t*)(b + L->s_ram); }
-    K10S_HD uint64_t* s_present() const { return (uint64_t*)(b + L->s_present); }
-    K10S_HD NodeState& node(uint32_t n) const { return ((NodeState*)(b + L->node))[n]; }
-    K10S_HD uint64_t* pend_rm() const { return (uint64_t*)(b + L->pend_rm); }
-    K10S_HD PodState& pod(uint32_t p) const { return ((PodState*)(b + L->pod))[p]; }
-    K10S_HD k10s_pod_record* prec() const { return L->rec_on ? (k10s_pod_record*)(b + L->prec) : nullptr; }
-    K10S_HD SlotState& slot(int32_t s) const { return ((SlotState*)(b + L->slot))[s]; }
-    K10S_HD uint32_t* pool_ring() const { return (uint32_t*)(b + L->pool_ring); }
-    K10S_HD GroupState* grp() const { return (GroupState*)(b + L->grp); }
-    K10S_HD uint64_t* grp_bits() const { return (uint64_t*)(b + L->grp_bits); }
-    K10S_HD uint32_t* cag() const { return (uint32_t*)(b + L->cag); }
-    K10S_HD CAAct* ca_act() const { return (CAAct*)(b + L->ca_act); }
-    K10S_HD uint32_t* ca_cpu() const { return (uint32_t*)(b + L->ca_cpu); }
-    K10S_HD uint64_t* ca_ram() const { return (uint64_t*)(b + L->ca_ram); }
-    K10S_HD uint32_t* ca_undo() const { return (uint32_t*)(b + L->ca_undo); }
-    K10S_HD HeapEv* heap() const { return (HeapEv*)(b + L->heap); }
-    K10S_HD QInfo* aq() const { return (QInfo*)(b + L->aq); }
-    K10S_HD QInfo* uq() const { return (QInfo*)(b + L->uq); }
-    K10S_HD k10s_log_entry* log() const { return L->cap_log ? (k10s_log_entry*)(b + L->log) : nullptr; }
-    K10S_HD k10s_placement* place() const { return L->cap_place ? (k10s_placement*)(b + L->place) : nullptr; }
+// Everything a launch reads but never writes, as one block (device: __constant__ memory).
+struct DevConst {
+    Scenario sc;
+    Layout L;
+    K10S_RO(Params) params;   // [n_replicas]
+    K10S_GB(uint8_t) base;    // replica regions, stride L.stride
 };
-
-K10S_HD Rep make_rep(uint8_t* base, const Layout& L, uint32_t r) {
-    Rep v;
-    v.b = base + (uint64_t)r * L.stride;
-    v.L = &L;
-    return v;
-}
 
 }  // namespace k10s

@@ -24,6 +24,18 @@ struct HC {
     uint32_t R = 0;
 };
 
+// The engine's working header is a separate copy during a run, like the LDS staging of the device
+// kernels, so code that bypassed it would diverge here too.
+static Ctx make_ctx(HC* h, uint32_t r, RepHdr* work) {
+    Ctx c;
+    c.sc = &h->sc;
+    c.pr = &h->params[r];
+    c.h = work;
+    c.v = make_rep(h->state.data(), h->L, r);
+    c.Lp = &h->L;
+    return c;
+}
+
 extern "C" {
 
 void* hc_create(const char* text, const k10s_replica_params* params, uint32_t R, const k10s_capacities* caps,
@@ -54,7 +66,13 @@ void* hc_create(const char* text, const k10s_replica_params* params, uint32_t R,
         h->params[r].ca_max_node_count = h->hs.defaults.ca_max_node_count;
     }
     h->state.assign((size_t)h->L.stride * R, 0);
-    for (uint32_t r = 0; r < R; r++) init_replica(&h->sc, &h->params[r], &h->L, h->state.data(), r);
+    for (uint32_t r = 0; r < R; r++) {
+        RepHdr work;
+        std::memset(&work, 0xA5, sizeof work);
+        Ctx c = make_ctx(h, r, &work);
+        init_replica(c);
+        *c.v.h() = work;
+    }
     return h;
 }
 void hc_free(void* p) { delete (HC*)p; }
@@ -66,8 +84,13 @@ int hc_run(void* p, int mode, double until, double max_time, uint64_t budget) {
     HC* h = (HC*)p;
     int active = 0;
     for (uint32_t r = 0; r < h->R; r++) {
-        Rep v = make_rep(h->state.data(), h->L, r);
-        while (run_replica(&h->sc, &h->params[r], &h->L, h->state.data(), r, mode, until, max_time, budget, v.h())) {
+        RepHdr work;
+        Ctx c = make_ctx(h, r, &work);
+        int more = 1;
+        while (more) {  // one iteration = one device launch: stage, run, write back
+            work = *c.v.h();
+            more = run_replica(c, mode, until, max_time, budget);
+            *c.v.h() = work;
         }
     }
     return active;
