@@ -145,7 +145,10 @@ typedef struct k10s_capacities {
     uint32_t event_heap, active_queue, unschedulable, group_name_bound, ca_name_bound;
     uint32_t event_log, placement_log;   /* parity mode logs; 0 = off */
     uint32_t pod_records;                /* 1 = keep per-pod start/finish/removal times */
+    uint32_t delay_fifo;                 /* entries per delay-class event ring: 0 = default (512),
+                                            K10S_FIFO_OFF = every event in the heap */
 } k10s_capacities;
+#define K10S_FIFO_OFF 0xFFFFFFFFu
 
 /* Parity event-log entry: one delivered event (time, id order). */
 typedef struct k10s_log_entry {

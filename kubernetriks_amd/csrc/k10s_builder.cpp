@@ -653,6 +653,14 @@ Layout make_layout(const HostScenario& hs, const k10s_capacities& caps) {
     L.cap_log = caps.event_log;
     L.cap_place = caps.placement_log;
     L.rec_on = caps.pod_records ? 1 : 0;
+    if (caps.delay_fifo == K10S_FIFO_OFF) {
+        L.cap_fq = 0;
+    } else {
+        uint32_t want = caps.delay_fifo ? caps.delay_fifo : 512u;
+        if (want > (1u << 20)) want = 1u << 20;
+        L.cap_fq = 1;
+        while (L.cap_fq < want) L.cap_fq <<= 1;
+    }
     uint64_t off = 0;
     auto take = [&](uint64_t bytes) {
         uint64_t o = off;
@@ -683,6 +691,7 @@ Layout make_layout(const HostScenario& hs, const k10s_capacities& caps) {
     L.uq = take(sizeof(QInfo) * (uint64_t)L.cap_uq);
     L.log = take(sizeof(k10s_log_entry) * (uint64_t)L.cap_log);
     L.place = take(sizeof(k10s_placement) * (uint64_t)L.cap_place);
+    L.fq = take(sizeof(HeapEv) * (uint64_t)L.cap_fq * K10S_NFQ);
     L.stride = (off + 4095) & ~(uint64_t)4095;
     return L;
 }

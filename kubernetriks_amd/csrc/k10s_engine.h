@@ -62,6 +62,7 @@ struct Rep {
     K10S_HD uint64_t* ca_ram() const { return at<uint64_t>(L().ca_ram); }
     K10S_HD uint32_t* ca_undo() const { return at<uint32_t>(L().ca_undo); }
     K10S_HD HeapEv* heap() const { return at<HeapEv>(L().heap); }
+    K10S_HD HeapEv* fq() const { return at<HeapEv>(L().fq); }
     K10S_HD QInfo* aq() const { return at<QInfo>(L().aq); }
     K10S_HD QInfo* uq() const { return at<QInfo>(L().uq); }
     K10S_HD k10s_log_entry* log() const { return L().cap_log ? at<k10s_log_entry>(L().log) : nullptr; }
@@ -164,27 +165,61 @@ K10S_HD bool ev_before(double ta, uint32_t sa, double tb, uint32_t sb) {
 // 8 children of a level (256 contiguous bytes) are loaded and compared by 8 lanes at once.
 #define K10S_HEAP_D 8
 
-K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uint32_t a, uint32_t b, double x) {
-    if (c.H().error_code) return 0;
-    if (c.H().next_seq == 0xFFFFFFFFu) {
+// Delay classes: every emission site with a constant network delay (or delay 0) names its class;
+// emissions of one class happen in nondecreasing clock order, so clock + delay is nondecreasing
+// and ids increase: each class is a sorted run and goes to its FIFO ring.  An entry that would
+// break the run (a variable delay, or a full ring) goes to the heap instead, so correctness never
+// depends on the classification.  Ticks, the scheduling cycle and pod-finish self-events (variable
+// delays) always use the heap.
+enum : int {
+    FQ_HEAP = -1,
+    FQ_AS_TO_PS = 0,     // api server <-> persistent storage
+    FQ_PS_TO_SCHED = 1,  // persistent storage -> scheduler
+    FQ_SCHED_TO_AS = 2,  // scheduler -> api server (PodNotScheduled)
+    FQ_ASSIGN = 3,       // scheduler -> api server (AssignPodToNodeRequest: cycle offset + delay)
+    FQ_AS_TO_NODE = 4,   // api server <-> node components
+    FQ_AS_TO_CA = 5,     // cluster autoscaler / HPA actions
+    FQ_AS_TO_HPA = 6,
+    FQ_NOW = 7,          // emit_now (delay 0)
+};
+
+K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uint32_t a, uint32_t b, double x,
+                          int cls = FQ_HEAP) {
+    RepHdr& H = c.H();
+    if (H.error_code) return 0;
+    if (H.next_seq == 0xFFFFFFFFu) {
         fail(c, K10S_ERR_SEQ_OVERFLOW);
         return 0;
     }
-    if (c.H().heap_size >= c.Ly().cap_heap) {
-        fail(c, K10S_ERR_HEAP_FULL);
-        return 0;
-    }
     HeapEv e;
-    e.time = c.H().clock + delay;
-    e.seq = c.H().next_seq++;
+    e.time = H.clock + delay;
+    e.seq = H.next_seq;
     e.kind = (uint16_t)kind;
     e.slot = (int16_t)slot;
     e.a = a;
     e.b = b;
     e.x = x;
+    const int64_t k = total_key(e.time);
+    const uint32_t cap = c.Ly().cap_fq;
+    if (cls >= 0 && cap) {
+        const uint32_t hd = H.fq_head[cls], tl = H.fq_tail[cls];
+        if (tl - hd < cap && (tl == hd || k >= total_key(H.fq_last[cls]))) {
+            c.V().fq()[(uint32_t)cls * cap + (tl & (cap - 1))] = e;
+            if (tl == hd) H.fq_top[cls] = e;
+            H.fq_tail[cls] = tl + 1;
+            H.fq_last[cls] = e.time;
+            H.next_seq = e.seq + 1;
+            return e.seq;
+        }
+    }
+    if (H.heap_size >= c.Ly().cap_heap) {
+        fail(c, K10S_ERR_HEAP_FULL);
+        return 0;
+    }
+    H.next_seq = e.seq + 1;
     HeapEv* hp = c.V().heap();
-    uint32_t pos = c.H().heap_size++;
-    int64_t k = total_key(e.time);
+    uint32_t pos = H.heap_size;
+    H.heap_size = pos + 1;
     while (pos > 0) {
         uint32_t parent = (pos - 1) / K10S_HEAP_D;
         HeapEv p = hp[parent];
@@ -194,6 +229,7 @@ K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uin
         pos = parent;
     }
     hp[pos] = e;
+    if (pos == 0) H.heap_top = e;
     return e.seq;
 }
 K10S_HD uint32_t emit0(Ctx& c, uint32_t kind, double delay) { return emit(c, kind, delay, -1, 0, 0, 0.0); }
@@ -247,7 +283,8 @@ K10S_HD uint32_t heap_min_child(const HeapEv* hp, uint32_t first, uint32_t n, in
 
 K10S_HELPER void heap_pop(Ctx& c) {
     HeapEv* hp = c.V().heap();
-    uint32_t n = --c.H().heap_size;
+    uint32_t n = c.H().heap_size - 1;
+    c.H().heap_size = n;
     if (n == 0) return;
     HeapEv last = hp[n];
     int64_t kl = total_key(last.time);
@@ -259,10 +296,13 @@ K10S_HELPER void heap_pop(Ctx& c) {
         uint32_t sm;
         uint32_t m = heap_min_child(hp, first, n, km, sm);
         if (!(km < kl || (km == kl && sm < last.seq))) break;
-        hp[pos] = hp[m];
+        HeapEv child = hp[m];
+        hp[pos] = child;
+        if (pos == 0) c.H().heap_top = child;
         pos = m;
     }
     hp[pos] = last;
+    if (pos == 0) c.H().heap_top = last;
 }
 
 // ---- Rust std BinaryHeap<QueuedPodInfo> (scheduler action queue) ------------------------------
@@ -516,7 +556,7 @@ K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
         if (st != K10S_SCHED_OK) {
             q.timestamp = t + cycle_dur;
             uq_insert(c, q);
-            emit(c, K10S_EV_AS_POD_NOT_SCHEDULED, c.P().sched_to_as_network_delay, -1, p, 0, t + cycle_dur);
+            emit(c, K10S_EV_AS_POD_NOT_SCHEDULED, c.P().sched_to_as_network_delay, -1, p, 0, t + cycle_dur, FQ_SCHED_TO_AS);
             continue;
         }
         uint32_t n = (uint32_t)chosen;
@@ -524,7 +564,7 @@ K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
         c.V().s_ram()[n] -= rr;
         c.V().node(n).flags |= NF_S_ASSIGN;  // assign_node_to_pod (125-151)
         c.V().pod(p).s_assigned = (int32_t)n;
-        emit(c, K10S_EV_AS_ASSIGN_REQ, cycle_dur + c.P().sched_to_as_network_delay, -1, p, n, t + cycle_dur);
+        emit(c, K10S_EV_AS_ASSIGN_REQ, cycle_dur + c.P().sched_to_as_network_delay, -1, p, n, t + cycle_dur, FQ_ASSIGN);
         h->counters[K10S_C_PLACEMENTS] += 1;
         if (c.V().place()) {
             uint32_t k = h->place_n;
@@ -854,7 +894,7 @@ K10S_WARM void on_ps(Ctx& c, HeapEv e) {
         c.V().node(n).ps_ram = c.S().def_ram[def];
         c.V().node(n).ps_epoch += 1;
         h->ps_node_count += 1;
-        emit(c, K10S_EV_AS_CREATE_NODE_RESP, pr->as_to_ps_network_delay, -1, n, 0, 0.0);
+        emit(c, K10S_EV_AS_CREATE_NODE_RESP, pr->as_to_ps_network_delay, -1, n, 0, 0.0, FQ_AS_TO_PS);
         break;
     }
     case K10S_EV_PS_NODE_ADDED: {
@@ -863,7 +903,7 @@ K10S_WARM void on_ps(Ctx& c, HeapEv e) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
         }
-        emit(c, K10S_EV_S_ADD_NODE, pr->ps_to_sched_network_delay, -1, n, c.V().node(n).ps_cpu, u2f(c.V().node(n).ps_ram));
+        emit(c, K10S_EV_S_ADD_NODE, pr->ps_to_sched_network_delay, -1, n, c.V().node(n).ps_cpu, u2f(c.V().node(n).ps_ram), FQ_PS_TO_SCHED);
         h->counters[K10S_C_PROCESSED_NODES] += 1;
         break;
     }
@@ -876,7 +916,7 @@ K10S_WARM void on_ps(Ctx& c, HeapEv e) {
         c.V().pod(p).flags |= PF_IN_PS;
         c.V().pod(p).ps_assigned = -1;
         if (c.V().prec()) c.V().prec()[p].state = 1;
-        emit(c, K10S_EV_S_POD_SCHEDULE_REQ, pr->ps_to_sched_network_delay, -1, p, 0, 0.0);
+        emit(c, K10S_EV_S_POD_SCHEDULE_REQ, pr->ps_to_sched_network_delay, -1, p, 0, 0.0, FQ_PS_TO_SCHED);
         break;
     }
     case K10S_EV_PS_ASSIGN_REQ: {
@@ -897,7 +937,7 @@ K10S_WARM void on_ps(Ctx& c, HeapEv e) {
         c.V().node(n).ps_cpu -= c.V().pod(p).req_cpu;
         c.V().node(n).ps_ram -= c.V().pod(p).req_ram;
         c.V().pod(p).ps_aepoch = c.V().node(n).ps_epoch;
-        emit(c, K10S_EV_AS_ASSIGN_RESP, pr->as_to_ps_network_delay, -1, p, n, 0.0);
+        emit(c, K10S_EV_AS_ASSIGN_RESP, pr->as_to_ps_network_delay, -1, p, n, 0.0, FQ_AS_TO_PS);
         break;
     }
     case K10S_EV_PS_POD_NOT_SCHEDULED: {
@@ -936,7 +976,7 @@ K10S_WARM void on_ps(Ctx& c, HeapEv e) {
                 c.V().prec()[p].state = 2;
             }
         }
-        emit(c, K10S_EV_S_POD_FINISHED, pr->ps_to_sched_network_delay, -1, p, e.b, e.x);
+        emit(c, K10S_EV_S_POD_FINISHED, pr->ps_to_sched_network_delay, -1, p, e.b, e.x, FQ_PS_TO_SCHED);
         break;
     }
     case K10S_EV_PS_REMOVE_NODE_REQ: {
@@ -947,20 +987,20 @@ K10S_WARM void on_ps(Ctx& c, HeapEv e) {
         }
         c.V().node(n).flags &= (uint8_t)~NF_PS_PRESENT;
         h->ps_node_count -= 1;
-        emit(c, K10S_EV_AS_REMOVE_NODE_RESP, pr->as_to_ps_network_delay, -1, n, 0, 0.0);
+        emit(c, K10S_EV_AS_REMOVE_NODE_RESP, pr->as_to_ps_network_delay, -1, n, 0, 0.0, FQ_AS_TO_PS);
         break;
     }
     case K10S_EV_PS_NODE_REMOVED:
-        emit(c, K10S_EV_S_REMOVE_NODE, pr->ps_to_sched_network_delay, -1, e.a, 0, 0.0);
+        emit(c, K10S_EV_S_REMOVE_NODE, pr->ps_to_sched_network_delay, -1, e.a, 0, 0.0, FQ_PS_TO_SCHED);
         break;
     case K10S_EV_PS_CA_REQ:
         ca_decide(c);
-        emit0(c, K10S_EV_AS_CA_RESP, pr->as_to_ps_network_delay);
+        emit(c, K10S_EV_AS_CA_RESP, pr->as_to_ps_network_delay, -1, 0, 0, 0.0, FQ_AS_TO_PS);
         break;
     case K10S_EV_PS_REMOVE_POD_REQ: {
         uint32_t p = e.a;
         if (!(c.V().pod(p).flags & PF_IN_PS)) {
-            emit(c, K10S_EV_AS_REMOVE_POD_RESP, pr->as_to_ps_network_delay, -1, p, 0, 0.0);
+            emit(c, K10S_EV_AS_REMOVE_POD_RESP, pr->as_to_ps_network_delay, -1, p, 0, 0.0, FQ_AS_TO_PS);
             return;
         }
         c.V().pod(p).flags &= (uint8_t)~PF_IN_PS;
@@ -974,13 +1014,13 @@ K10S_WARM void on_ps(Ctx& c, HeapEv e) {
             ps_clean_up(c, p);
             flag = 1;
         } else {
-            emit(c, K10S_EV_S_REMOVE_POD, pr->ps_to_sched_network_delay, -1, p, 0, 0.0);
+            emit(c, K10S_EV_S_REMOVE_POD, pr->ps_to_sched_network_delay, -1, p, 0, 0.0, FQ_PS_TO_SCHED);
         }
-        emit(c, K10S_EV_AS_REMOVE_POD_RESP, pr->as_to_ps_network_delay, -1, p, flag ? (uint32_t)n : 0u, u2f(flag));
+        emit(c, K10S_EV_AS_REMOVE_POD_RESP, pr->as_to_ps_network_delay, -1, p, flag ? (uint32_t)n : 0u, u2f(flag), FQ_AS_TO_PS);
         break;
     }
     case K10S_EV_PS_POD_REMOVED:
-        if (e.b) emit(c, K10S_EV_S_REMOVE_POD, pr->ps_to_sched_network_delay, -1, e.a, 0, 0.0);
+        if (e.b) emit(c, K10S_EV_S_REMOVE_POD, pr->ps_to_sched_network_delay, -1, e.a, 0, 0.0, FQ_PS_TO_SCHED);
         break;
     default:
         break;
@@ -998,7 +1038,7 @@ K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
         uint32_t def = e.b;
         uint32_t n = sc->def_node[def];
         c.V().node(n).pend_def = (int32_t)def;
-        emit(c, K10S_EV_PS_CREATE_NODE_REQ, pr->as_to_ps_network_delay, -1, n, def, 0.0);
+        emit(c, K10S_EV_PS_CREATE_NODE_REQ, pr->as_to_ps_network_delay, -1, n, def, 0.0, FQ_AS_TO_PS);
         break;
     }
     case K10S_EV_AS_CREATE_NODE_RESP: {  // handle_create_node (96-115)
@@ -1024,16 +1064,16 @@ K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
         }
         c.V().node(n).as_slot = (int32_t)slot;
         h->as_node_count += 1;
-        emit(c, K10S_EV_PS_NODE_ADDED, pr->as_to_ps_network_delay, -1, n, 0, e.time);
+        emit(c, K10S_EV_PS_NODE_ADDED, pr->as_to_ps_network_delay, -1, n, 0, e.time, FQ_AS_TO_PS);
         break;
     }
     case K10S_EV_AS_CREATE_POD_REQ:
-        emit(c, K10S_EV_PS_CREATE_POD_REQ, pr->as_to_ps_network_delay, -1, e.a, 0, 0.0);
+        emit(c, K10S_EV_PS_CREATE_POD_REQ, pr->as_to_ps_network_delay, -1, e.a, 0, 0.0, FQ_AS_TO_PS);
         break;
     case K10S_EV_AS_ASSIGN_REQ: {
         uint32_t n = e.b;
         if (bit_test(c.V().pend_rm(), sc->node_uid[n]) || c.V().node(n).as_slot < 0) return;
-        emit(c, K10S_EV_PS_ASSIGN_REQ, pr->as_to_ps_network_delay, -1, e.a, n, e.x);
+        emit(c, K10S_EV_PS_ASSIGN_REQ, pr->as_to_ps_network_delay, -1, e.a, n, e.x, FQ_AS_TO_PS);
         break;
     }
     case K10S_EV_AS_ASSIGN_RESP: {
@@ -1043,23 +1083,23 @@ K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
         }
-        emit(c, K10S_EV_N_BIND, pr->as_to_node_network_delay, slot, e.a, n, 0.0);
+        emit(c, K10S_EV_N_BIND, pr->as_to_node_network_delay, slot, e.a, n, 0.0, FQ_AS_TO_NODE);
         break;
     }
     case K10S_EV_AS_POD_NOT_SCHEDULED:
-        emit(c, K10S_EV_PS_POD_NOT_SCHEDULED, pr->as_to_ps_network_delay, -1, e.a, 0, e.x);
+        emit(c, K10S_EV_PS_POD_NOT_SCHEDULED, pr->as_to_ps_network_delay, -1, e.a, 0, e.x, FQ_AS_TO_PS);
         break;
     case K10S_EV_AS_POD_STARTED:
-        emit(c, K10S_EV_PS_POD_STARTED, pr->as_to_ps_network_delay, -1, e.a, 0, e.x);
+        emit(c, K10S_EV_PS_POD_STARTED, pr->as_to_ps_network_delay, -1, e.a, 0, e.x, FQ_AS_TO_PS);
         break;
     case K10S_EV_AS_POD_FINISHED:
         h->counters[K10S_C_TERMINATED_PODS] += 1;
         h->counters[K10S_C_PODS_SUCCEEDED] += 1;
-        emit(c, K10S_EV_PS_POD_FINISHED, pr->as_to_ps_network_delay, -1, e.a, e.b, e.x);
+        emit(c, K10S_EV_PS_POD_FINISHED, pr->as_to_ps_network_delay, -1, e.a, e.b, e.x, FQ_AS_TO_PS);
         break;
     case K10S_EV_AS_REMOVE_NODE_REQ:
         bit_set(c.V().pend_rm(), sc->node_uid[e.a]);
-        emit(c, K10S_EV_PS_REMOVE_NODE_REQ, pr->as_to_ps_network_delay, -1, e.a, 0, 0.0);
+        emit(c, K10S_EV_PS_REMOVE_NODE_REQ, pr->as_to_ps_network_delay, -1, e.a, 0, 0.0, FQ_AS_TO_PS);
         break;
     case K10S_EV_AS_REMOVE_NODE_RESP: {
         int32_t slot = c.V().node(e.a).as_slot;
@@ -1067,7 +1107,7 @@ K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
         }
-        emit(c, K10S_EV_N_REMOVE_NODE, pr->as_to_node_network_delay, slot, e.a, 0, 0.0);
+        emit(c, K10S_EV_N_REMOVE_NODE, pr->as_to_node_network_delay, slot, e.a, 0, 0.0, FQ_AS_TO_NODE);
         break;
     }
     case K10S_EV_AS_NODE_REMOVED: {
@@ -1089,18 +1129,18 @@ K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
         c.V().pool_ring()[tail] = (uint32_t)slot;
         h->pool_count += 1;
         bit_clear(c.V().pend_rm(), sc->node_uid[n]);
-        emit(c, K10S_EV_PS_NODE_REMOVED, pr->as_to_ps_network_delay, -1, n, 0, e.x);
+        emit(c, K10S_EV_PS_NODE_REMOVED, pr->as_to_ps_network_delay, -1, n, 0, e.x, FQ_AS_TO_PS);
         break;
     }
     case K10S_EV_AS_CA_REQ:
-        emit0(c, K10S_EV_PS_CA_REQ, pr->as_to_ps_network_delay);
+        emit(c, K10S_EV_PS_CA_REQ, pr->as_to_ps_network_delay, -1, 0, 0, 0.0, FQ_AS_TO_PS);
         break;
     case K10S_EV_AS_CA_RESP:
-        emit0(c, K10S_EV_CA_RESP, pr->as_to_ca_network_delay);
+        emit(c, K10S_EV_CA_RESP, pr->as_to_ca_network_delay, -1, 0, 0, 0.0, FQ_AS_TO_CA);
         break;
     case K10S_EV_AS_REMOVE_POD_REQ:
         bit_set(c.V().pend_rm(), sc->pod_uid[e.a]);  // quirk (api_server.rs:343): the NODE removal set
-        emit(c, K10S_EV_PS_REMOVE_POD_REQ, pr->as_to_ps_network_delay, -1, e.a, 0, 0.0);
+        emit(c, K10S_EV_PS_REMOVE_POD_REQ, pr->as_to_ps_network_delay, -1, e.a, 0, 0.0, FQ_AS_TO_PS);
         break;
     case K10S_EV_AS_REMOVE_POD_RESP: {
         if (f2u(e.x) != 0) {
@@ -1109,7 +1149,7 @@ K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
                 fail(c, K10S_PANIC_MISSING_NODE);
                 return;
             }
-            emit(c, K10S_EV_N_REMOVE_POD, pr->as_to_node_network_delay, slot, e.a, e.b, 0.0);
+            emit(c, K10S_EV_N_REMOVE_POD, pr->as_to_node_network_delay, slot, e.a, e.b, 0.0, FQ_AS_TO_NODE);
         }
         break;
     }
@@ -1118,7 +1158,7 @@ K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
             h->counters[K10S_C_TERMINATED_PODS] += 1;
             h->counters[K10S_C_PODS_REMOVED] += 1;
         }
-        emit(c, K10S_EV_PS_POD_REMOVED, pr->as_to_ps_network_delay, -1, e.a, e.b, e.x);
+        emit(c, K10S_EV_PS_POD_REMOVED, pr->as_to_ps_network_delay, -1, e.a, e.b, e.x, FQ_AS_TO_PS);
         break;
     case K10S_EV_AS_CREATE_GROUP_REQ: {
         uint32_t g = e.a;
@@ -1139,8 +1179,8 @@ K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
             return;
         }
         for (uint32_t k = 0; k < init && !c.H().error_code; k++)
-            emit(c, K10S_EV_PS_CREATE_POD_REQ, pr->as_to_ps_network_delay, -1, sc->g_pod[g * sc->group_bound + k], 0, 0.0);
-        if (sc->hpa_enabled) emit(c, K10S_EV_HPA_REGISTER_GROUP, pr->as_to_hpa_network_delay, -1, g, 0, e.time);
+            emit(c, K10S_EV_PS_CREATE_POD_REQ, pr->as_to_ps_network_delay, -1, sc->g_pod[g * sc->group_bound + k], 0, 0.0, FQ_AS_TO_PS);
+        if (sc->hpa_enabled) emit(c, K10S_EV_HPA_REGISTER_GROUP, pr->as_to_hpa_network_delay, -1, g, 0, e.time, FQ_AS_TO_HPA);
         break;
     }
     default:
@@ -1177,7 +1217,7 @@ K10S_WARM void on_node(Ctx& c, HeapEv e) {
         c.V().pod(p).finish_seq = fseq;
         int32_t g = c.S().pod_group[p];
         if (g >= 0) c.V().grp()[g].running += 1;
-        emit(c, K10S_EV_AS_POD_STARTED, pr->as_to_node_network_delay, -1, p, 0, e.time);
+        emit(c, K10S_EV_AS_POD_STARTED, pr->as_to_node_network_delay, -1, p, 0, e.time, FQ_AS_TO_NODE);
         break;
     }
     case K10S_EV_N_POD_FINISHED: {
@@ -1187,7 +1227,7 @@ K10S_WARM void on_node(Ctx& c, HeapEv e) {
             return;
         }
         run_remove(c, p);
-        emit(c, K10S_EV_AS_POD_FINISHED, 0.0, -1, p, e.b, e.x);  // emit_now
+        emit(c, K10S_EV_AS_POD_FINISHED, 0.0, -1, p, e.b, e.x, FQ_NOW);  // emit_now
         break;
     }
     case K10S_EV_N_REMOVE_NODE: {
@@ -1206,7 +1246,7 @@ K10S_WARM void on_node(Ctx& c, HeapEv e) {
             run_remove(c, (uint32_t)p);
             p = nx;
         }
-        emit(c, K10S_EV_AS_NODE_REMOVED, pr->as_to_node_network_delay, -1, n, 0, e.time);
+        emit(c, K10S_EV_AS_NODE_REMOVED, pr->as_to_node_network_delay, -1, n, 0, e.time, FQ_AS_TO_NODE);
         c.V().slot(slot).removed = 1;
         c.V().slot(slot).rtime = e.time;
         break;
@@ -1219,11 +1259,11 @@ K10S_WARM void on_node(Ctx& c, HeapEv e) {
         }
         if (c.V().pod(p).run_slot == slot) {
             run_remove(c, p);
-            emit(c, K10S_EV_AS_POD_REMOVED, pr->as_to_node_network_delay, -1, p, 1, e.time);
+            emit(c, K10S_EV_AS_POD_REMOVED, pr->as_to_node_network_delay, -1, p, 1, e.time, FQ_AS_TO_NODE);
         } else if (c.V().pod(p).cancel_slot == slot && c.V().pod(p).cancel_gen == c.V().slot(slot).gen) {
-            emit(c, K10S_EV_AS_POD_REMOVED, pr->as_to_node_network_delay, -1, p, 1, c.V().slot(slot).rtime);
+            emit(c, K10S_EV_AS_POD_REMOVED, pr->as_to_node_network_delay, -1, p, 1, c.V().slot(slot).rtime, FQ_AS_TO_NODE);
         } else {
-            emit(c, K10S_EV_AS_POD_REMOVED, pr->as_to_node_network_delay, -1, p, 0, 0.0);
+            emit(c, K10S_EV_AS_POD_REMOVED, pr->as_to_node_network_delay, -1, p, 0, 0.0, FQ_AS_TO_NODE);
         }
         break;
     }
@@ -1239,16 +1279,16 @@ K10S_COLD void on_ca(Ctx& c, HeapEv e) {
     const Params* pr = &c.P();
     if (e.kind == K10S_EV_CA_TICK) {
         h->ca_last_cycle_time = e.time;
-        emit0(c, K10S_EV_AS_CA_REQ, pr->as_to_ca_network_delay);
+        emit(c, K10S_EV_AS_CA_REQ, pr->as_to_ca_network_delay, -1, 0, 0, 0.0, FQ_AS_TO_CA);
         return;
     }
     for (uint32_t i = 0; i < h->ca_n_act && !c.H().error_code; i++) {
         CAAct a = c.V().ca_act()[i];
         if (a.up) {
-            emit(c, K10S_EV_AS_CREATE_NODE_REQ, pr->as_to_ca_network_delay, -1, c.S().def_node[a.arg], a.arg, 0.0);
+            emit(c, K10S_EV_AS_CREATE_NODE_REQ, pr->as_to_ca_network_delay, -1, c.S().def_node[a.arg], a.arg, 0.0, FQ_AS_TO_CA);
             h->counters[K10S_C_TOTAL_SCALED_UP_NODES] += 1;
         } else {
-            emit(c, K10S_EV_AS_REMOVE_NODE_REQ, pr->as_to_ca_network_delay, -1, a.arg, 0, 0.0);
+            emit(c, K10S_EV_AS_REMOVE_NODE_REQ, pr->as_to_ca_network_delay, -1, a.arg, 0, 0.0, FQ_AS_TO_CA);
             h->counters[K10S_C_TOTAL_SCALED_DOWN_NODES] += 1;
         }
     }
@@ -1314,7 +1354,7 @@ K10S_COLD void on_hpa(Ctx& c, HeapEv e) {
                 bit_set(bits, sc->g_pos[g * B + k]);
                 gs.created_count += 1;
                 gs.total_created += 1;
-                emit(c, K10S_EV_AS_CREATE_POD_REQ, c.P().as_to_ca_network_delay, -1, sc->g_pod[g * B + k], 0, 0.0);
+                emit(c, K10S_EV_AS_CREATE_POD_REQ, c.P().as_to_ca_network_delay, -1, sc->g_pod[g * B + k], 0, 0.0, FQ_AS_TO_CA);
                 h->counters[K10S_C_TOTAL_SCALED_UP_PODS] += 1;
             }
         } else if (cur > desired) {
@@ -1329,7 +1369,7 @@ K10S_COLD void on_hpa(Ctx& c, HeapEv e) {
                 bit_clear(bits, j);
                 gs.created_count -= 1;
                 uint32_t k = sc->g_sorted_k[g * B + j];
-                emit(c, K10S_EV_AS_REMOVE_POD_REQ, c.P().as_to_ca_network_delay, -1, sc->g_pod[g * B + k], 0, 0.0);
+                emit(c, K10S_EV_AS_REMOVE_POD_REQ, c.P().as_to_ca_network_delay, -1, sc->g_pod[g * B + k], 0, 0.0, FQ_AS_TO_CA);
                 h->counters[K10S_C_TOTAL_SCALED_DOWN_PODS] += 1;
             }
         }
@@ -1499,6 +1539,100 @@ K10S_HD void init_replica(Ctx& c) {
     h->status = K10S_REPLICA_RUNNING;
 }
 
+// ---- event-queue merge -------------------------------------------------------------------------
+enum : int { SRC_TRACE = K10S_NFQ, SRC_HEAP = K10S_NFQ + 1 };
+
+// Which source holds the minimum (time, id): a FIFO class 0..K10S_NFQ-1, SRC_TRACE, SRC_HEAP, or
+// -1 when all are empty.  Device: lanes 0..7 hold the FIFO heads, lane 8 the heap root, lane 9 the
+// trace head; a 4-step xor-shuffle min over the 16-lane group, broadcast from lane 0.
+K10S_HD int next_source(Ctx& c, uint32_t ntr) {
+    const RepHdr& H = c.H();
+    const uint32_t cur = H.trace_cursor;
+    const bool ht = cur < ntr;
+    int64_t tkey = 0x7FFFFFFFFFFFFFFFll;
+    uint32_t tseq = 0xFFFFFFFFu;
+    if (ht) {
+        tkey = total_key(c.S().trace[cur].time);
+        tseq = c.S().trace[cur].seq;
+    }
+#if K10S_DEVICE
+    const int lane = lane_id() & 15;
+    int64_t k = 0x7FFFFFFFFFFFFFFFll;
+    uint32_t sq = 0xFFFFFFFFu;
+    int src = -1;
+    if (lane < K10S_NFQ) {
+        if (H.fq_head[lane] != H.fq_tail[lane]) {
+            k = total_key(H.fq_top[lane].time);
+            sq = H.fq_top[lane].seq;
+            src = lane;
+        }
+    } else if (lane == SRC_HEAP) {
+        if (H.heap_size > 0) {
+            k = total_key(H.heap_top.time);
+            sq = H.heap_top.seq;
+            src = SRC_HEAP;
+        }
+    } else if (lane == SRC_TRACE) {
+        if (ht) {
+            k = tkey;
+            sq = tseq;
+            src = SRC_TRACE;
+        }
+    }
+#pragma unroll
+    for (int m = 8; m >= 1; m >>= 1) {
+        int64_t ok = (int64_t)shfl_xor_u64((uint64_t)k, m);
+        uint32_t os = (uint32_t)__shfl_xor((int)sq, m, 64);
+        int osrc = __shfl_xor(src, m, 64);
+        if (ok < k || (ok == k && os < sq)) {
+            k = ok;
+            sq = os;
+            src = osrc;
+        }
+    }
+    return (int)__builtin_amdgcn_readfirstlane(src);
+#else
+    int64_t k = tkey;
+    uint32_t sq = tseq;
+    int src = ht ? SRC_TRACE : -1;
+    if (H.heap_size > 0) {
+        int64_t hk = total_key(H.heap_top.time);
+        if (src < 0 || hk < k || (hk == k && H.heap_top.seq < sq)) {
+            k = hk;
+            sq = H.heap_top.seq;
+            src = SRC_HEAP;
+        }
+    }
+    for (int q = 0; q < K10S_NFQ; q++) {
+        if (H.fq_head[q] == H.fq_tail[q]) continue;
+        int64_t qk = total_key(H.fq_top[q].time);
+        if (src < 0 || qk < k || (qk == k && H.fq_top[q].seq < sq)) {
+            k = qk;
+            sq = H.fq_top[q].seq;
+            src = q;
+        }
+    }
+    return src;
+#endif
+}
+
+// Remove the event next_source selected; a FIFO refills its cached head from its ring.
+K10S_HD void consume_source(Ctx& c, int src) {
+    RepHdr& H = c.H();
+    if (src == SRC_TRACE) {
+        H.trace_cursor += 1;
+    } else if (src == SRC_HEAP) {
+        heap_pop(c);
+    } else {
+        const uint32_t hd = H.fq_head[src] + 1;
+        H.fq_head[src] = hd;
+        if (hd != H.fq_tail[src]) {
+            const uint32_t cap = c.Ly().cap_fq;
+            H.fq_top[src] = c.V().fq()[(uint32_t)src * cap + (hd & (cap - 1))];
+        }
+    }
+}
+
 // ---- the event loop -----------------------------------------------------------------------------
 // Returns 1 if the replica still has work (event budget exhausted), else 0.  The working header
 // c.H() is LDS on the device (staged by the kernel) and the replica's header in place on the host.
@@ -1520,44 +1654,38 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
             status = K10S_REPLICA_FINISHED;
             break;
         }
-        // next non-canceled event: merge the shared trace stream with the dynamic heap
+        // next non-canceled event: the minimum (time, id) over the shared trace stream, the heap
+        // root and the heads of the delay-class FIFOs (all cached: LDS / scalar cache)
         HeapEv e;
-        bool from_trace = false;
+        int src = 0;
         bool have = false;
         for (;;) {
-            const uint32_t cur = h->trace_cursor;
-            bool ht = cur < ntr;
-            bool hh = h->heap_size > 0;
-            if (!ht && !hh) break;
-            if (hh) {
-                e = c.V().heap()[0];
-                uniform_event(e);
-            }
-            if (ht) {
-                const double tt = sc->trace[cur].time;
-                const uint32_t ts = sc->trace[cur].seq;
-                if (!hh || ev_before(tt, ts, e.time, e.seq)) {
-                    const uint32_t tk = sc->trace[cur].kind, ta = sc->trace[cur].arg;
-                    e.time = tt;
-                    e.seq = ts;
-                    e.kind = (uint16_t)tk;
-                    e.slot = -1;
-                    e.x = 0.0;
-                    e.a = ta;
-                    e.b = 0;
-                    if (tk == K10S_EV_AS_CREATE_NODE_REQ) {
-                        e.a = sc->def_node[ta];
-                        e.b = ta;
-                    }
-                    from_trace = true;
-                    have = true;
-                    break;
+            src = next_source(c, ntr);
+            if (src < 0) break;
+            if (src == SRC_TRACE) {
+                const uint32_t cur = h->trace_cursor;
+                const uint32_t tk = sc->trace[cur].kind, ta = sc->trace[cur].arg;
+                e.time = sc->trace[cur].time;
+                e.seq = sc->trace[cur].seq;
+                e.kind = (uint16_t)tk;
+                e.slot = -1;
+                e.x = 0.0;
+                e.a = ta;
+                e.b = 0;
+                if (tk == K10S_EV_AS_CREATE_NODE_REQ) {
+                    e.a = sc->def_node[ta];
+                    e.b = ta;
                 }
+            } else if (src == SRC_HEAP) {
+                e = h->heap_top;
+                if (e.kind == K10S_EV_N_POD_FINISHED && c.V().pod(e.a).finish_seq != e.seq) {  // canceled
+                    heap_pop(c);
+                    continue;
+                }
+            } else {
+                e = h->fq_top[src];
             }
-            if (e.kind == K10S_EV_N_POD_FINISHED && c.V().pod(e.a).finish_seq != e.seq) {  // canceled
-                heap_pop(c);
-                continue;
-            }
+            uniform_event(e);
             have = true;
             break;
         }
@@ -1578,8 +1706,7 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
             more = 1;
             break;
         }
-        if (from_trace) h->trace_cursor += 1;
-        else heap_pop(c);
+        consume_source(c, src);
         h->clock = e.time;
         h->cur_kind = e.kind;
         h->cur_seq = e.seq;

@@ -123,6 +123,20 @@ K10S_HELPER void est_add(Estimator& e, double x) {
     e.sum2 += delta_n * delta_n * nf * (nf - 1.0);
 }
 
+struct HeapEv {             // dslab Event {id, time, dst, data}, 32 B
+    double time;
+    uint32_t seq;
+    uint16_t kind;
+    int16_t slot;           // node component for N_* kinds
+    uint32_t a;             // pod idx / node idx / group idx
+    uint32_t b;             // node idx / def id / alloc cpu / flags
+    double x;               // event time field (assign/finish/removal/add/start) or alloc ram bits
+};
+
+// Delay-class FIFOs of the event queue (k10s_engine.h): events emitted with the same constant
+// delay are emitted in (time, id) order, so each class is an already-sorted run.
+#define K10S_NFQ 8
+
 struct RepHdr {
     double clock;
     uint32_t next_seq;
@@ -150,16 +164,12 @@ struct RepHdr {
     uint32_t unsched_cache_count;
     uint32_t cur_kind, cur_seq;   // event being handled (panic attribution)
     uint32_t pad;
-};
-
-struct HeapEv {             // dslab Event {id, time, dst, data}, 32 B
-    double time;
-    uint32_t seq;
-    uint16_t kind;
-    int16_t slot;           // node component for N_* kinds
-    uint32_t a;             // pod idx / node idx / group idx
-    uint32_t b;             // node idx / def id / alloc cpu / flags
-    double x;               // event time field (assign/finish/removal/add/start) or alloc ram bits
+    // event queue: delay-class FIFO rings (head/tail counters, newest time, cached head entries)
+    // and the cached root of the heap (valid while heap_size > 0)
+    uint32_t fq_head[K10S_NFQ], fq_tail[K10S_NFQ];
+    double fq_last[K10S_NFQ];
+    HeapEv fq_top[K10S_NFQ];
+    HeapEv heap_top;
 };
 
 struct QInfo {              // QueuedPodInfo (queue.rs:13-27), 24 B
@@ -242,7 +252,9 @@ struct Layout {
     uint64_t node, pend_rm, pod, prec, slot, pool_ring;
     uint64_t grp, grp_bits;
     uint64_t cag, ca_act, ca_cpu, ca_ram, ca_undo;
-    uint64_t heap, aq, uq, log, place;
+    uint64_t heap, aq, uq, log, place, fq;
+    uint32_t cap_fq;      // entries per delay-class ring (power of two; 0 = no rings)
+    uint32_t pad0;
     uint32_t cap_heap, cap_aq, cap_uq, cap_act, cap_log, cap_place, cap_undo, rec_on;
     uint32_t words_nodes, words_uids, words_group;
     uint32_t pad;

@@ -60,7 +60,8 @@ class Capacities(ctypes.Structure):
     _fields_ = [("event_heap", ctypes.c_uint32), ("active_queue", ctypes.c_uint32),
                 ("unschedulable", ctypes.c_uint32), ("group_name_bound", ctypes.c_uint32),
                 ("ca_name_bound", ctypes.c_uint32), ("event_log", ctypes.c_uint32),
-                ("placement_log", ctypes.c_uint32), ("pod_records", ctypes.c_uint32)]
+                ("placement_log", ctypes.c_uint32), ("pod_records", ctypes.c_uint32),
+                ("delay_fifo", ctypes.c_uint32)]
 
 
 class LogEntry(ctypes.Structure):

@@ -83,6 +83,30 @@ def test_fuzz_gpu(seed):
     _fuzz("gpu", seed)
 
 
+# Delay-class FIFO rings are an optimisation of the event queue: tiny rings (constant spill to the
+# heap), one-entry rings and no rings at all must deliver the identical event sequence.
+FIFO_CASES = [(seed, fifo) for seed in (1, 4, 6, 10, 13, 22) for fifo in (1, 2, 0xFFFFFFFF)]
+
+
+@pytest.mark.parametrize("seed,fifo", FIFO_CASES)
+def test_fifo_capacity_host(seed, fifo):
+    kw = dict(ca=(seed % 3 == 1), hpa=(seed % 4 == 2))
+    mode = RUN_UNTIL_TIME if kw["hpa"] else RUN_UNTIL_ALL_FINISHED
+    od, eng = parity.run_pair(engine_cls("host"), gen.random_scenario(seed, **kw), mode=mode, until=3000.0,
+                              max_time=20000.0, fifo=fifo)
+    assert parity.compare(od, eng) == [], (seed, fifo)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,fifo", FIFO_CASES)
+def test_fifo_capacity_gpu(seed, fifo):
+    kw = dict(ca=(seed % 3 == 1), hpa=(seed % 4 == 2))
+    mode = RUN_UNTIL_TIME if kw["hpa"] else RUN_UNTIL_ALL_FINISHED
+    od, eng = parity.run_pair(engine_cls("gpu"), gen.random_scenario(seed, **kw), mode=mode, until=3000.0,
+                              max_time=20000.0, fifo=fifo)
+    assert parity.compare(od, eng) == [], (seed, fifo)
+
+
 @pytest.mark.parametrize("backend", BACKENDS)
 def test_budgeted_launches_equal_one_launch(backend):
     """Pausing every few events (multi-launch runs) must not change anything."""
