@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-workers", type=int, default=0, help="0 = min(16, cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pruned-scan", action="store_true", help="exact block-bound pruned scan (DESIGN.md §3)")
+    ap.add_argument("--profile", action="store_true", help="print the K10S_PROF cycle attribution (variant builds)")
     return ap.parse_args()
 
 
@@ -105,7 +107,7 @@ def main():
     from kubernetriks_amd.build import build
     build()
     from kubernetriks_amd import workloads as wl
-    from kubernetriks_amd.native import Engine
+    from kubernetriks_amd.native import NUM_COUNTERS, Capacities, Engine, version
     from kubernetriks_amd.scenario import SimulationConfig, scenario_text
 
     cfg = SimulationConfig()
@@ -117,7 +119,9 @@ def main():
     probe.close()
     params = wl.replica_params(defaults, R, base_seed=123, perturb=True, replica_offset=rank * R)
     t = time.perf_counter()
-    eng = Engine(scn, R, params=params, device=local_rank)
+    caps = Capacities()
+    caps.pruned_scan = 1 if args.pruned_scan else 0
+    eng = Engine(scn, R, params=params, caps=caps, device=local_rank)
     log(f"[rank {rank}] engine: {R} replicas x {eng.replica_bytes / 2**20:.1f} MiB, init {time.perf_counter() - t:.2f}s")
 
     def one_step():
@@ -130,7 +134,7 @@ def main():
         log(f"[rank {rank}] warmup {i}: {time.perf_counter() - t:.2f}s")
 
     import numpy as np
-    counters = np.zeros(16, dtype=np.float64)
+    counters = np.zeros(NUM_COUNTERS, dtype=np.float64)
     kernel_ms = []
     if world > 1:
         dist.barrier()
@@ -141,7 +145,7 @@ def main():
         kernel_ms.append(ms)
         res = eng.raw_results()
         for r in res:
-            for k in range(16):
+            for k in range(NUM_COUNTERS):
                 counters[k] += r.counters[k]
         log(f"[rank {rank}] step {i}: run {ms:.1f} ms")
     torch.cuda.synchronize()
@@ -165,18 +169,22 @@ def main():
         dist.all_reduce(cvec, op=dist.ReduceOp.SUM)  # RCCL over xGMI: metric counters only
     elapsed, mean_kernel_ms = float(tvec[0]), float(tvec[1])
     c = cvec.cpu().numpy()
-    placements, attempts, events, scanned = c[12], c[13], c[14], c[15]
+    placements, attempts, events, scanned, nread = c[12], c[13], c[14], c[15], c[16]
     value = placements / elapsed
 
     # roofline for the dominant kernel (per launch, this rank's launch time, all-rank bytes / world)
     per_launch_bytes = (12.0 * scanned + 12.0 * attempts + 12.0 * placements) / (args.steps * world)
     achieved = per_launch_bytes / (mean_kernel_ms * 1e-3)
+    # what the scans actually read (pruned scan: block bounds + scanned blocks + bound upkeep)
+    touched_bytes = (12.0 * nread + 12.0 * attempts + 12.0 * placements) / (args.steps * world)
     traffic = None
     pmc_path = os.path.join(REPO, "profiles", "pmc_run_kernel.json")
     if os.path.exists(pmc_path):
         try:
             pm = json.load(open(pmc_path))
-            if pm.get("config") == [R, args.nodes, args.pods]:
+            # only a PMC pass over this exact kernel build, config and scan mode counts
+            if pm.get("config") == [R, args.nodes, args.pods] and pm.get("engine") == version() and \
+                    pm.get("scan_mode") == ("pruned" if args.pruned_scan else "full"):
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -201,8 +209,13 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK, "traffic": traffic,
                      "kernel": "k10s_run_kernel", "kernel_ms_per_launch": mean_kernel_ms,
-                     "algorithmic_bytes_per_launch": per_launch_bytes},
+                     "algorithmic_bytes_per_launch": per_launch_bytes,
+                     "scan_mode": "pruned" if args.pruned_scan else "full",
+                     "touched_bytes_per_launch": touched_bytes,
+                     "touched_GBps": touched_bytes / (mean_kernel_ms * 1e-3) / 1e9},
+        "engine": version(),
         "totals": {"placements": placements, "attempts": attempts, "events": events, "nodes_scanned": scanned,
+                   "nodes_read": nread,
                    "replica_status": {str(k): v for k, v in statuses.items()}, "replica_errors": errors},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -211,6 +224,13 @@ def main():
         except Exception as ex:  # the GPU number stands on its own
             log("cpu baseline failed:", ex)
             out["cpu_baseline"] = None
+    if args.profile:
+        prof = eng.profile()
+        tot = {k: float(sum(p[k] for p in prof)) for k in prof[0]}
+        loop = tot["loop"] or 1.0
+        out["profile"] = {"cycles_total": tot, "share_of_loop": {k: v / loop for k, v in tot.items() if k != "scans"},
+                          "cycles_per_event": loop / max(events / args.steps / world, 1.0),
+                          "scan_cycles_per_scan": tot["scan"] / max(tot["scans"], 1.0)}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -96,6 +96,8 @@ enum k10s_counter {
     K10S_C_ATTEMPTS,         /* schedule_one calls reaching the filter (kube_scheduler.rs:89) */
     K10S_C_EVENTS,           /* delivered (non-canceled) events */
     K10S_C_NODES_SCANNED,    /* Σ |scheduler cache| over attempts: algorithmic scan volume */
+    K10S_C_NODES_READ,       /* scheduler-cache entries actually read (block bounds, scanned blocks,
+                                bound maintenance): the pruned scan's real volume, engine-only */
     K10S_NUM_COUNTERS
 };
 
@@ -147,6 +149,9 @@ typedef struct k10s_capacities {
     uint32_t pod_records;                /* 1 = keep per-pod start/finish/removal times */
     uint32_t delay_fifo;                 /* entries per delay-class event ring: 0 = default (512),
                                             K10S_FIFO_OFF = every event in the heap */
+    uint32_t pruned_scan;                /* 0 = every attempt scans every node (default);
+                                            1 = exact block-bound pruned scan where it applies
+                                             */
 } k10s_capacities;
 #define K10S_FIFO_OFF 0xFFFFFFFFu
 
@@ -252,6 +257,11 @@ const char* k10s_engine_group_name(const k10s_engine* e, uint32_t idx);
 /* Per-replica device-state footprint in bytes and device pointer of replica r's scheduler
    cache SoA (for profiling tools). */
 uint64_t k10s_engine_replica_bytes(const k10s_engine* e);
+
+/* Tooling: per-replica cycle attribution of the event loop, 8 words per replica
+   (loop, select, consume, dispatch, scheduling cycle, scan, scans, bound maintenance; s_memtime
+   cycles).  All zero unless the library was built with -DK10S_PROF=1 (variant builds only). */
+int32_t k10s_engine_profile(const k10s_engine* e, uint64_t* out /* [n_replicas * 8] */);
 
 const char* k10s_last_error(void);
 const char* k10s_version(void);

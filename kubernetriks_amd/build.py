@@ -5,6 +5,7 @@ check and produces the .so that travels to the GPU box.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
@@ -36,6 +37,17 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def build_id(extra=()) -> str:
+    """Content hash of everything that goes into the kernels (sources, headers, flags): ties
+    profiles/ measurements (PMC traffic) to the exact kernel they were taken on."""
+    h = hashlib.sha1()
+    for f in [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + \
+            [os.path.join(REPO, "include", f) for f in ("k10s.h", "k10s_events.h")]:
+        h.update(open(f, "rb").read())
+    h.update(" ".join(FLAGS + list(extra)).encode())
+    return h.hexdigest()[:12]
+
+
 def build(force: bool = False, verbose: bool = False, extra=(), out: str = None) -> str:
     """Compile the engine.  `extra` adds compiler flags (e.g. tuning -D knobs) and `out` an
     alternative output path (variant builds for A/B measurements; load them via K10S_LIB)."""
@@ -44,6 +56,7 @@ def build(force: bool = False, verbose: bool = False, extra=(), out: str = None)
         return OUT
     os.makedirs(os.path.dirname(target), exist_ok=True)
     tag = os.path.basename(target).replace(".so", "")
+    extra = list(extra) + [f'-DK10S_BUILD_ID="{build_id(extra)}"']
     objs = []
     procs = []
     for src in SOURCES:

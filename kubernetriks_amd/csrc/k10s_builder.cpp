@@ -672,6 +672,12 @@ Layout make_layout(const HostScenario& hs, const k10s_capacities& caps) {
     L.s_cpu = take(4 * N);
     L.s_ram = take(8 * N);
     L.s_present = take(8 * (uint64_t)L.words_nodes);
+    L.pruned = caps.pruned_scan ? 1u : 0u;
+    L.bshift = 6;
+    while (((N + (1ull << L.bshift) - 1) >> L.bshift) > 64) L.bshift++;
+    L.nblocks = (uint32_t)((N + (1ull << L.bshift) - 1) >> L.bshift);
+    L.s_bcpu = take(4 * (uint64_t)L.nblocks);
+    L.s_bram = take(8 * (uint64_t)L.nblocks);
     L.node = take(sizeof(NodeState) * N);
     L.pend_rm = take(8 * (uint64_t)L.words_uids);
     L.pod = take(sizeof(PodState) * P);

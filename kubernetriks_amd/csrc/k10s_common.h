@@ -120,45 +120,133 @@ K10S_HD int lane_id() {
 }
 
 #if K10S_DEVICE
-K10S_D uint64_t shfl_xor_u64(uint64_t v, int m) {
-    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-    lo = (uint32_t)__shfl_xor((int)lo, m, 64);
-    hi = (uint32_t)__shfl_xor((int)hi, m, 64);
-    return ((uint64_t)hi << 32) | lo;
+// Cross-lane exchange without LDS: DPP and gfx950 permlane swaps (VALU only; __shfl_xor would be
+// ds_bpermute through the LDS crossbar, ~100 cycles per step).  Step S pairs each lane with one
+// partner; xpair<S>(v, a, b) returns the two values of the pair (own and partner, in some order),
+// so combining a and b with a commutative, associative operation and repeating for S = 0..k-1
+// leaves every lane of each 2^(k+1)-lane group with the group's reduction:
+//   S=0 quad xor 1, S=1 quad xor 2, S=2 half-row mirror (8 lanes), S=3 row mirror (16 lanes),
+//   S=4 permlane16 swap (32 lanes), S=5 permlane32 swap (64 lanes).
+template <int S>
+K10S_D void xpair(uint32_t v, uint32_t& a, uint32_t& b) {
+    if constexpr (S < 4) {
+        constexpr int ctrl = S == 0 ? 0xB1 : S == 1 ? 0x4E : S == 2 ? 0x141 : 0x140;
+        a = v;
+        b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, ctrl, 0xF, 0xF, false);
+    } else if constexpr (S == 4) {
+        auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        a = r[0];
+        b = r[1];
+    } else {
+        auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        a = r[0];
+        b = r[1];
+    }
+}
+K10S_D uint64_t join64(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+
+// one reduction step of a lexicographic (key, idx) max
+template <int S>
+K10S_D void argmax_step(uint64_t& key, int32_t& idx) {
+    uint32_t la, lb, ha, hb, ia, ib;
+    xpair<S>((uint32_t)key, la, lb);
+    xpair<S>((uint32_t)(key >> 32), ha, hb);
+    xpair<S>((uint32_t)idx, ia, ib);
+    const uint64_t ka = join64(la, ha), kb = join64(lb, hb);
+    const bool tb = kb > ka || (kb == ka && (int32_t)ib > (int32_t)ia);
+    key = tb ? kb : ka;
+    idx = (int32_t)(tb ? ib : ia);
+}
+// one reduction step of a lexicographic (key signed 64, seq, payload) min
+template <int S>
+K10S_D void keymin_step(int64_t& key, uint32_t& seq, uint32_t& pay) {
+    uint32_t la, lb, ha, hb, sa, sb, pa, pb;
+    xpair<S>((uint32_t)(uint64_t)key, la, lb);
+    xpair<S>((uint32_t)((uint64_t)key >> 32), ha, hb);
+    xpair<S>(seq, sa, sb);
+    xpair<S>(pay, pa, pb);
+    const int64_t ka = (int64_t)join64(la, ha), kb = (int64_t)join64(lb, hb);
+    const bool tb = kb < ka || (kb == ka && sb < sa);
+    key = tb ? kb : ka;
+    seq = tb ? sb : sa;
+    pay = tb ? pb : pa;
 }
 #endif
 
 // Reduce (key, idx) to the lexicographic max over the wave; every lane gets the result.
 K10S_HD void wave_argmax(uint64_t& key, int32_t& idx) {
 #if K10S_DEVICE
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        uint64_t ok = shfl_xor_u64(key, m);
-        int32_t oi = __shfl_xor(idx, m, 64);
-        if (ok > key || (ok == key && oi > idx)) {
-            key = ok;
-            idx = oi;
-        }
-    }
+    argmax_step<0>(key, idx);
+    argmax_step<1>(key, idx);
+    argmax_step<2>(key, idx);
+    argmax_step<3>(key, idx);
+    argmax_step<4>(key, idx);
+    argmax_step<5>(key, idx);
 #else
     (void)key;
     (void)idx;
 #endif
 }
+#if K10S_DEVICE
+template <int S>
+K10S_D uint32_t max_step(uint32_t v) {
+    uint32_t a, b;
+    xpair<S>(v, a, b);
+    return a > b ? a : b;
+}
+template <int S>
+K10S_D int32_t min_step_i32(int32_t v) {
+    uint32_t a, b;
+    xpair<S>((uint32_t)v, a, b);
+    return (int32_t)a < (int32_t)b ? (int32_t)a : (int32_t)b;
+}
+template <int S>
+K10S_D uint32_t sum_step(uint32_t v) {
+    uint32_t a, b;
+    xpair<S>(v, a, b);
+    return a + b;
+}
+template <int S>
+K10S_D uint64_t max_step64(uint64_t v) {
+    uint32_t la, lb, ha, hb;
+    xpair<S>((uint32_t)v, la, lb);
+    xpair<S>((uint32_t)(v >> 32), ha, hb);
+    const uint64_t a = join64(la, ha), b = join64(lb, hb);
+    return a > b ? a : b;
+}
+#endif
+K10S_HD uint32_t wave_max_u32(uint32_t v) {
+#if K10S_DEVICE
+    v = max_step<0>(v); v = max_step<1>(v); v = max_step<2>(v);
+    v = max_step<3>(v); v = max_step<4>(v); v = max_step<5>(v);
+#endif
+    return v;
+}
+K10S_HD uint64_t wave_max_u64(uint64_t v) {
+#if K10S_DEVICE
+    v = max_step64<0>(v); v = max_step64<1>(v); v = max_step64<2>(v);
+    v = max_step64<3>(v); v = max_step64<4>(v); v = max_step64<5>(v);
+#endif
+    return v;
+}
+K10S_HD bool wave_any(bool b) {
+#if K10S_DEVICE
+    return __ballot(b) != 0;
+#else
+    return b;
+#endif
+}
 K10S_HD int32_t wave_min_i32(int32_t v) {
 #if K10S_DEVICE
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        int32_t o = __shfl_xor(v, m, 64);
-        v = o < v ? o : v;
-    }
+    v = min_step_i32<0>(v); v = min_step_i32<1>(v); v = min_step_i32<2>(v);
+    v = min_step_i32<3>(v); v = min_step_i32<4>(v); v = min_step_i32<5>(v);
 #endif
     return v;
 }
 K10S_HD uint32_t wave_sum_u32(uint32_t v) {
 #if K10S_DEVICE
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v += (uint32_t)__shfl_xor((int)v, m, 64);
+    v = sum_step<0>(v); v = sum_step<1>(v); v = sum_step<2>(v);
+    v = sum_step<3>(v); v = sum_step<4>(v); v = sum_step<5>(v);
 #endif
     return v;
 }

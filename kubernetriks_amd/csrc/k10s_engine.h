@@ -48,6 +48,8 @@ struct Rep {
     K10S_HD uint32_t* s_cpu() const { return at<uint32_t>(L().s_cpu); }
     K10S_HD uint64_t* s_ram() const { return at<uint64_t>(L().s_ram); }
     K10S_HD uint64_t* s_present() const { return at<uint64_t>(L().s_present); }
+    K10S_HD uint32_t* s_bcpu() const { return at<uint32_t>(L().s_bcpu); }
+    K10S_HD uint64_t* s_bram() const { return at<uint64_t>(L().s_bram); }
     K10S_HD NodeState& node(uint32_t n) const { return at<NodeState>(L().node)[n]; }
     K10S_HD uint64_t* pend_rm() const { return at<uint64_t>(L().pend_rm); }
     K10S_HD PodState& pod(uint32_t p) const { return at<PodState>(L().pod)[p]; }
@@ -133,6 +135,25 @@ K10S_HD void uniform_event(HeapEv& e) {
     (void)e;
 #endif
 }
+
+// ---- cycle attribution (K10S_PROF builds: tooling only, semantics-neutral) ----------------------
+// s_memtime deltas per loop phase, accumulated in RepHdr::prof and read by k10s_engine_profile.
+#ifndef K10S_PROF
+#define K10S_PROF 0
+#endif
+enum : int { PROF_LOOP = 0, PROF_SELECT = 1, PROF_CONSUME = 2, PROF_DISPATCH = 3, PROF_CYCLE = 4, PROF_SCAN = 5,
+             PROF_NSCAN = 6, PROF_BOUNDS = 7 };
+K10S_HD uint64_t prof_now() {
+#if K10S_PROF && K10S_DEVICE
+    return (uint64_t)__builtin_readcyclecounter();
+#else
+    return 0;
+#endif
+}
+#define K10S_PROF_ADD(c, slot, t0)                                        \
+    do {                                                                  \
+        if (K10S_PROF) (c).H().prof[(slot)] += prof_now() - (t0);         \
+    } while (0)
 
 // ---- small helpers ---------------------------------------------------------------------------
 K10S_HD bool bit_test(const uint64_t* w, uint32_t i) { return (w[i >> 6] >> (i & 63)) & 1ull; }
@@ -234,7 +255,8 @@ K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uin
 }
 K10S_HD uint32_t emit0(Ctx& c, uint32_t kind, double delay) { return emit(c, kind, delay, -1, 0, 0, 0.0); }
 
-// Smallest (time, id) among children [first, min(first + D, n)); returns its index.
+// Smallest (time, id) among children [first, min(first + D, n)); returns its index.  Device: lanes
+// 0..7 load one child each (one 256-B read) and reduce with 3 DPP steps.
 K10S_HD uint32_t heap_min_child(const HeapEv* hp, uint32_t first, uint32_t n, int64_t& kmin, uint32_t& smin) {
 #if K10S_DEVICE
     const int lane = lane_id();
@@ -245,17 +267,10 @@ K10S_HD uint32_t heap_min_child(const HeapEv* hp, uint32_t first, uint32_t n, in
         k = total_key(hp[i].time);
         sq = hp[i].seq;
     }
-#pragma unroll
-    for (int m = K10S_HEAP_D / 2; m >= 1; m >>= 1) {
-        int64_t ok = (int64_t)shfl_xor_u64((uint64_t)k, m);
-        uint32_t os = (uint32_t)__shfl_xor((int)sq, m, 64);
-        uint32_t oi = (uint32_t)__shfl_xor((int)i, m, 64);
-        if (ok < k || (ok == k && os < sq)) {
-            k = ok;
-            sq = os;
-            i = oi;
-        }
-    }
+    static_assert(K10S_HEAP_D == 8, "the DPP reduction below covers 8-lane groups");
+    keymin_step<0>(k, sq, i);
+    keymin_step<1>(k, sq, i);
+    keymin_step<2>(k, sq, i);
     // lanes 0..D-1 now agree; broadcast lane 0's result to the whole wave
     const uint64_t klo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)k);
     const uint64_t khi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)k >> 32));
@@ -470,8 +485,14 @@ K10S_HD double la_score(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr) {
 // Returns K10S_SCHED_* and writes the chosen node index.  Wave-parallel over node indices (name
 // order): each lane owns 4 consecutive nodes per 256-node step (one 16-B cpu load + two 16-B ram
 // loads), keeps "score >= best" (the last maximum) over its nodes in ascending order, and the
-// cross-lane (key, n) max reproduces the reference's left-to-right argmax.
-// Requires s_cpu / s_ram 16-B aligned (node arrays start on 256-B boundaries).
+// cross-lane (key, n) max reproduces the reference's left-to-right argmax.  The loads run
+// K10S_SCAN_PIPE steps ahead of the arithmetic (software pipeline), so a wave keeps several
+// 3 KiB steps in flight instead of waiting one memory round trip per step.
+// Requires s_cpu / s_ram 16-B aligned and readable up to the next multiple of 4 nodes (engine
+// sections are 256-B padded; the unit surface's rows are node_stride (multiple of 64) long).
+#ifndef K10S_SCAN_PIPE
+#define K10S_SCAN_PIPE 2
+#endif
 K10S_HD void scan_node(uint32_t n, uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr, double weight, int32_t& first,
                        uint64_t& best_key, int32_t& best_n) {
     if (rc <= ac && rr <= ar) {
@@ -487,32 +508,54 @@ K10S_HD void scan_node(uint32_t n, uint32_t ac, uint64_t ar, uint32_t rc, uint64
     }
 }
 
+#if K10S_DEVICE
+struct ScanGrp {            // one lane's 4 consecutive nodes of a 256-node step
+    uint32_t bits;          // present & < n_nodes
+    uint4 cv;
+    ulonglong2 r01, r23;
+};
+K10S_D ScanGrp scan_load(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
+                         uint32_t n0) {
+    ScanGrp g;
+    g.bits = 0;
+    g.cv = make_uint4(0, 0, 0, 0);
+    g.r01 = make_ulonglong2(0, 0);
+    g.r23 = make_ulonglong2(0, 0);
+    if (n0 < n_nodes) {
+        const uint32_t valid = n_nodes - n0;
+        g.bits = (uint32_t)(present[n0 >> 6] >> (n0 & 63)) & (valid >= 4 ? 0xFu : ((1u << valid) - 1u));
+        g.cv = *reinterpret_cast<const uint4*>(s_cpu + n0);
+        g.r01 = *reinterpret_cast<const ulonglong2*>(s_ram + n0);
+        g.r23 = *reinterpret_cast<const ulonglong2*>(s_ram + n0 + 2);
+    }
+    return g;
+}
+K10S_D void scan_grp(const ScanGrp& g, uint32_t n0, uint32_t rc, uint64_t rr, double weight, int32_t& first,
+                     uint64_t& best_key, int32_t& best_n) {
+    if (g.bits) {
+        if (g.bits & 1u) scan_node(n0, g.cv.x, g.r01.x, rc, rr, weight, first, best_key, best_n);
+        if (g.bits & 2u) scan_node(n0 + 1, g.cv.y, g.r01.y, rc, rr, weight, first, best_key, best_n);
+        if (g.bits & 4u) scan_node(n0 + 2, g.cv.z, g.r23.x, rc, rr, weight, first, best_key, best_n);
+        if (g.bits & 8u) scan_node(n0 + 3, g.cv.w, g.r23.y, rc, rr, weight, first, best_key, best_n);
+    }
+}
+#endif
+
 K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
                           uint32_t rc, uint64_t rr, double weight, int32_t* chosen) {
     uint64_t best_key = 0;
     int32_t best_n = -1;
     int32_t first = 0x7fffffff;
 #if K10S_DEVICE
-    const uint32_t lane = (uint32_t)lane_id();
+    const uint32_t l4 = 4u * (uint32_t)lane_id();
+    ScanGrp g[K10S_SCAN_PIPE + 1];
+#pragma unroll
+    for (int i = 0; i < K10S_SCAN_PIPE; i++) g[i] = scan_load(s_cpu, s_ram, present, n_nodes, 256u * i + l4);
     for (uint32_t base = 0; base < n_nodes; base += 256) {
-        uint32_t n0 = base + 4 * lane;
-        if (n0 < n_nodes) {
-            uint32_t bits = (uint32_t)(present[n0 >> 6] >> (n0 & 63)) & 0xFu;
-            if (bits) {
-                if (n0 + 4 <= n_nodes) {
-                    uint4 cv = *reinterpret_cast<const uint4*>(s_cpu + n0);
-                    ulonglong2 r01 = *reinterpret_cast<const ulonglong2*>(s_ram + n0);
-                    ulonglong2 r23 = *reinterpret_cast<const ulonglong2*>(s_ram + n0 + 2);
-                    if (bits & 1u) scan_node(n0, cv.x, r01.x, rc, rr, weight, first, best_key, best_n);
-                    if (bits & 2u) scan_node(n0 + 1, cv.y, r01.y, rc, rr, weight, first, best_key, best_n);
-                    if (bits & 4u) scan_node(n0 + 2, cv.z, r23.x, rc, rr, weight, first, best_key, best_n);
-                    if (bits & 8u) scan_node(n0 + 3, cv.w, r23.y, rc, rr, weight, first, best_key, best_n);
-                } else {
-                    for (uint32_t j = 0; j < 4 && n0 + j < n_nodes; j++)
-                        if (bits & (1u << j)) scan_node(n0 + j, s_cpu[n0 + j], s_ram[n0 + j], rc, rr, weight, first, best_key, best_n);
-                }
-            }
-        }
+        g[K10S_SCAN_PIPE] = scan_load(s_cpu, s_ram, present, n_nodes, base + 256u * K10S_SCAN_PIPE + l4);
+        scan_grp(g[0], base + l4, rc, rr, weight, first, best_key, best_n);
+#pragma unroll
+        for (int i = 0; i < K10S_SCAN_PIPE; i++) g[i] = g[i + 1];
     }
 #else
     for (uint32_t n = 0; n < n_nodes; n++)
@@ -524,6 +567,143 @@ K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const ui
     // kube_scheduler.rs:140-148: start from filtered[0]; if its score is NaN nothing replaces it
     double s0 = 0.0 + la_score(s_cpu[first], s_ram[first], rc, rr) * weight;
     *chosen = is_nan(s0) ? first : best_n;
+    return K10S_SCHED_OK;
+}
+
+// ---- block bounds of the scheduler cache and the exact pruned scan ------------------------------
+// The node cache is cut into blocks of 2^bshift consecutive indices (64 <= block, <= 64 blocks);
+// s_bcpu[b] / s_bram[b] hold the largest allocatable cpu / ram over the block's present nodes (0 if
+// none), recomputed whenever a node of the block changes (reserve, release, add, remove).
+//
+// Why a bound is exact: with rc > 0, rr > 0 and every ram below 2^46, each LeastAllocated term is
+// a correctly rounded quotient of exactly represented integers (100·(a − r) < 2^53, a < 2^53) whose
+// real value 100·(1 − r/a) grows with a, and rounding is monotone, so the f64 score
+// ((c + r) / 2.0, weight 1.0) of any fitting node is <= the f64 score of (bcpu[b], bram[b]).  A
+// block whose bound is below the best exact score found so far — or equal to it with all its
+// indices below the best node (ties go to the last node in name order, kube_scheduler.rs:140-148)
+// — cannot contain the argmax; rc, rr > 0 also rules out the 0/0 NaN of filtered[0].
+K10S_HD void block_recompute(Ctx& c, uint32_t b) {
+    const uint32_t N = c.S().n_nodes, sh = c.Ly().bshift;
+    const uint32_t lo = b << sh;
+    const uint32_t hi = (lo + (1u << sh)) < N ? (lo + (1u << sh)) : N;
+    const uint32_t* cpu = c.V().s_cpu();
+    const uint64_t* ram = c.V().s_ram();
+    const uint64_t* pres = c.V().s_present();
+    uint32_t mc = 0;
+    uint64_t mr = 0;
+    for (uint32_t n = lo + (uint32_t)lane_id(); n < hi; n += K10S_LANES) {
+        if ((pres[n >> 6] >> (n & 63)) & 1ull) {
+            uint32_t x = cpu[n];
+            uint64_t y = ram[n];
+            mc = x > mc ? x : mc;
+            mr = y > mr ? y : mr;
+        }
+    }
+    mc = wave_max_u32(mc);
+    mr = wave_max_u64(mr);
+    c.V().s_bcpu()[b] = mc;
+    c.V().s_bram()[b] = mr;
+    c.H().counters[K10S_C_NODES_READ] += hi - lo;
+}
+K10S_HD void node_bound_changed(Ctx& c, uint32_t n) {
+    if (!c.Ly().pruned) return;
+    const uint64_t t0 = prof_now();
+    block_recompute(c, n >> c.Ly().bshift);
+    K10S_PROF_ADD(c, PROF_BOUNDS, t0);
+}
+
+// Returns K10S_SCHED_OK / NO_SUFFICIENT_RESOURCES, or -1 when the bound argument does not apply
+// (a block maximum of ram >= 2^46): the caller then runs the full scan.  Preconditions (caller):
+// weight == 1.0, rc > 0, rr > 0.  *nread = scheduler-cache entries read (bounds + scanned blocks).
+K10S_HD int schedule_scan_pruned(Ctx& c, uint32_t rc, uint64_t rr, int32_t* chosen, uint32_t* nread) {
+    const uint32_t N = c.S().n_nodes, NB = c.Ly().nblocks, sh = c.Ly().bshift;
+    const uint32_t* bc = c.V().s_bcpu();
+    const uint64_t* br = c.V().s_bram();
+    const uint32_t* cpu = c.V().s_cpu();
+    const uint64_t* ram = c.V().s_ram();
+    const uint64_t* pres = c.V().s_present();
+    const uint64_t BIG = 1ull << 46;
+    uint32_t touched = NB;
+    uint64_t best_key = 0;
+    int32_t best_n = -1;
+#if K10S_DEVICE
+    // lane b holds block b's bound key (0: no node of the block can fit)
+    const uint32_t lane = (uint32_t)lane_id();
+    uint64_t bkey = 0;
+    bool big = false;
+    if (lane < NB) {
+        const uint32_t A = bc[lane];
+        const uint64_t Rm = br[lane];
+        big = Rm >= BIG;
+        if (A >= rc && Rm >= rr) bkey = score_key(la_score(A, Rm, rc, rr));
+    }
+    if (wave_any(big)) return -1;
+    for (;;) {
+        uint64_t k = bkey;
+        int32_t bi = bkey ? (int32_t)lane : -1;
+        wave_argmax(k, bi);
+        if (k == 0) break;
+        if (best_n >= 0 && (k < best_key || (k == best_key && (int32_t)(((uint32_t)bi + 1u) << sh) <= best_n))) break;
+        const uint32_t lo = (uint32_t)bi << sh;
+        const uint32_t hi = (lo + (1u << sh)) < N ? (lo + (1u << sh)) : N;
+        uint64_t lk = 0;
+        int32_t ln = -1;
+        for (uint32_t n = lo + lane; n < hi; n += 64) {
+            if ((pres[n >> 6] >> (n & 63)) & 1ull) {
+                const uint32_t ac = cpu[n];
+                const uint64_t ar = ram[n];
+                if (rc <= ac && rr <= ar) {
+                    const uint64_t kk = score_key(la_score(ac, ar, rc, rr));
+                    if (kk >= lk) {
+                        lk = kk;
+                        ln = (int32_t)n;
+                    }
+                }
+            }
+        }
+        touched += hi - lo;
+        wave_argmax(lk, ln);
+        if (ln >= 0 && (lk > best_key || (lk == best_key && ln > best_n))) {
+            best_key = lk;
+            best_n = ln;
+        }
+        if ((int32_t)lane == bi) bkey = 0;
+    }
+#else
+    uint64_t keys[64];
+    for (uint32_t b = 0; b < NB; b++) {
+        if (br[b] >= BIG) return -1;
+        keys[b] = (bc[b] >= rc && br[b] >= rr) ? score_key(la_score(bc[b], br[b], rc, rr)) : 0;
+    }
+    for (;;) {
+        uint64_t k = 0;
+        int32_t bi = -1;
+        for (uint32_t b = 0; b < NB; b++)
+            if (keys[b] && keys[b] >= k) {
+                k = keys[b];
+                bi = (int32_t)b;
+            }
+        if (k == 0) break;
+        if (best_n >= 0 && (k < best_key || (k == best_key && (int32_t)(((uint32_t)bi + 1u) << sh) <= best_n))) break;
+        const uint32_t lo = (uint32_t)bi << sh;
+        const uint32_t hi = (lo + (1u << sh)) < N ? (lo + (1u << sh)) : N;
+        for (uint32_t n = lo; n < hi; n++) {
+            if (!((pres[n >> 6] >> (n & 63)) & 1ull)) continue;
+            if (rc <= cpu[n] && rr <= ram[n]) {
+                const uint64_t kk = score_key(la_score(cpu[n], ram[n], rc, rr));
+                if (kk > best_key || (kk == best_key && (int32_t)n > best_n)) {  // (key, index) max
+                    best_key = kk;
+                    best_n = (int32_t)n;
+                }
+            }
+        }
+        touched += hi - lo;
+        keys[bi] = 0;
+    }
+#endif
+    *nread = touched;
+    if (best_n < 0) return K10S_SCHED_NO_SUFFICIENT_RESOURCES;
+    *chosen = best_n;
     return K10S_SCHED_OK;
 }
 
@@ -551,7 +731,17 @@ K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
         } else {
             h->counters[K10S_C_ATTEMPTS] += 1;
             h->counters[K10S_C_NODES_SCANNED] += nn;
-            st = schedule_scan(c.V().s_cpu(), c.V().s_ram(), c.V().s_present(), c.S().n_nodes, rc, rr, w, &chosen);
+            st = -1;
+            uint32_t nread = 0;
+            const uint64_t t_scan = prof_now();
+            if (c.Ly().pruned && w == 1.0 && rc > 0 && rr > 0) st = schedule_scan_pruned(c, rc, rr, &chosen, &nread);
+            if (st < 0) {
+                st = schedule_scan(c.V().s_cpu(), c.V().s_ram(), c.V().s_present(), c.S().n_nodes, rc, rr, w, &chosen);
+                nread = c.S().n_nodes;
+            }
+            h->counters[K10S_C_NODES_READ] += nread;
+            K10S_PROF_ADD(c, PROF_SCAN, t_scan);
+            if (K10S_PROF) h->prof[PROF_NSCAN] += 1;
         }
         if (st != K10S_SCHED_OK) {
             q.timestamp = t + cycle_dur;
@@ -562,6 +752,7 @@ K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
         uint32_t n = (uint32_t)chosen;
         c.V().s_cpu()[n] -= rc;  // reserve_node_resources (118-123)
         c.V().s_ram()[n] -= rr;
+        node_bound_changed(c, n);
         c.V().node(n).flags |= NF_S_ASSIGN;  // assign_node_to_pod (125-151)
         c.V().pod(p).s_assigned = (int32_t)n;
         emit(c, K10S_EV_AS_ASSIGN_REQ, cycle_dur + c.P().sched_to_as_network_delay, -1, p, n, t + cycle_dur, FQ_ASSIGN);
@@ -618,14 +809,18 @@ K10S_HD void s_release(Ctx& c, uint32_t p) {  // release_node_resources (153-162
     }
     c.V().s_cpu()[n] += c.V().pod(p).req_cpu;
     c.V().s_ram()[n] += c.V().pod(p).req_ram;
+    node_bound_changed(c, (uint32_t)n);
 }
 
 K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
     RepHdr* h = &c.H();
     switch (e.kind) {
-    case K10S_EV_S_RUN_CYCLE:
+    case K10S_EV_S_RUN_CYCLE: {
+        const uint64_t t0 = prof_now();
         run_scheduling_cycle(c, e.time);
+        K10S_PROF_ADD(c, PROF_CYCLE, t0);
         break;
+    }
     case K10S_EV_S_FLUSH:
         s_move(c, 1, e.time, 0, 0);
         emit0(c, K10S_EV_S_FLUSH, 30.0);  // POD_FLUSH_INTERVAL (queue.rs:11)
@@ -640,6 +835,7 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
             bit_set(c.V().s_present(), n);
             h->s_node_count += 1;
         }
+        node_bound_changed(c, n);
         if (c.P().enable_unscheduled_pods_conditional_move) s_move(c, 3, 0.0, ac, ar);
         else s_move(c, 0, 0.0, 0, 0);
         break;
@@ -680,6 +876,7 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
         }
         bit_clear(c.V().s_present(), n);
         h->s_node_count -= 1;
+        node_bound_changed(c, n);
         if (c.V().node(n).flags & NF_S_ASSIGN) {  // reschedule_unfinished_pods (352-364), name order
             c.V().node(n).flags &= (uint8_t)~NF_S_ASSIGN;
             double t = e.time;
@@ -1526,6 +1723,9 @@ K10S_HD void init_replica(Ctx& c) {
         bit_set(v.s_present(), n);
     }
     h->s_node_count = sc->n_default;
+    wave_sync();
+    for (uint32_t b = 0; b < L->nblocks; b++) block_recompute(c, b);  // zero bounds for absent nodes
+    h->counters[K10S_C_NODES_READ] = 0;
     h->ps_node_count = sc->n_default;
     h->as_node_count = sc->n_default;
     h->cur_kind = 0xFFFF;
@@ -1544,7 +1744,7 @@ enum : int { SRC_TRACE = K10S_NFQ, SRC_HEAP = K10S_NFQ + 1 };
 
 // Which source holds the minimum (time, id): a FIFO class 0..K10S_NFQ-1, SRC_TRACE, SRC_HEAP, or
 // -1 when all are empty.  Device: lanes 0..7 hold the FIFO heads, lane 8 the heap root, lane 9 the
-// trace head; a 4-step xor-shuffle min over the 16-lane group, broadcast from lane 0.
+// trace head; a 4-step DPP min over the 16-lane row, broadcast from lane 0.
 K10S_HD int next_source(Ctx& c, uint32_t ntr) {
     const RepHdr& H = c.H();
     const uint32_t cur = H.trace_cursor;
@@ -1579,18 +1779,12 @@ K10S_HD int next_source(Ctx& c, uint32_t ntr) {
             src = SRC_TRACE;
         }
     }
-#pragma unroll
-    for (int m = 8; m >= 1; m >>= 1) {
-        int64_t ok = (int64_t)shfl_xor_u64((uint64_t)k, m);
-        uint32_t os = (uint32_t)__shfl_xor((int)sq, m, 64);
-        int osrc = __shfl_xor(src, m, 64);
-        if (ok < k || (ok == k && os < sq)) {
-            k = ok;
-            sq = os;
-            src = osrc;
-        }
-    }
-    return (int)__builtin_amdgcn_readfirstlane(src);
+    uint32_t us = (uint32_t)src;
+    keymin_step<0>(k, sq, us);
+    keymin_step<1>(k, sq, us);
+    keymin_step<2>(k, sq, us);
+    keymin_step<3>(k, sq, us);
+    return (int)__builtin_amdgcn_readfirstlane((int)us);
 #else
     int64_t k = tkey;
     uint32_t sq = tseq;
@@ -1648,9 +1842,10 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
     uint64_t done = 0;
     int more = 0;
     uint32_t status = K10S_REPLICA_RUNNING;
+    const uint64_t t_loop = prof_now();
     while (!h->error_code) {
-        if (mode == K10S_RUN_UNTIL_ALL_FINISHED && is_multiple_of_1000(h->clock) &&
-            h->counters[K10S_C_TERMINATED_PODS] >= total_pods) {
+        if (mode == K10S_RUN_UNTIL_ALL_FINISHED && h->counters[K10S_C_TERMINATED_PODS] >= total_pods &&
+            is_multiple_of_1000(h->clock)) {
             status = K10S_REPLICA_FINISHED;
             break;
         }
@@ -1659,6 +1854,7 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
         HeapEv e;
         int src = 0;
         bool have = false;
+        const uint64_t t_sel = prof_now();
         for (;;) {
             src = next_source(c, ntr);
             if (src < 0) break;
@@ -1689,6 +1885,7 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
             have = true;
             break;
         }
+        K10S_PROF_ADD(c, PROF_SELECT, t_sel);
         if (!have) {
             if (mode == K10S_RUN_UNTIL_TIME) h->clock = until_time;
             status = mode == K10S_RUN_UNTIL_TIME ? K10S_REPLICA_RUNNING : K10S_REPLICA_FINISHED;
@@ -1706,7 +1903,9 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
             more = 1;
             break;
         }
+        const uint64_t t_con = prof_now();
         consume_source(c, src);
+        K10S_PROF_ADD(c, PROF_CONSUME, t_con);
         h->clock = e.time;
         h->cur_kind = e.kind;
         h->cur_seq = e.seq;
@@ -1756,8 +1955,11 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
                 h->flags |= 1u;
             }
         }
+        const uint64_t t_dis = prof_now();
         dispatch(c, e);
+        K10S_PROF_ADD(c, PROF_DISPATCH, t_dis);
     }
+    K10S_PROF_ADD(c, PROF_LOOP, t_loop);
     if (h->error_code) status = K10S_REPLICA_ERROR;
     h->status = status;
     return more;

@@ -90,7 +90,10 @@ static int32_t engine_init(k10s_engine* e) {
 extern "C" {
 
 const char* k10s_last_error(void) { return g_err.c_str(); }
-const char* k10s_version(void) { return "k10s-mi355x 0.1 (gfx950)"; }
+#ifndef K10S_BUILD_ID
+#define K10S_BUILD_ID "dev"
+#endif
+const char* k10s_version(void) { return "k10s-mi355x 0.2 (gfx950) build " K10S_BUILD_ID; }
 
 int32_t k10s_schedule_one_batch(const uint32_t* alloc_cpu, const uint64_t* alloc_ram, const uint64_t* present_bits,
                                 uint32_t n_nodes, uint32_t node_stride, const uint32_t* req_cpu, const uint64_t* req_ram,
@@ -349,6 +352,17 @@ int32_t k10s_engine_results(const k10s_engine* e, k10s_replica_result* out) {
     HIPCHK(hipMemcpy2D(hdr.data(), sizeof(RepHdr), e->d_state + e->L.hdr, e->L.stride, sizeof(RepHdr), e->R,
                        hipMemcpyDeviceToHost));
     for (uint32_t r = 0; r < e->R; r++) hdr_to_result(hdr[r], out[r]);
+    return K10S_OK;
+}
+
+int32_t k10s_engine_profile(const k10s_engine* e, uint64_t* out) {
+    if (!e || !out) return set_err(K10S_E_INVALID, "null");
+    std::vector<RepHdr> hdr(e->R);
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipMemcpy2D(hdr.data(), sizeof(RepHdr), e->d_state + e->L.hdr, e->L.stride, sizeof(RepHdr), e->R,
+                       hipMemcpyDeviceToHost));
+    for (uint32_t r = 0; r < e->R; r++)
+        for (int i = 0; i < 8; i++) out[(size_t)r * 8 + i] = hdr[r].prof[i];
     return K10S_OK;
 }
 

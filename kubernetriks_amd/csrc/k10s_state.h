@@ -170,6 +170,8 @@ struct RepHdr {
     double fq_last[K10S_NFQ];
     HeapEv fq_top[K10S_NFQ];
     HeapEv heap_top;
+    // cycle attribution of the event loop (K10S_PROF builds only, zero otherwise): K10S_PROF_*
+    uint64_t prof[8];
 };
 
 struct QInfo {              // QueuedPodInfo (queue.rs:13-27), 24 B
@@ -249,14 +251,17 @@ struct Layout {
     uint64_t stride;
     uint64_t hdr;
     uint64_t s_cpu, s_ram, s_present;    // hot scheduler-cache SoA (scan target)
+    uint64_t s_bcpu, s_bram;             // per-block maxima of the present nodes' allocatable
     uint64_t node, pend_rm, pod, prec, slot, pool_ring;
     uint64_t grp, grp_bits;
     uint64_t cag, ca_act, ca_cpu, ca_ram, ca_undo;
     uint64_t heap, aq, uq, log, place, fq;
     uint32_t cap_fq;      // entries per delay-class ring (power of two; 0 = no rings)
-    uint32_t pad0;
+    uint32_t pruned;      // 1: block bounds maintained, exact pruned scan where it applies
     uint32_t cap_heap, cap_aq, cap_uq, cap_act, cap_log, cap_place, cap_undo, rec_on;
     uint32_t words_nodes, words_uids, words_group;
+    uint32_t bshift;      // block = 2^bshift consecutive node indices (>= 64, <= 64 blocks)
+    uint32_t nblocks;
     uint32_t pad;
 };
 

@@ -14,12 +14,12 @@ from typing import Dict, List, Optional, Sequence
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("K10S_LIB") or os.path.join(REPO, "build", "libk10s.so")
 
-NUM_COUNTERS = 16
+NUM_COUNTERS = 17
 COUNTER_NAMES = [
     "total_nodes_in_trace", "total_pods_in_trace", "pods_succeeded", "pods_unschedulable", "pods_failed",
     "pods_removed", "total_scaled_up_nodes", "total_scaled_down_nodes", "total_scaled_up_pods",
     "total_scaled_down_pods", "processed_nodes", "terminated_pods", "placements", "attempts", "events",
-    "nodes_scanned",
+    "nodes_scanned", "nodes_read",
 ]
 EST_NAMES = ["pod_duration", "pod_schedule_time", "pod_queue_time"]
 
@@ -61,7 +61,7 @@ class Capacities(ctypes.Structure):
                 ("unschedulable", ctypes.c_uint32), ("group_name_bound", ctypes.c_uint32),
                 ("ca_name_bound", ctypes.c_uint32), ("event_log", ctypes.c_uint32),
                 ("placement_log", ctypes.c_uint32), ("pod_records", ctypes.c_uint32),
-                ("delay_fifo", ctypes.c_uint32)]
+                ("delay_fifo", ctypes.c_uint32), ("pruned_scan", ctypes.c_uint32)]
 
 
 class LogEntry(ctypes.Structure):
@@ -289,6 +289,17 @@ class Engine(EngineBase):
 
     def step_until_time(self, t: float, max_events_per_launch: int = 0) -> float:
         return self.run(RUN_UNTIL_TIME, t, 1e300, max_events_per_launch)
+
+    def profile(self):
+        """Per-replica cycle attribution (K10S_PROF variant builds; zeros otherwise): a list of
+        dicts with loop/select/consume/dispatch/cycle/scan/scans/bounds."""
+        n = self.n_replicas * 8
+        buf = (ctypes.c_uint64 * n)()
+        self._L.k10s_engine_profile.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        self._L.k10s_engine_profile.restype = ctypes.c_int32
+        self._check(self._L.k10s_engine_profile(self._h, buf))
+        keys = ["loop", "select", "consume", "dispatch", "cycle", "scan", "scans", "bounds"]
+        return [dict(zip(keys, buf[r * 8:(r + 1) * 8])) for r in range(self.n_replicas)]
 
     def step_async(self, mode: int, until_time: float, max_time: float, budget: int):
         self._check(self._L.k10s_engine_step_async(self._h, mode, until_time, max_time, budget))

@@ -26,9 +26,10 @@ def feq(a: float, b: float) -> bool:
     return fbits(a) == fbits(b)
 
 
-def parity_caps(log: bool = True, fifo: int = 0) -> Capacities:
+def parity_caps(log: bool = True, fifo: int = 0, pruned: int = 0) -> Capacities:
     c = Capacities()
     c.delay_fifo = fifo
+    c.pruned_scan = pruned
     c.event_log = (1 << 20) if log else 0
     c.placement_log = 1 << 20
     c.pod_records = 1
@@ -36,7 +37,8 @@ def parity_caps(log: bool = True, fifo: int = 0) -> Capacities:
 
 
 def run_pair(engine_cls, scenario: str, mode: int = RUN_UNTIL_ALL_FINISHED, until: Optional[float] = None,
-             max_time: float = 1e7, budget: int = 0, log: bool = True, params=None, fifo: int = 0):
+             max_time: float = 1e7, budget: int = 0, log: bool = True, params=None, fifo: int = 0,
+             pruned: int = 0):
     """Run the oracle and one engine replica on the same scenario; return (oracle dict, engine, res)."""
     o = ob.OracleSim(scenario, log=log)
     if mode == RUN_UNTIL_ALL_FINISHED:
@@ -45,7 +47,7 @@ def run_pair(engine_cls, scenario: str, mode: int = RUN_UNTIL_ALL_FINISHED, unti
         st = o.step_until_time(until)
     od = o.result(placements=True, log=log)
     od["status_name"] = ORACLE_STATUS[st] if not od["panicked"] else "error"
-    eng = engine_cls(scenario, 1, params=params, caps=parity_caps(log, fifo))
+    eng = engine_cls(scenario, 1, params=params, caps=parity_caps(log, fifo, pruned))
     if mode == RUN_UNTIL_ALL_FINISHED:
         eng.run_until_all_finished(max_time, budget)
     else:

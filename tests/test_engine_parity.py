@@ -107,6 +107,54 @@ def test_fifo_capacity_gpu(seed, fifo):
     assert parity.compare(od, eng) == [], (seed, fifo)
 
 
+# Block-bound pruned scan: many-node clusters (several 64-node blocks), identical
+# nodes (score ties decided by the last index), node removals; the pruned engine, the full-scan
+# engine and the oracle must agree event for event.
+PRUNE_SEEDS = list(range(200, 216))
+
+
+def _prune_case(backend, seed, pruned):
+    n_nodes = (70, 130, 257, 400)[seed % 4]
+    scn = gen.random_scenario(seed, n_pods=240, n_nodes=n_nodes, same_nodes=(seed % 2 == 0))
+    od, eng = parity.run_pair(engine_cls(backend), scn, max_time=40000.0, pruned=pruned)
+    assert parity.compare(od, eng) == [], (seed, pruned)
+    return eng.results()[0]["counters"]
+
+
+@pytest.mark.parametrize("seed", PRUNE_SEEDS)
+def test_pruned_scan_many_nodes_host(seed):
+    c = _prune_case("host", seed, 1)
+    f = _prune_case("host", seed, 0)
+    assert c["placements"] == f["placements"] and c["attempts"] == f["attempts"]
+
+
+def test_pruned_scan_reads_less():
+    """The bound prunes where blocks differ: big nodes first in name order, small ones after."""
+    from kubernetriks_amd.scenario import GenericClusterTrace, GenericWorkloadTrace, Node, Pod
+    c = GenericClusterTrace()
+    for i in range(256):
+        big = i < 64
+        c.create_node(0.0, Node(f"node_{i:03d}", 128000 if big else 8000, (256 if big else 16) << 30))
+    w = GenericWorkloadTrace()
+    for i in range(300):
+        w.create_pod(float(1 + i // 10), Pod(f"pod_{i:03d}", 500 + (i % 7) * 100, (1 + i % 3) << 30, 400.0))
+    scn = scenario_text(SimulationConfig(), c, w)
+    od, eng = parity.run_pair(engine_cls("host"), scn, max_time=1e6, pruned=1)
+    assert parity.compare(od, eng) == []
+    k = eng.results()[0]["counters"]
+    # each node addition re-derives its block's bound (64 entries); the rest is scans + upkeep
+    per_attempt = (k["nodes_read"] - 64 * k["processed_nodes"]) / k["attempts"]
+    assert k["attempts"] == 300 and per_attempt < 0.8 * 256, k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", PRUNE_SEEDS)
+def test_pruned_scan_many_nodes_gpu(seed):
+    c = _prune_case("gpu", seed, 1)
+    f = _prune_case("gpu", seed, 0)
+    assert c["placements"] == f["placements"] and c["attempts"] == f["attempts"]
+
+
 @pytest.mark.parametrize("backend", BACKENDS)
 def test_budgeted_launches_equal_one_launch(backend):
     """Pausing every few events (multi-launch runs) must not change anything."""
