@@ -106,6 +106,7 @@ def main():
 
     from kubernetriks_amd.build import build
     build()
+    from kubernetriks_amd import ensemble
     from kubernetriks_amd import workloads as wl
     from kubernetriks_amd.native import NUM_COUNTERS, Capacities, Engine, version
     from kubernetriks_amd.scenario import SimulationConfig, scenario_text
@@ -117,7 +118,7 @@ def main():
     probe = Engine(scn, 1, device=local_rank)
     defaults = probe.default_params()
     probe.close()
-    params = wl.replica_params(defaults, R, base_seed=123, perturb=True, replica_offset=rank * R)
+    params = ensemble.shard_params(defaults, R, rank, base_seed=123, perturb=True)  # replicas [rank*R, (rank+1)*R)
     t = time.perf_counter()
     caps = Capacities()
     caps.pruned_scan = 1 if args.pruned_scan else 0
@@ -162,13 +163,11 @@ def main():
     if statuses.get(2):
         log(f"[rank {rank}] WARNING: {statuses[2]} replicas ended in error: {errors}")
 
-    tvec = torch.tensor([elapsed, sum(kernel_ms) / len(kernel_ms)], dtype=torch.float64, device="cuda")
-    cvec = torch.tensor(counters, dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(tvec, op=dist.ReduceOp.MAX)
-        dist.all_reduce(cvec, op=dist.ReduceOp.SUM)  # RCCL over xGMI: metric counters only
-    elapsed, mean_kernel_ms = float(tvec[0]), float(tvec[1])
-    c = cvec.cpu().numpy()
+    # cross-rank reduction (RCCL over xGMI): max of the timings, sum of the counters; the per-replica
+    # estimators of the last step are gathered in rank order into the job's ensemble summary
+    elapsed, mean_kernel_ms = ensemble.max_over_ranks([elapsed, sum(kernel_ms) / len(kernel_ms)])
+    c = ensemble.sum_over_ranks(counters.tolist())
+    summary = ensemble.ensemble_summary(eng.raw_results()).as_dict()
     placements, attempts, events, scanned, nread = c[12], c[13], c[14], c[15], c[16]
     value = placements / elapsed
 
@@ -217,6 +216,10 @@ def main():
         "totals": {"placements": placements, "attempts": attempts, "events": events, "nodes_scanned": scanned,
                    "nodes_read": nread,
                    "replica_status": {str(k): v for k, v in statuses.items()}, "replica_errors": errors},
+        "ensemble": {"replicas": summary["replicas"], "replica_status": summary["replica_status"],
+                     "counters": {k: summary["counters"][k] for k in ("total_pods_in_trace", "pods_succeeded",
+                                                                       "terminated_pods", "placements", "events")},
+                     "timings": summary["timings"]},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

@@ -94,10 +94,15 @@ def c2_workload(n_pods: int = 2000, seed: int = 123, horizon: float = 5000.0) ->
     return w
 
 
-def c2_scenario(n_pods: int = 2000, seed: int = 123) -> str:
+def c2_parts(n_pods: int = 2000, seed: int = 123):
+    """(config, cluster trace, workload trace) of C2: the 31-node default cluster, no cluster trace."""
     cfg = SimulationConfig()
     cfg.default_cluster = default_cluster_31()
-    return scenario_text(cfg, GenericClusterTrace(), c2_workload(n_pods, seed))
+    return cfg, GenericClusterTrace(), c2_workload(n_pods, seed)
+
+
+def c2_scenario(n_pods: int = 2000, seed: int = 123) -> str:
+    return scenario_text(*c2_parts(n_pods, seed))
 
 
 # ---- Alibaba-like (C3) ------------------------------------------------------------------------
@@ -165,6 +170,11 @@ def c3_scenario(n_nodes: int = 4096, n_pods: int = 16384, arrival_window: float 
 def c4_scenario(n_batch_pods: int = 400, seed: int = 7) -> str:
     """tests/test_hpa.rs pod group + config.yaml:14-33 CA node groups, with a burst of batch pods
     that forces scale-up and then drains (scale-down)."""
+    return scenario_text(*c4_parts(n_batch_pods, seed))
+
+
+def c4_parts(n_batch_pods: int = 400, seed: int = 7):
+    """(config, cluster trace, workload trace) of C4 (see c4_scenario)."""
     rng = random.Random(seed)
     cfg = SimulationConfig()
     cfg.hpa_enabled = True
@@ -181,7 +191,7 @@ def c4_scenario(n_batch_pods: int = 400, seed: int = 7) -> str:
         w.create_pod(float(100 + int(rng.random() * 300)),
                      Pod(f"batch_{i}", rng.choice([4000, 8000, 16000]), rng.choice([8, 16, 32]) << 30,
                          float(rng.randint(60, 600))))
-    return scenario_text(cfg, c, w)
+    return cfg, c, w
 
 
 # ---- parameter sweep (C5) ---------------------------------------------------------------------
@@ -204,6 +214,30 @@ def c5_params(defaults, n: int, base_seed: int = 123, replica_offset: int = 0):
         p.perturb = 1
         out.append(p)
     return out
+
+
+def config_for_params(cfg: SimulationConfig, p) -> SimulationConfig:
+    """The SimulationConfig a replica with k10s_replica_params `p` runs under (the per-replica
+    sweep axes mapped back onto config.rs fields), so the CPU oracle can replay that replica."""
+    import copy
+    c = copy.deepcopy(cfg)
+    c.scheduling_cycle_interval = p.scheduling_cycle_interval
+    c.enable_unscheduled_pods_conditional_move = bool(p.enable_unscheduled_pods_conditional_move)
+    for k in ("as_to_ps", "ps_to_sched", "sched_to_as", "as_to_node", "as_to_ca", "as_to_hpa"):
+        setattr(c, f"{k}_network_delay", getattr(p, f"{k}_network_delay"))
+    c.ca_scan_interval = p.ca_scan_interval
+    c.ca_scale_down_utilization_threshold = p.ca_scale_down_utilization_threshold
+    c.hpa_scan_interval = p.hpa_scan_interval
+    c.hpa_target_threshold_tolerance = p.hpa_target_threshold_tolerance
+    c.score_weight = p.score_weight
+    return c
+
+
+def replica_scenario(cfg: SimulationConfig, cluster: GenericClusterTrace, workload: GenericWorkloadTrace, p) -> str:
+    """Scenario text of one replica as the oracle must see it: its parameters and, when perturbed,
+    its seed-perturbed workload (the engine applies both on the device)."""
+    w = perturb_workload(workload, p.seed) if p.perturb else workload
+    return scenario_text(config_for_params(cfg, p), cluster, w)
 
 
 def ctypes_copy(dst, src):

@@ -1,0 +1,98 @@
+"""BASELINE.json configs C2, C4 and C5 as batched parity cases: R replicas in one engine batch, each
+replica compared bit-exactly (counters, estimators, clock, placements, per-pod times) with the CPU
+oracle run on that replica's own scenario (its parameters + its seed-perturbed trace, materialized
+on the host by workloads.replica_scenario).  Shapes are scaled down so the oracle finishes in
+seconds; the full-size configs run in bench.py.
+
+  C2  31-node default cluster (config.yaml:45-68), test_determinism-style pods, seed-perturbed
+  C4  test_hpa.rs pod group + config.yaml:14-33 CA node groups, burst workload (scale-up, drain)
+  C5  C3-shaped cluster with the scheduler/autoscaler parameter sweep (cycle interval, conditional
+      move, network delays, CA threshold, HPA tolerance), and the same sweep over the C4 scenario
+"""
+import pytest
+
+import oracle_bridge as ob
+import parity
+from hostcheck_bridge import HostEngine
+from kubernetriks_amd import workloads as wl
+from kubernetriks_amd.native import RUN_UNTIL_ALL_FINISHED, RUN_UNTIL_TIME
+from kubernetriks_amd.scenario import scenario_text
+
+BACKENDS = [pytest.param("host", id="host"), pytest.param("gpu", id="gpu", marks=pytest.mark.gpu)]
+
+
+def engine_cls(backend):
+    if backend == "host":
+        return HostEngine
+    from kubernetriks_amd.native import Engine
+    return Engine
+
+
+def _batch_parity(backend, parts, params_fn, R, check, mode=RUN_UNTIL_ALL_FINISHED, until=0.0, max_time=1e6):
+    cfg, c, w = parts
+    E = engine_cls(backend)
+    probe = E(scenario_text(cfg, c, w), 1)
+    params = params_fn(probe.default_params(), R)
+    eng = E(scenario_text(cfg, c, w), R, params=params, caps=parity.parity_caps(False))
+    if mode == RUN_UNTIL_ALL_FINISHED:
+        eng.run_until_all_finished(max_time)
+    else:
+        eng.step_until_time(until)
+    for r in check:
+        o = ob.OracleSim(wl.replica_scenario(cfg, c, w, params[r]))
+        st = o.run_until_all_finished(max_time) if mode == RUN_UNTIL_ALL_FINISHED else o.step_until_time(until)
+        od = o.result(placements=True)
+        od["status_name"] = parity.ORACLE_STATUS[st] if not od["panicked"] else "error"
+        assert parity.compare(od, eng, r=r, log=False) == [], r
+    return eng
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_c2_default_cluster_seed_perturbed(backend):
+    R = 32 if backend == "gpu" else 4
+    eng = _batch_parity(backend, wl.c2_parts(n_pods=300, seed=123),
+                        lambda d, n: wl.replica_params(d, n, base_seed=123, perturb=True), R,
+                        check=sorted({0, 1, R // 2, R - 1}))
+    res = eng.results()
+    assert all(r["status"] == "finished" for r in res)
+    assert len({r["counters"]["events"] for r in res}) > 1  # perturbation makes replicas differ
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_c4_hpa_and_cluster_autoscaler_batched(backend):
+    R = 24 if backend == "gpu" else 3
+    eng = _batch_parity(backend, wl.c4_parts(n_batch_pods=80, seed=7),
+                        lambda d, n: wl.replica_params(d, n, base_seed=7, perturb=True), R,
+                        check=sorted({0, R // 2, R - 1}), mode=RUN_UNTIL_TIME, until=1500.0)
+    c = eng.results()[0]["counters"]
+    assert c["total_scaled_up_nodes"] > 0 and c["total_scaled_up_pods"] > 0
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_c5_parameter_sweep_c3_shape(backend):
+    R = 48 if backend == "gpu" else 8
+    # replicas 0..7 cover every cycle interval with and without conditional move
+    parts = (wl.SimulationConfig(),) + wl.c3_traces(n_nodes=192, n_pods=400, arrival_window=200.0, seed=11)
+    _batch_parity(backend, parts, lambda d, n: wl.c5_params(d, n, base_seed=123), R,
+                  check=list(range(8)) if backend == "host" else [0, 3, 5, 8, 13, 24, 31, 47])
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_c5_parameter_sweep_over_autoscalers(backend):
+    """The sweep axes that only matter with autoscalers on: CA scale-down threshold (replica // 24)
+    and HPA tolerance (replica // 72), over the C4 scenario."""
+    idx = [0, 24, 48, 72, 144] if backend == "host" else list(range(0, 216, 9))
+    R = max(idx) + 1
+    cfg, c, w = wl.c4_parts(n_batch_pods=40, seed=3)
+    E = engine_cls(backend)
+    probe = E(scenario_text(cfg, c, w), 1)
+    allp = wl.c5_params(probe.default_params(), R, base_seed=500)
+    params = [allp[i] for i in idx]
+    eng = E(scenario_text(cfg, c, w), len(idx), params=params, caps=parity.parity_caps(False))
+    eng.step_until_time(1500.0)
+    for k in range(len(idx)):
+        o = ob.OracleSim(wl.replica_scenario(cfg, c, w, params[k]))
+        o.step_until_time(1500.0)
+        od = o.result(placements=True)
+        od["status_name"] = parity.ORACLE_STATUS[4] if not od["panicked"] else "error"
+        assert parity.compare(od, eng, r=k, log=False) == [], idx[k]
