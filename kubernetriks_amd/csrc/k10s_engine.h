@@ -204,6 +204,57 @@ enum : int {
     FQ_NOW = 7,          // emit_now (delay 0)
 };
 
+// Heap position i: the top K10S_HEAP_TOP positions (levels 0-2 of the 8-ary heap) are in the working
+// header, the rest in the replica's HBM heap array.  Level boundaries coincide with K10S_HEAP_TOP,
+// so the children of one node are either all in the header or all in HBM.
+static_assert(K10S_HEAP_TOP == 1 + K10S_HEAP_D + K10S_HEAP_D * K10S_HEAP_D, "heap top = levels 0..2");
+// Device: both arrays are reached through address-space-typed pointers (LDS symbol, global
+// pointer), so the compiler can never merge the two paths into one generic (FLAT) access.
+#if K10S_DEVICE
+// HBM part through a raw buffer descriptor (scalar base, 32-bit offsets): distinct instructions
+// from the LDS path, so the two are never merged into one generic (FLAT) access.
+K10S_D __amdgpu_buffer_rsrc_t heap_rsrc(Ctx& c) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(c.V().b + k10s_dc.L.heap), (short)0,
+                                             (int)(k10s_dc.L.cap_heap * (uint32_t)sizeof(HeapEv)), 0x00020000);
+}
+K10S_D HeapEv heap_get(Ctx& c, uint32_t i) {
+    if (i < K10S_HEAP_TOP) return k10s_hdr.heap_lds[i];
+    const __amdgpu_buffer_rsrc_t rs = heap_rsrc(c);
+    const int off = (int)(i * (uint32_t)sizeof(HeapEv));
+    auto lo = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    auto hi = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0);
+    HeapEv e;
+    e.time = u2f(((uint64_t)lo[1] << 32) | lo[0]);
+    e.seq = lo[2];
+    e.kind = (uint16_t)lo[3];
+    e.slot = (int16_t)(lo[3] >> 16);
+    e.a = hi[0];
+    e.b = hi[1];
+    e.x = u2f(((uint64_t)hi[3] << 32) | hi[2]);
+    return e;
+}
+K10S_D void heap_put(Ctx& c, uint32_t i, const HeapEv& e) {
+    if (i < K10S_HEAP_TOP) {
+        k10s_hdr.heap_lds[i] = e;
+        return;
+    }
+    const __amdgpu_buffer_rsrc_t rs = heap_rsrc(c);
+    const int off = (int)(i * (uint32_t)sizeof(HeapEv));
+    const uint64_t tb = f2u(e.time), xb = f2u(e.x);
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    v4u lo = {(uint32_t)tb, (uint32_t)(tb >> 32), e.seq, (uint32_t)e.kind | ((uint32_t)(uint16_t)e.slot << 16)};
+    v4u hi = {e.a, e.b, (uint32_t)xb, (uint32_t)(xb >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b128(lo, rs, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(hi, rs, off + 16, 0, 0);
+}
+#else
+K10S_HD HeapEv heap_get(Ctx& c, uint32_t i) { return i < K10S_HEAP_TOP ? c.H().heap_lds[i] : c.V().heap()[i]; }
+K10S_HD void heap_put(Ctx& c, uint32_t i, const HeapEv& e) {
+    if (i < K10S_HEAP_TOP) c.H().heap_lds[i] = e;
+    else c.V().heap()[i] = e;
+}
+#endif
+
 K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uint32_t a, uint32_t b, double x,
                           int cls = FQ_HEAP) {
     RepHdr& H = c.H();
@@ -225,7 +276,12 @@ K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uin
     if (cls >= 0 && cap) {
         const uint32_t hd = H.fq_head[cls], tl = H.fq_tail[cls];
         if (tl - hd < cap && (tl == hd || k >= total_key(H.fq_last[cls]))) {
-            c.V().fq()[(uint32_t)cls * cap + (tl & (cap - 1))] = e;
+            if (H.fq_wend[cls] == tl && tl - hd < K10S_FQW) {  // the window holds the whole ring: append
+                H.fq_win[(uint32_t)cls * K10S_FQW + (tl & (K10S_FQW - 1))] = e;
+                H.fq_wend[cls] = tl + 1;
+            } else {
+                c.V().fq()[(uint32_t)cls * cap + (tl & (cap - 1))] = e;
+            }
             if (tl == hd) H.fq_top[cls] = e;
             H.fq_tail[cls] = tl + 1;
             H.fq_last[cls] = e.time;
@@ -238,18 +294,18 @@ K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uin
         return 0;
     }
     H.next_seq = e.seq + 1;
-    HeapEv* hp = c.V().heap();
-    uint32_t pos = H.heap_size;
+    uint32_t pos = uniform_u32(H.heap_size);
     H.heap_size = pos + 1;
     while (pos > 0) {
         uint32_t parent = (pos - 1) / K10S_HEAP_D;
-        HeapEv p = hp[parent];
+        HeapEv p = heap_get(c, parent);
+        uniform_event(p);  // wave-uniform by construction: keep the sift loop on the scalar unit
         int64_t kp = total_key(p.time);
         if (!(k < kp || (k == kp && e.seq < p.seq))) break;
-        hp[pos] = p;
+        heap_put(c, pos, p);
         pos = parent;
     }
-    hp[pos] = e;
+    heap_put(c, pos, e);
     if (pos == 0) H.heap_top = e;
     return e.seq;
 }
@@ -257,15 +313,22 @@ K10S_HD uint32_t emit0(Ctx& c, uint32_t kind, double delay) { return emit(c, kin
 
 // Smallest (time, id) among children [first, min(first + D, n)); returns its index.  Device: lanes
 // 0..7 load one child each (one 256-B read) and reduce with 3 DPP steps.
-K10S_HD uint32_t heap_min_child(const HeapEv* hp, uint32_t first, uint32_t n, int64_t& kmin, uint32_t& smin) {
+K10S_HD uint32_t heap_min_child(Ctx& c, uint32_t first, uint32_t n, int64_t& kmin, uint32_t& smin) {
 #if K10S_DEVICE
     const int lane = lane_id();
     uint32_t i = first + (uint32_t)(lane & (K10S_HEAP_D - 1));
     int64_t k = 0x7FFFFFFFFFFFFFFFll;
     uint32_t sq = 0xFFFFFFFFu;
     if (lane < K10S_HEAP_D && i < n) {
-        k = total_key(hp[i].time);
-        sq = hp[i].seq;
+        if (first < K10S_HEAP_TOP) {
+            k = total_key(k10s_hdr.heap_lds[i].time);
+            sq = k10s_hdr.heap_lds[i].seq;
+        } else {
+            const __amdgpu_buffer_rsrc_t rs = heap_rsrc(c);
+            auto lo = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * (uint32_t)sizeof(HeapEv)), 0, 0);
+            k = total_key(u2f(((uint64_t)lo[1] << 32) | lo[0]));
+            sq = lo[2];
+        }
     }
     static_assert(K10S_HEAP_D == 8, "the DPP reduction below covers 8-lane groups");
     keymin_step<0>(k, sq, i);
@@ -279,14 +342,16 @@ K10S_HD uint32_t heap_min_child(const HeapEv* hp, uint32_t first, uint32_t n, in
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
 #else
     uint32_t best = first;
-    int64_t kb = total_key(hp[first].time);
-    uint32_t sb = hp[first].seq;
+    HeapEv f = heap_get(c, first);
+    int64_t kb = total_key(f.time);
+    uint32_t sb = f.seq;
     uint32_t end = first + K10S_HEAP_D < n ? first + K10S_HEAP_D : n;
     for (uint32_t i = first + 1; i < end; i++) {
-        int64_t k = total_key(hp[i].time);
-        if (k < kb || (k == kb && hp[i].seq < sb)) {
+        HeapEv h = heap_get(c, i);
+        int64_t k = total_key(h.time);
+        if (k < kb || (k == kb && h.seq < sb)) {
             kb = k;
-            sb = hp[i].seq;
+            sb = h.seq;
             best = i;
         }
     }
@@ -297,11 +362,11 @@ K10S_HD uint32_t heap_min_child(const HeapEv* hp, uint32_t first, uint32_t n, in
 }
 
 K10S_HELPER void heap_pop(Ctx& c) {
-    HeapEv* hp = c.V().heap();
-    uint32_t n = c.H().heap_size - 1;
+    uint32_t n = uniform_u32(c.H().heap_size) - 1;
     c.H().heap_size = n;
     if (n == 0) return;
-    HeapEv last = hp[n];
+    HeapEv last = heap_get(c, n);
+    uniform_event(last);
     int64_t kl = total_key(last.time);
     uint32_t pos = 0;
     for (;;) {
@@ -309,14 +374,15 @@ K10S_HELPER void heap_pop(Ctx& c) {
         if (first >= n) break;
         int64_t km;
         uint32_t sm;
-        uint32_t m = heap_min_child(hp, first, n, km, sm);
+        uint32_t m = heap_min_child(c, first, n, km, sm);
         if (!(km < kl || (km == kl && sm < last.seq))) break;
-        HeapEv child = hp[m];
-        hp[pos] = child;
+        HeapEv child = heap_get(c, m);
+        uniform_event(child);
+        heap_put(c, pos, child);
         if (pos == 0) c.H().heap_top = child;
         pos = m;
     }
-    hp[pos] = last;
+    heap_put(c, pos, last);
     if (pos == 0) c.H().heap_top = last;
 }
 
@@ -1810,7 +1876,20 @@ K10S_HD int next_source(Ctx& c, uint32_t ntr) {
 #endif
 }
 
-// Remove the event next_source selected; a FIFO refills its cached head from its ring.
+// Refill a drained delay-class window from the HBM ring: positions [hd, hd + min(W, tail - hd)),
+// one 32-B entry per lane, so a burst of FIFO events costs one memory round trip per K10S_FQW pops.
+K10S_HD void fq_refill(Ctx& c, int cls, uint32_t hd) {
+    RepHdr& H = c.H();
+    const uint32_t cap = c.Ly().cap_fq;
+    const uint32_t avail = H.fq_tail[cls] - hd;
+    const uint32_t n = avail < K10S_FQW ? avail : K10S_FQW;
+    const HeapEv* ring = c.V().fq() + (uint32_t)cls * cap;
+    for (uint32_t i = (uint32_t)lane_id(); i < n; i += K10S_LANES)
+        H.fq_win[(uint32_t)cls * K10S_FQW + ((hd + i) & (K10S_FQW - 1))] = ring[(hd + i) & (cap - 1)];
+    H.fq_wend[cls] = hd + n;
+}
+
+// Remove the event next_source selected; a FIFO takes its next head from its window.
 K10S_HD void consume_source(Ctx& c, int src) {
     RepHdr& H = c.H();
     if (src == SRC_TRACE) {
@@ -1821,8 +1900,8 @@ K10S_HD void consume_source(Ctx& c, int src) {
         const uint32_t hd = H.fq_head[src] + 1;
         H.fq_head[src] = hd;
         if (hd != H.fq_tail[src]) {
-            const uint32_t cap = c.Ly().cap_fq;
-            H.fq_top[src] = c.V().fq()[(uint32_t)src * cap + (hd & (cap - 1))];
+            if (hd == H.fq_wend[src]) fq_refill(c, src, hd);
+            H.fq_top[src] = H.fq_win[(uint32_t)src * K10S_FQW + (hd & (K10S_FQW - 1))];
         }
     }
 }

@@ -136,6 +136,18 @@ struct HeapEv {             // dslab Event {id, time, dst, data}, 32 B
 // Delay-class FIFOs of the event queue (k10s_engine.h): events emitted with the same constant
 // delay are emitted in (time, id) order, so each class is an already-sorted run.
 #define K10S_NFQ 8
+// The head of every delay-class ring lives in the working header (LDS on the device): ring
+// positions [fq_head, fq_wend) are held in a K10S_FQW-entry window, the rest in the HBM ring, and a
+// drained window is refilled K10S_FQW entries at a time by one lane-parallel load.
+#ifndef K10S_FQW
+#define K10S_FQW 8
+#endif
+static_assert((K10S_FQW & (K10S_FQW - 1)) == 0 && K10S_FQW <= 64, "K10S_FQW: power of two <= 64");
+// The top levels of the 8-ary event heap (1 + 8 + 64 entries) live in the working header too; the
+// HBM heap array holds positions >= K10S_HEAP_TOP only.
+#ifndef K10S_HEAP_TOP
+#define K10S_HEAP_TOP 73
+#endif
 
 struct RepHdr {
     double clock;
@@ -167,9 +179,12 @@ struct RepHdr {
     // event queue: delay-class FIFO rings (head/tail counters, newest time, cached head entries)
     // and the cached root of the heap (valid while heap_size > 0)
     uint32_t fq_head[K10S_NFQ], fq_tail[K10S_NFQ];
+    uint32_t fq_wend[K10S_NFQ];   // the window holds ring positions [fq_head, fq_wend)
     double fq_last[K10S_NFQ];
     HeapEv fq_top[K10S_NFQ];
     HeapEv heap_top;
+    HeapEv fq_win[K10S_NFQ * K10S_FQW];
+    HeapEv heap_lds[K10S_HEAP_TOP];
     // cycle attribution of the event loop (K10S_PROF builds only, zero otherwise): K10S_PROF_*
     uint64_t prof[8];
 };

@@ -5,6 +5,7 @@
   wN     -DK10S_WAVES_PER_EU=N
   sN     -DK10S_SPLIT=N
   pN     -DK10S_SCAN_PIPE=N (scan loads N steps ahead)
+  qN     -DK10S_FQW=N (delay-class FIFO window entries in LDS)
 Usage: tools/variants.py prof w8 s1 ..."""
 import os
 import sys
@@ -22,6 +23,8 @@ def flags(name):
             out.append(f"-DK10S_WAVES_PER_EU={int(part[1:])}")
         elif part.startswith("p"):
             out.append(f"-DK10S_SCAN_PIPE={int(part[1:])}")
+        elif part.startswith("q"):
+            out.append(f"-DK10S_FQW={int(part[1:])}")
         elif part.startswith("s"):
             out.append(f"-DK10S_SPLIT={int(part[1:])}")
         else:
