@@ -557,7 +557,7 @@ K10S_HD double la_score(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr) {
 // Requires s_cpu / s_ram 16-B aligned and readable up to the next multiple of 4 nodes (engine
 // sections are 256-B padded; the unit surface's rows are node_stride (multiple of 64) long).
 #ifndef K10S_SCAN_PIPE
-#define K10S_SCAN_PIPE 2
+#define K10S_SCAN_PIPE 1
 #endif
 K10S_HD void scan_node(uint32_t n, uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr, double weight, int32_t& first,
                        uint64_t& best_key, int32_t& best_n) {
