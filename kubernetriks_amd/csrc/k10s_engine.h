@@ -258,25 +258,37 @@ K10S_HD void heap_put(Ctx& c, uint32_t i, const HeapEv& e) {
 K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uint32_t a, uint32_t b, double x,
                           int cls = FQ_HEAP) {
     RepHdr& H = c.H();
-    if (H.error_code) return 0;
-    if (H.next_seq == 0xFFFFFFFFu) {
+    // Everything emit reads from the header and the launch constants, as one batch ahead of every
+    // branch (the compiler may not hoist loads above the early returns): one LDS/scalar round trip
+    // instead of one per field.
+    const uint32_t err = H.error_code, seq = H.next_seq, hsize = H.heap_size;
+    const double clock = H.clock;
+    const uint32_t cap = c.Ly().cap_fq, cap_heap = c.Ly().cap_heap;
+    uint32_t hd = 0, tl = 0, we = 0;
+    double last = 0.0;
+    if (cls >= 0) {
+        hd = H.fq_head[cls];
+        tl = H.fq_tail[cls];
+        we = H.fq_wend[cls];
+        last = H.fq_last[cls];
+    }
+    if (err) return 0;
+    if (seq == 0xFFFFFFFFu) {
         fail(c, K10S_ERR_SEQ_OVERFLOW);
         return 0;
     }
     HeapEv e;
-    e.time = H.clock + delay;
-    e.seq = H.next_seq;
+    e.time = clock + delay;
+    e.seq = seq;
     e.kind = (uint16_t)kind;
     e.slot = (int16_t)slot;
     e.a = a;
     e.b = b;
     e.x = x;
     const int64_t k = total_key(e.time);
-    const uint32_t cap = c.Ly().cap_fq;
     if (cls >= 0 && cap) {
-        const uint32_t hd = H.fq_head[cls], tl = H.fq_tail[cls];
-        if (tl - hd < cap && (tl == hd || k >= total_key(H.fq_last[cls]))) {
-            if (H.fq_wend[cls] == tl && tl - hd < K10S_FQW) {  // the window holds the whole ring: append
+        if (tl - hd < cap && (tl == hd || k >= total_key(last))) {
+            if (we == tl && tl - hd < K10S_FQW) {  // the window holds the whole ring: append
                 H.fq_win[(uint32_t)cls * K10S_FQW + (tl & (K10S_FQW - 1))] = e;
                 H.fq_wend[cls] = tl + 1;
             } else {
@@ -289,12 +301,12 @@ K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uin
             return e.seq;
         }
     }
-    if (H.heap_size >= c.Ly().cap_heap) {
+    if (hsize >= cap_heap) {
         fail(c, K10S_ERR_HEAP_FULL);
         return 0;
     }
     H.next_seq = e.seq + 1;
-    uint32_t pos = uniform_u32(H.heap_size);
+    uint32_t pos = uniform_u32(hsize);
     H.heap_size = pos + 1;
     while (pos > 0) {
         uint32_t parent = (pos - 1) / K10S_HEAP_D;
@@ -557,7 +569,7 @@ K10S_HD double la_score(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr) {
 // Requires s_cpu / s_ram 16-B aligned and readable up to the next multiple of 4 nodes (engine
 // sections are 256-B padded; the unit surface's rows are node_stride (multiple of 64) long).
 #ifndef K10S_SCAN_PIPE
-#define K10S_SCAN_PIPE 1
+#define K10S_SCAN_PIPE 2
 #endif
 K10S_HD void scan_node(uint32_t n, uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr, double weight, int32_t& first,
                        uint64_t& best_key, int32_t& best_n) {
@@ -1685,6 +1697,14 @@ K10S_HD void dispatch(Ctx& c, const HeapEv& e) {
     else on_hpa(c, e);
 }
 
+// Cache the trace stream's head (time, id) in the working header.
+K10S_HD void trace_head_load(Ctx& c, uint32_t cur) {
+    if (cur < c.S().n_trace) {
+        c.H().tr_time = c.S().trace[cur].time;
+        c.H().tr_seq = c.S().trace[cur].seq;
+    }
+}
+
 // ---- initialize (simulator.rs:68-275 minus the trace emission, which is the shared stream) -----
 K10S_HD void perturb_pod(const Params& pr, uint32_t key, uint32_t& cpu, uint64_t& ram, double& dur) {
     uint64_t u = splitmix64(pr.seed ^ (0xD1B54A32D192ED03ull * ((uint64_t)key + 1)));
@@ -1802,6 +1822,7 @@ K10S_HD void init_replica(Ctx& c) {
     emit0(c, K10S_EV_S_FLUSH, 0.0);
     if (sc->ca_enabled) emit0(c, K10S_EV_CA_TICK, 0.0);
     if (sc->hpa_enabled) emit0(c, K10S_EV_HPA_TICK, 0.0);
+    trace_head_load(c, 0);
     h->status = K10S_REPLICA_RUNNING;
 }
 
@@ -1813,47 +1834,49 @@ enum : int { SRC_TRACE = K10S_NFQ, SRC_HEAP = K10S_NFQ + 1 };
 // trace head; a 4-step DPP min over the 16-lane row, broadcast from lane 0.
 K10S_HD int next_source(Ctx& c, uint32_t ntr) {
     const RepHdr& H = c.H();
-    const uint32_t cur = H.trace_cursor;
-    const bool ht = cur < ntr;
-    int64_t tkey = 0x7FFFFFFFFFFFFFFFll;
-    uint32_t tseq = 0xFFFFFFFFu;
-    if (ht) {
-        tkey = total_key(c.S().trace[cur].time);
-        tseq = c.S().trace[cur].seq;
-    }
 #if K10S_DEVICE
+    // every lane reads its candidate's fields in one batch of LDS reads (no branch in between), then
+    // masks invalid candidates: one LDS round trip per selection
     const int lane = lane_id() & 15;
-    int64_t k = 0x7FFFFFFFFFFFFFFFll;
+    const uint32_t li = lane < K10S_NFQ ? (uint32_t)lane : 0u;
+    const uint32_t qh = H.fq_head[li], qt = H.fq_tail[li], qseq = H.fq_top[li].seq;
+    const double qtime = H.fq_top[li].time;
+    const uint32_t hs = H.heap_size, hseq = H.heap_top.seq;
+    const double htime = H.heap_top.time;
+    const uint32_t cur = H.trace_cursor, tseq = H.tr_seq;
+    const double ttime = H.tr_time;
+    bool valid = false;
+    double t = 0.0;
     uint32_t sq = 0xFFFFFFFFu;
     int src = -1;
     if (lane < K10S_NFQ) {
-        if (H.fq_head[lane] != H.fq_tail[lane]) {
-            k = total_key(H.fq_top[lane].time);
-            sq = H.fq_top[lane].seq;
-            src = lane;
-        }
+        valid = qh != qt;
+        t = qtime;
+        sq = qseq;
+        src = lane;
     } else if (lane == SRC_HEAP) {
-        if (H.heap_size > 0) {
-            k = total_key(H.heap_top.time);
-            sq = H.heap_top.seq;
-            src = SRC_HEAP;
-        }
+        valid = hs > 0;
+        t = htime;
+        sq = hseq;
+        src = SRC_HEAP;
     } else if (lane == SRC_TRACE) {
-        if (ht) {
-            k = tkey;
-            sq = tseq;
-            src = SRC_TRACE;
-        }
+        valid = cur < ntr;
+        t = ttime;
+        sq = tseq;
+        src = SRC_TRACE;
     }
-    uint32_t us = (uint32_t)src;
+    int64_t k = valid ? total_key(t) : 0x7FFFFFFFFFFFFFFFll;
+    sq = valid ? sq : 0xFFFFFFFFu;
+    uint32_t us = valid ? (uint32_t)src : 0xFFFFFFFFu;
     keymin_step<0>(k, sq, us);
     keymin_step<1>(k, sq, us);
     keymin_step<2>(k, sq, us);
     keymin_step<3>(k, sq, us);
     return (int)__builtin_amdgcn_readfirstlane((int)us);
 #else
-    int64_t k = tkey;
-    uint32_t sq = tseq;
+    const bool ht = H.trace_cursor < ntr;
+    int64_t k = ht ? total_key(H.tr_time) : 0x7FFFFFFFFFFFFFFFll;
+    uint32_t sq = ht ? H.tr_seq : 0xFFFFFFFFu;
     int src = ht ? SRC_TRACE : -1;
     if (H.heap_size > 0) {
         int64_t hk = total_key(H.heap_top.time);
@@ -1893,7 +1916,9 @@ K10S_HD void fq_refill(Ctx& c, int cls, uint32_t hd) {
 K10S_HD void consume_source(Ctx& c, int src) {
     RepHdr& H = c.H();
     if (src == SRC_TRACE) {
-        H.trace_cursor += 1;
+        const uint32_t cur = H.trace_cursor + 1;
+        H.trace_cursor = cur;
+        trace_head_load(c, cur);
     } else if (src == SRC_HEAP) {
         heap_pop(c);
     } else {

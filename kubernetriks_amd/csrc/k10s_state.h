@@ -183,6 +183,8 @@ struct RepHdr {
     double fq_last[K10S_NFQ];
     HeapEv fq_top[K10S_NFQ];
     HeapEv heap_top;
+    double tr_time;               // cached head of the shared trace stream (valid while
+    uint32_t tr_seq, tr_pad;      // trace_cursor < n_trace)
     HeapEv fq_win[K10S_NFQ * K10S_FQW];
     HeapEv heap_lds[K10S_HEAP_TOP];
     // cycle attribution of the event loop (K10S_PROF builds only, zero otherwise): K10S_PROF_*
