@@ -189,6 +189,15 @@ class EngineBase:
         _, _, gn = self._names()
         return {gn[i]: (c[i], t[i]) for i in range(n.value)}
 
+    def step_for_duration(self, duration: float, max_events_per_launch: int = 0):
+        """KubernetriksSimulation::step_for_duration (simulator.rs:394-396) = dslab
+        step_until_time(time() + duration).  Every replica must be at the same clock (as after a
+        step_until_time); replicas run to completion have their own clocks and are rejected."""
+        clocks = {r.clock for r in self.raw_results()}
+        if len(clocks) != 1:
+            raise ValueError("step_for_duration needs every replica at the same clock")
+        return self.step_until_time(clocks.pop() + duration, max_events_per_launch)
+
     @property
     def replica_bytes(self) -> int:
         return int(self._fn["replica_bytes"](self._h))
