@@ -932,18 +932,41 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
     }
     case K10S_EV_S_POD_FINISHED: {
         uint32_t p = e.a, n = e.b;
-        if (!pod_in_s(c, p)) {
+        // one batch of loads: the pod's fields, the event node's flags, and the scheduler-cache entry
+        // of the event node (the pod's assigned node in every run so far; re-read if it is not)
+        PodState& P = c.V().pod(p);
+        const uint8_t pf = P.flags;
+        const int32_t sa = P.s_assigned;
+        const uint32_t rc = P.req_cpu;
+        const uint64_t rr = P.req_ram;
+        const uint8_t nf = c.V().node(n).flags;
+        const bool n_present = bit_test(c.V().s_present(), n);
+        const uint32_t n_cpu = c.V().s_cpu()[n];
+        const uint64_t n_ram = c.V().s_ram()[n];
+        if (!(pf & PF_IN_S)) {
             fail(c, K10S_PANIC_MISSING_POD);
             return;
         }
-        c.V().pod(p).flags &= (uint8_t)~PF_IN_S;
-        if (!(c.V().node(n).flags & NF_S_ASSIGN)) {
+        P.flags = (uint8_t)(pf & ~PF_IN_S);
+        if (!(nf & NF_S_ASSIGN)) {
             fail(c, K10S_PANIC_MISSING_ASSIGNMENTS);
             return;
         }
-        s_release(c, p);
-        if (c.H().error_code) return;
-        s_move_after_free(c, c.V().pod(p).req_cpu, c.V().pod(p).req_ram);
+        // release_node_resources (scheduler.rs:153-162) on the pod's assigned node
+        const bool present = sa == (int32_t)n ? n_present : (sa >= 0 && bit_test(c.V().s_present(), (uint32_t)sa));
+        if (sa < 0 || !present) {
+            fail(c, K10S_PANIC_MISSING_NODE);
+            return;
+        }
+        if (sa == (int32_t)n) {
+            c.V().s_cpu()[n] = n_cpu + rc;
+            c.V().s_ram()[n] = n_ram + rr;
+        } else {
+            c.V().s_cpu()[sa] += rc;
+            c.V().s_ram()[sa] += rr;
+        }
+        node_bound_changed(c, (uint32_t)sa);
+        s_move_after_free(c, rc, rr);
         break;
     }
     case K10S_EV_S_REMOVE_NODE: {
@@ -1143,12 +1166,19 @@ K10S_COLD void ca_decide(Ctx& c) {
 
 // ---- persistent storage (persistent_storage.rs:185-490) --------------------------------------
 K10S_HD void ps_clean_up(Ctx& c, uint32_t p) {  // 173-182
-    int32_t n = c.V().pod(p).ps_assigned;
+    PodState& P = c.V().pod(p);
+    const int32_t n = P.ps_assigned;
+    const uint32_t rc = P.req_cpu, pae = P.ps_aepoch;
+    const uint64_t rr = P.req_ram;
     if (n < 0) return;
-    if (c.V().node(n).flags & NF_PS_PRESENT) {
-        c.V().node(n).ps_cpu += c.V().pod(p).req_cpu;
-        c.V().node(n).ps_ram += c.V().pod(p).req_ram;
-        if (c.V().pod(p).ps_aepoch == c.V().node(n).ps_epoch) c.V().pod(p).ps_aepoch = 0;
+    NodeState& N = c.V().node(n);
+    const uint8_t nf = N.flags;  // one batch of loads from the node line
+    const uint32_t ncpu = N.ps_cpu, nep = N.ps_epoch;
+    const uint64_t nram = N.ps_ram;
+    if (nf & NF_PS_PRESENT) {
+        N.ps_cpu = ncpu + rc;
+        N.ps_ram = nram + rr;
+        if (pae == nep) P.ps_aepoch = 0;
     }
 }
 
@@ -1196,22 +1226,27 @@ K10S_WARM void on_ps(Ctx& c, HeapEv e) {
     }
     case K10S_EV_PS_ASSIGN_REQ: {
         uint32_t p = e.a, n = e.b;
-        if (!(c.V().pod(p).flags & PF_IN_PS)) {
+        PodState& P = c.V().pod(p);
+        NodeState& N = c.V().node(n);
+        const uint8_t pf = P.flags, nf = N.flags;  // one batch of loads (pod line, node line)
+        const uint32_t rc = P.req_cpu, ncpu = N.ps_cpu, nep = N.ps_epoch;
+        const uint64_t rr = P.req_ram, nram = N.ps_ram;
+        if (!(pf & PF_IN_PS)) {
             fail(c, K10S_PANIC_MISSING_POD);
             return;
         }
-        c.V().pod(p).ps_assigned = (int32_t)n;
-        if (c.V().pod(p).flags & PF_UNSCHED) {
-            c.V().pod(p).flags &= (uint8_t)~PF_UNSCHED;
+        P.ps_assigned = (int32_t)n;
+        if (pf & PF_UNSCHED) {
+            P.flags = (uint8_t)(pf & ~PF_UNSCHED);
             h->unsched_cache_count -= 1;
         }
-        if (!(c.V().node(n).flags & NF_PS_PRESENT)) {
+        if (!(nf & NF_PS_PRESENT)) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
         }
-        c.V().node(n).ps_cpu -= c.V().pod(p).req_cpu;
-        c.V().node(n).ps_ram -= c.V().pod(p).req_ram;
-        c.V().pod(p).ps_aepoch = c.V().node(n).ps_epoch;
+        N.ps_cpu = ncpu - rc;
+        N.ps_ram = nram - rr;
+        P.ps_aepoch = nep;
         emit(c, K10S_EV_AS_ASSIGN_RESP, pr->as_to_ps_network_delay, -1, p, n, 0.0, FQ_AS_TO_PS);
         break;
     }
@@ -1238,14 +1273,17 @@ K10S_WARM void on_ps(Ctx& c, HeapEv e) {
     }
     case K10S_EV_PS_POD_FINISHED: {
         uint32_t p = e.a;
-        if (c.V().pod(p).flags & PF_IN_PS) {
-            c.V().pod(p).flags &= (uint8_t)~PF_IN_PS;
+        PodState& P = c.V().pod(p);
+        const uint8_t pf = P.flags, sflags = c.S().pod_flags[p];  // one batch of loads
+        const double dur = P.dur;
+        if (pf & PF_IN_PS) {
+            P.flags = (uint8_t)(pf & ~PF_IN_PS);
             ps_clean_up(c, p);
-            if (!(c.S().pod_flags[p] & POD_HAS_DUR)) {
+            if (!(sflags & POD_HAS_DUR)) {
                 fail(c, K10S_PANIC_MISSING_POD);
                 return;
             }
-            est_add(h->est[K10S_EST_POD_DURATION], c.V().pod(p).dur);
+            est_add(h->est[K10S_EST_POD_DURATION], dur);
             if (c.V().prec()) {
                 c.V().prec()[p].t_finished = e.x;
                 c.V().prec()[p].state = 2;
@@ -1347,7 +1385,9 @@ K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
         break;
     case K10S_EV_AS_ASSIGN_REQ: {
         uint32_t n = e.b;
-        if (bit_test(c.V().pend_rm(), sc->node_uid[n]) || c.V().node(n).as_slot < 0) return;
+        const int32_t as_slot = c.V().node(n).as_slot;  // loaded with the removal bit, not after it
+        const bool pending = bit_test(c.V().pend_rm(), sc->node_uid[n]);
+        if (pending || as_slot < 0) return;
         emit(c, K10S_EV_PS_ASSIGN_REQ, pr->as_to_ps_network_delay, -1, e.a, n, e.x, FQ_AS_TO_PS);
         break;
     }
@@ -1471,26 +1511,37 @@ K10S_WARM void on_node(Ctx& c, HeapEv e) {
     switch (e.kind) {
     case K10S_EV_N_BIND: {
         uint32_t p = e.a, n = e.b;
-        if (c.V().slot(slot).removed) {
+        // one batch of loads: the component's slot line, the pod line and the pod's scenario flags
+        SlotState& SL = c.V().slot(slot);
+        PodState& P = c.V().pod(p);
+        const uint32_t removed = SL.removed;
+        const int32_t snode = SL.node, shead = SL.head;
+        const int32_t prs = P.run_slot;
+        const double dur = P.dur;
+        const uint8_t sflags = c.S().pod_flags[p];
+        const int32_t g = c.S().pod_group[p];
+        if (removed) {
             fail(c, K10S_PANIC_BIND_REMOVED_NODE);
             return;
         }
-        if (c.V().slot(slot).node != (int32_t)n) {
+        if (snode != (int32_t)n) {
             fail(c, K10S_PANIC_BIND_REMOVED_NODE);
             return;
         }
-        if (c.V().pod(p).run_slot >= 0) {  // a second concurrent bind of one pod: not modelled
+        if (prs >= 0) {  // a second concurrent bind of one pod: not modelled
             fail(c, K10S_PANIC_BIND_REMOVED_NODE);
             return;
         }
         uint32_t fseq = 0;
-        if (c.S().pod_flags[p] & POD_HAS_DUR) {  // simulate_pod_runtime (114-175)
-            double dur = c.V().pod(p).dur;
+        if (sflags & POD_HAS_DUR)  // simulate_pod_runtime (114-175)
             fseq = emit(c, K10S_EV_N_POD_FINISHED, dur + pr->as_to_node_network_delay, slot, p, n, e.time + dur);
-        }
-        run_insert(c, slot, p);
-        c.V().pod(p).finish_seq = fseq;
-        int32_t g = c.S().pod_group[p];
+        // run_insert with the head loaded above (emit touches only the event queue)
+        P.run_prev = -1;
+        P.run_next = shead;
+        if (shead >= 0) c.V().pod(shead).run_prev = (int32_t)p;
+        SL.head = (int32_t)p;
+        P.run_slot = slot;
+        P.finish_seq = fseq;
         if (g >= 0) c.V().grp()[g].running += 1;
         emit(c, K10S_EV_AS_POD_STARTED, pr->as_to_node_network_delay, -1, p, 0, e.time, FQ_AS_TO_NODE);
         break;
