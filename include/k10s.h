@@ -188,6 +188,19 @@ int32_t k10s_schedule_one_batch(const uint32_t* alloc_cpu, const uint64_t* alloc
                                 uint32_t n_problems, int32_t* out_node, int32_t* out_status,
                                 void* stream);
 
+/* (1b) -------------------------------------------------------------------------------------
+ * ScorePlugin surface: replaces `ScorePlugin::score(&self, pod: &Pod, node: &Node) -> f64`
+ * (src/core/scheduler/plugin.rs:25-31) for LeastAllocatedResources (plugin.rs:52-63), applied
+ * the way KubeScheduler accumulates it (0.0 + score * weight, kube_scheduler.rs:113-138), for n
+ * independent (node allocatable, pod request) pairs.  Element i: out_score[i] = 0.0 +
+ * LeastAllocated(alloc_cpu[i], alloc_ram[i], req_cpu[i], req_ram[i]) * weight, bit-identical to
+ * the values k10s_schedule_one_batch and the engine compare (NaN for a 0/0 resource term).
+ * Callers guarantee req <= alloc per element (the Fit filter ran first, as in the reference).
+ * All pointers are DEVICE pointers.  Returns K10S_OK or a negative K10S_E_* code. */
+int32_t k10s_score_batch(const uint32_t* alloc_cpu, const uint64_t* alloc_ram, const uint32_t* req_cpu,
+                         const uint64_t* req_ram, double weight, uint64_t n, double* out_score,
+                         void* stream);
+
 /* (1') Host-buffer form of (1) for hosts without HIP bindings (the Rust PodSchedulingAlgorithm
  * adapter in INTEGRATION.md): a handle owns device buffers for up to max_problems problems of up
  * to max_nodes nodes.  k10s_scheduler_schedule takes HOST arrays — problem r's nodes are

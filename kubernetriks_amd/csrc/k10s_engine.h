@@ -608,13 +608,79 @@ K10S_D ScanGrp scan_load(const uint32_t* s_cpu, const uint64_t* s_ram, const uin
     }
     return g;
 }
+// Device form of la_score's two quotients: the same operations the compiler emits for an IEEE f64
+// division (v_rcp_f64, two Newton steps, q = x·r, one remainder correction), minus the
+// v_div_scale / v_div_fixup pair.  Those only change anything when an operand is 0, inf/NaN, near
+// the denormal range or 2^±768 apart; here x = 100·(a − r) and y = a are integers in [0, 2^71) with
+// x/y in [0, 100], so scale is the identity (and div_fmas a plain fma), and the result is bit-for-
+// bit the correctly rounded quotient.  The one special case that occurs, 0/0 (a == r == 0), gives
+// NaN through rcp(0) = inf, as the IEEE division does (plugin.rs:52-63).
+K10S_D double div_rn(double x, double y) {
+    double r = __builtin_amdgcn_rcp(y);
+    double e = __builtin_fma(-y, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-y, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    const double q = x * r;
+    const double rem = __builtin_fma(-y, q, x);
+    return __builtin_fma(rem, r, q);
+}
+// u64 -> f64 with one rounding (hi·2^32 is exact; the fma rounds hi·2^32 + lo once), = Rust `as f64`.
+// (The high word's u32 -> f64 is written as the instruction itself: as C the compiler re-forms the
+// u64 conversion and adds a dead 0·2^32 term.)
+K10S_D double u64_f64(uint64_t v) {
+    const uint2 w = __builtin_bit_cast(uint2, v);
+    double hi;
+    asm("v_cvt_f64_u32 %0, %1" : "=v"(hi) : "v"(w.y));
+    return __builtin_fma(hi, 4294967296.0, (double)w.x);
+}
+// la_score on the device (plugin.rs:52-63), bit-identical to la_score.  Also the elementwise
+// ScorePlugin surface k10s_score_batch.
+K10S_D double la_score_d(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr) {
+    const double cs = div_rn((double)(ac - rc) * 100.0, (double)ac);
+    const double rs = div_rn(u64_f64(ar - rr) * 100.0, u64_f64(ar));
+    return (cs + rs) * 0.5;  // (c + r) / 2.0, exact halving
+}
+// scan_node on the device: the score stays a double and the lane max is an f64 compare.  The
+// score is never -0.0 (a +0 quotient sum, or 0.0 + s·w), so for non-NaN scores ">=" on doubles is
+// the score_key order, NaN never compares true (= "NaN is never selected"), and -inf as the start
+// value accepts the first non-NaN score like score_key's 0.  W1: weight == 1.0, where 0.0 + s·1.0
+// is the identity on scores >= +0 and NaN.
+template <bool W1>
+K10S_D void scan_node_d(uint32_t n, uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr, double weight,
+                        int32_t& first, double& best_s, int32_t& best_n) {
+    if (rc <= ac && rr <= ar) {
+        first = (int32_t)n < first ? (int32_t)n : first;
+        double s = la_score_d(ac, ar, rc, rr);
+        if (!W1) s = 0.0 + s * weight;
+        if (s >= best_s) {
+            best_s = s;
+            best_n = (int32_t)n;
+        }
+    }
+}
+template <bool W1>
 K10S_D void scan_grp(const ScanGrp& g, uint32_t n0, uint32_t rc, uint64_t rr, double weight, int32_t& first,
-                     uint64_t& best_key, int32_t& best_n) {
+                     double& best_s, int32_t& best_n) {
     if (g.bits) {
-        if (g.bits & 1u) scan_node(n0, g.cv.x, g.r01.x, rc, rr, weight, first, best_key, best_n);
-        if (g.bits & 2u) scan_node(n0 + 1, g.cv.y, g.r01.y, rc, rr, weight, first, best_key, best_n);
-        if (g.bits & 4u) scan_node(n0 + 2, g.cv.z, g.r23.x, rc, rr, weight, first, best_key, best_n);
-        if (g.bits & 8u) scan_node(n0 + 3, g.cv.w, g.r23.y, rc, rr, weight, first, best_key, best_n);
+        if (g.bits & 1u) scan_node_d<W1>(n0, g.cv.x, g.r01.x, rc, rr, weight, first, best_s, best_n);
+        if (g.bits & 2u) scan_node_d<W1>(n0 + 1, g.cv.y, g.r01.y, rc, rr, weight, first, best_s, best_n);
+        if (g.bits & 4u) scan_node_d<W1>(n0 + 2, g.cv.z, g.r23.x, rc, rr, weight, first, best_s, best_n);
+        if (g.bits & 8u) scan_node_d<W1>(n0 + 3, g.cv.w, g.r23.y, rc, rr, weight, first, best_s, best_n);
+    }
+}
+template <bool W1>
+K10S_D void scan_lanes(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
+                       uint32_t rc, uint64_t rr, double weight, int32_t& first, double& best_s, int32_t& best_n) {
+    const uint32_t l4 = 4u * (uint32_t)lane_id();
+    ScanGrp g[K10S_SCAN_PIPE + 1];
+#pragma unroll
+    for (int i = 0; i < K10S_SCAN_PIPE; i++) g[i] = scan_load(s_cpu, s_ram, present, n_nodes, 256u * i + l4);
+    for (uint32_t base = 0; base < n_nodes; base += 256) {
+        g[K10S_SCAN_PIPE] = scan_load(s_cpu, s_ram, present, n_nodes, base + 256u * K10S_SCAN_PIPE + l4);
+        scan_grp<W1>(g[0], base + l4, rc, rr, weight, first, best_s, best_n);
+#pragma unroll
+        for (int i = 0; i < K10S_SCAN_PIPE; i++) g[i] = g[i + 1];
     }
 }
 #endif
@@ -625,16 +691,10 @@ K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const ui
     int32_t best_n = -1;
     int32_t first = 0x7fffffff;
 #if K10S_DEVICE
-    const uint32_t l4 = 4u * (uint32_t)lane_id();
-    ScanGrp g[K10S_SCAN_PIPE + 1];
-#pragma unroll
-    for (int i = 0; i < K10S_SCAN_PIPE; i++) g[i] = scan_load(s_cpu, s_ram, present, n_nodes, 256u * i + l4);
-    for (uint32_t base = 0; base < n_nodes; base += 256) {
-        g[K10S_SCAN_PIPE] = scan_load(s_cpu, s_ram, present, n_nodes, base + 256u * K10S_SCAN_PIPE + l4);
-        scan_grp(g[0], base + l4, rc, rr, weight, first, best_key, best_n);
-#pragma unroll
-        for (int i = 0; i < K10S_SCAN_PIPE; i++) g[i] = g[i + 1];
-    }
+    double best_s = -__builtin_inf();
+    if (weight == 1.0) scan_lanes<true>(s_cpu, s_ram, present, n_nodes, rc, rr, weight, first, best_s, best_n);
+    else scan_lanes<false>(s_cpu, s_ram, present, n_nodes, rc, rr, weight, first, best_s, best_n);
+    best_key = best_n >= 0 ? score_key(best_s) : 0;
 #else
     for (uint32_t n = 0; n < n_nodes; n++)
         if ((present[n >> 6] >> (n & 63)) & 1ull) scan_node(n, s_cpu[n], s_ram[n], rc, rr, weight, first, best_key, best_n);

@@ -22,6 +22,8 @@ hipError_t k10s_launch_schedule(const uint32_t* alloc_cpu, const uint64_t* alloc
                                 uint32_t n_nodes, uint32_t node_stride, const uint32_t* req_cpu, const uint64_t* req_ram,
                                 double weight, uint32_t n_problems, int32_t* out_node, int32_t* out_status,
                                 hipStream_t s);
+hipError_t k10s_launch_score(const uint32_t* alloc_cpu, const uint64_t* alloc_ram, const uint32_t* req_cpu,
+                             const uint64_t* req_ram, double weight, uint64_t n, double* out, hipStream_t s);
 
 namespace {
 thread_local std::string g_err;
@@ -107,6 +109,16 @@ int32_t k10s_schedule_one_batch(const uint32_t* alloc_cpu, const uint64_t* alloc
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return set_err(K10S_E_NO_DEVICE, "no HIP device");
     HIPCHK(k10s_launch_schedule(alloc_cpu, alloc_ram, present_bits, n_nodes, node_stride, req_cpu, req_ram, weight,
                                 n_problems, out_node, out_status, (hipStream_t)stream));
+    return K10S_OK;
+}
+
+int32_t k10s_score_batch(const uint32_t* alloc_cpu, const uint64_t* alloc_ram, const uint32_t* req_cpu,
+                         const uint64_t* req_ram, double weight, uint64_t n, double* out_score, void* stream) {
+    if (n == 0) return K10S_OK;
+    if (!alloc_cpu || !alloc_ram || !req_cpu || !req_ram || !out_score) return set_err(K10S_E_INVALID, "null pointer");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return set_err(K10S_E_NO_DEVICE, "no HIP device");
+    HIPCHK(k10s_launch_score(alloc_cpu, alloc_ram, req_cpu, req_ram, weight, n, out_score, (hipStream_t)stream));
     return K10S_OK;
 }
 

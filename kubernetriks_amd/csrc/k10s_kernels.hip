@@ -91,6 +91,19 @@ __global__ __launch_bounds__(64) void k10s_schedule_kernel(const uint32_t* __res
     }
 }
 
+// ScorePlugin surface: out[i] = 0.0 + LeastAllocated(alloc[i], req[i]) * weight, the scheduler's
+// per-plugin accumulation (kube_scheduler.rs:113-138) for one (pod, node) pair per element.
+__global__ __launch_bounds__(256) void k10s_score_kernel(const uint32_t* __restrict__ alloc_cpu,
+                                                         const uint64_t* __restrict__ alloc_ram,
+                                                         const uint32_t* __restrict__ req_cpu,
+                                                         const uint64_t* __restrict__ req_ram, double weight,
+                                                         uint64_t n, double* __restrict__ out) {
+#if K10S_DEVICE
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = 0.0 + la_score_d(alloc_cpu[i], alloc_ram[i], req_cpu[i], req_ram[i]) * weight;
+#endif
+}
+
 // ---- launchers (called from k10s_host.cpp) -------------------------------------------------------
 // The launch constants live in the one __constant__ block k10s_dc, so every engine launch first
 // copies its block (from pinned host memory, stream-ordered) and then launches; engines of a device
@@ -125,5 +138,13 @@ hipError_t k10s_launch_schedule(const uint32_t* alloc_cpu, const uint64_t* alloc
                                 hipStream_t s) {
     hipLaunchKernelGGL(k10s_schedule_kernel, dim3(n_problems), dim3(64), 0, s, alloc_cpu, alloc_ram, present, n_nodes,
                        node_stride, req_cpu, req_ram, weight, n_problems, out_node, out_status);
+    return hipGetLastError();
+}
+
+hipError_t k10s_launch_score(const uint32_t* alloc_cpu, const uint64_t* alloc_ram, const uint32_t* req_cpu,
+                             const uint64_t* req_ram, double weight, uint64_t n, double* out, hipStream_t s) {
+    const uint64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(k10s_score_kernel, dim3((uint32_t)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, s, alloc_cpu,
+                       alloc_ram, req_cpu, req_ram, weight, n, out);
     return hipGetLastError();
 }

@@ -245,6 +245,9 @@ def lib():
         L.k10s_schedule_one_batch.restype = ctypes.c_int32
         L.k10s_schedule_one_batch.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint32, ctypes.c_uint32] + \
             [ctypes.c_void_p] * 2 + [ctypes.c_double, ctypes.c_uint32] + [ctypes.c_void_p] * 3
+        L.k10s_score_batch.restype = ctypes.c_int32
+        L.k10s_score_batch.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_double, ctypes.c_uint64] + \
+            [ctypes.c_void_p] * 2
         L.k10s_scheduler_create.restype = ctypes.c_void_p
         L.k10s_scheduler_create.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int32]
         L.k10s_scheduler_destroy.argtypes = [ctypes.c_void_p]
