@@ -258,6 +258,10 @@ K10S_HD uint32_t uniform_u32(uint32_t v) {
     return v;
 #endif
 }
+K10S_HD uint64_t uniform_u64(uint64_t v) {
+    return (uint64_t)uniform_u32((uint32_t)v) | ((uint64_t)uniform_u32((uint32_t)(v >> 32)) << 32);
+}
+K10S_HD double uniform_f64(double v) { return u2f(uniform_u64(f2u(v))); }
 K10S_HD void wave_sync() {
 #if K10S_DEVICE
     __syncthreads();  // one wavefront per workgroup: orders cross-lane global writes (cheap)

@@ -569,7 +569,12 @@ K10S_HD double la_score(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr) {
 // Requires s_cpu / s_ram 16-B aligned and readable up to the next multiple of 4 nodes (engine
 // sections are 256-B padded; the unit surface's rows are node_stride (multiple of 64) long).
 #ifndef K10S_SCAN_PIPE
-#define K10S_SCAN_PIPE 2
+#define K10S_SCAN_PIPE 1
+#endif
+// K10S_SCAN_BF: 1 evaluates every node's score and selects (no exec-mask branches), 0 branches
+// on Fit per node.  Semantics-neutral tuning knob.
+#ifndef K10S_SCAN_BF
+#define K10S_SCAN_BF 0
 #endif
 K10S_HD void scan_node(uint32_t n, uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr, double weight, int32_t& first,
                        uint64_t& best_key, int32_t& best_n) {
@@ -587,26 +592,27 @@ K10S_HD void scan_node(uint32_t n, uint32_t ac, uint64_t ar, uint32_t rc, uint64
 }
 
 #if K10S_DEVICE
-struct ScanGrp {            // one lane's 4 consecutive nodes of a 256-node step
-    uint32_t bits;          // present & < n_nodes
+struct ScanGrp {            // one lane's 4 consecutive nodes of a 256-node step, as loaded
+    uint64_t pw;            // the presence word holding them
     uint4 cv;
     ulonglong2 r01, r23;
 };
+// Unconditional loads: a lane past the end re-reads nodes 0..3 (n_nodes >= 1; valid and cached) and grp_bits() masks it out, so no branch and no zero fill sits
+// between the load and its use.
 K10S_D ScanGrp scan_load(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
                          uint32_t n0) {
+    const uint32_t a = n0 < n_nodes ? n0 : 0u;
     ScanGrp g;
-    g.bits = 0;
-    g.cv = make_uint4(0, 0, 0, 0);
-    g.r01 = make_ulonglong2(0, 0);
-    g.r23 = make_ulonglong2(0, 0);
-    if (n0 < n_nodes) {
-        const uint32_t valid = n_nodes - n0;
-        g.bits = (uint32_t)(present[n0 >> 6] >> (n0 & 63)) & (valid >= 4 ? 0xFu : ((1u << valid) - 1u));
-        g.cv = *reinterpret_cast<const uint4*>(s_cpu + n0);
-        g.r01 = *reinterpret_cast<const ulonglong2*>(s_ram + n0);
-        g.r23 = *reinterpret_cast<const ulonglong2*>(s_ram + n0 + 2);
-    }
+    g.pw = present[a >> 6];
+    g.cv = *reinterpret_cast<const uint4*>(s_cpu + a);
+    g.r01 = *reinterpret_cast<const ulonglong2*>(s_ram + a);
+    g.r23 = *reinterpret_cast<const ulonglong2*>(s_ram + a + 2);
     return g;
+}
+K10S_D uint32_t grp_bits(const ScanGrp& g, uint32_t n0, uint32_t n_nodes) {
+    if (n0 >= n_nodes) return 0;
+    const uint32_t valid = n_nodes - n0;
+    return (uint32_t)(g.pw >> (n0 & 63)) & (valid >= 4 ? 0xFu : ((1u << valid) - 1u));
 }
 // Device form of la_score's two quotients: the same operations the compiler emits for an IEEE f64
 // division (v_rcp_f64, two Newton steps, q = x·r, one remainder correction), minus the
@@ -647,38 +653,70 @@ K10S_D double la_score_d(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr) {
 // value accepts the first non-NaN score like score_key's 0.  W1: weight == 1.0, where 0.0 + s·1.0
 // is the identity on scores >= +0 and NaN.
 template <bool W1>
-K10S_D void scan_node_d(uint32_t n, uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr, double weight,
-                        int32_t& first, double& best_s, int32_t& best_n) {
-    if (rc <= ac && rr <= ar) {
+K10S_D void scan_node_d(uint32_t n, bool present, uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr, double frc,
+                        double frr, double weight, int32_t& first, double& best_s, int32_t& best_n) {
+#if K10S_SCAN_BF
+    // Branch-free: the score is evaluated for every node of the group and kept only if the node
+    // is present and fits (the wave runs all four nodes anyway unless every lane skips one).
+    const bool fit = present && rc <= ac && rr <= ar;
+    const double fac = (double)ac;
+    const double cs = div_rn((fac - frc) * 100.0, fac);  // = (double)(ac - rc): u32 values are exact
+    const uint2 w = __builtin_bit_cast(uint2, ar);
+    const double far = u64_f64(ar);
+    // (ar - rr) as f64: far - frr is exact while ar < 2^53 (then rr <= ar is exact too)
+    double dr = far - frr;
+    if (__builtin_expect(w.y >= (1u << 21), 0)) dr = u64_f64(ar - rr);
+    double s = (cs + div_rn(dr * 100.0, far)) * 0.5;
+    if (!W1) s = 0.0 + s * weight;
+    first = (fit && (int32_t)n < first) ? (int32_t)n : first;
+    const bool take = fit && s >= best_s;
+    best_s = take ? s : best_s;
+    best_n = take ? (int32_t)n : best_n;
+#else
+    if (rc <= ac && rr <= ar && present) {
         first = (int32_t)n < first ? (int32_t)n : first;
-        double s = la_score_d(ac, ar, rc, rr);
+        const double fac = (double)ac;
+        const double cs = div_rn((fac - frc) * 100.0, fac);
+        const uint2 w = __builtin_bit_cast(uint2, ar);
+        const double far = u64_f64(ar);
+        double dr = far - frr;
+        if (__builtin_expect(w.y >= (1u << 21), 0)) dr = u64_f64(ar - rr);
+        double s = (cs + div_rn(dr * 100.0, far)) * 0.5;
         if (!W1) s = 0.0 + s * weight;
         if (s >= best_s) {
             best_s = s;
             best_n = (int32_t)n;
         }
     }
+#endif
 }
 template <bool W1>
-K10S_D void scan_grp(const ScanGrp& g, uint32_t n0, uint32_t rc, uint64_t rr, double weight, int32_t& first,
-                     double& best_s, int32_t& best_n) {
-    if (g.bits) {
-        if (g.bits & 1u) scan_node_d<W1>(n0, g.cv.x, g.r01.x, rc, rr, weight, first, best_s, best_n);
-        if (g.bits & 2u) scan_node_d<W1>(n0 + 1, g.cv.y, g.r01.y, rc, rr, weight, first, best_s, best_n);
-        if (g.bits & 4u) scan_node_d<W1>(n0 + 2, g.cv.z, g.r23.x, rc, rr, weight, first, best_s, best_n);
-        if (g.bits & 8u) scan_node_d<W1>(n0 + 3, g.cv.w, g.r23.y, rc, rr, weight, first, best_s, best_n);
+K10S_D void scan_grp(const ScanGrp& g, uint32_t n0, uint32_t n_nodes, uint32_t rc, uint64_t rr, double frc,
+                     double frr, double weight, int32_t& first, double& best_s, int32_t& best_n) {
+    const uint32_t bits = grp_bits(g, n0, n_nodes);
+    if (bits) {
+        scan_node_d<W1>(n0, bits & 1u, g.cv.x, g.r01.x, rc, rr, frc, frr, weight, first, best_s, best_n);
+        scan_node_d<W1>(n0 + 1, bits & 2u, g.cv.y, g.r01.y, rc, rr, frc, frr, weight, first, best_s, best_n);
+        scan_node_d<W1>(n0 + 2, bits & 4u, g.cv.z, g.r23.x, rc, rr, frc, frr, weight, first, best_s, best_n);
+        scan_node_d<W1>(n0 + 3, bits & 8u, g.cv.w, g.r23.y, rc, rr, frc, frr, weight, first, best_s, best_n);
     }
 }
 template <bool W1>
 K10S_D void scan_lanes(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
                        uint32_t rc, uint64_t rr, double weight, int32_t& first, double& best_s, int32_t& best_n) {
     const uint32_t l4 = 4u * (uint32_t)lane_id();
+    // the pod's request is wave-uniform: keep it (and its f64 forms) in SGPRs, out of the VGPR budget
+    rc = uniform_u32(rc);
+    rr = uniform_u64(rr);
+    const double frc = uniform_f64((double)rc), frr = uniform_f64(u64_f64(rr));
+    if (n_nodes == 0) return;
+    // Software pipeline: loads run K10S_SCAN_PIPE steps (of 256 nodes) ahead of the arithmetic.
     ScanGrp g[K10S_SCAN_PIPE + 1];
 #pragma unroll
     for (int i = 0; i < K10S_SCAN_PIPE; i++) g[i] = scan_load(s_cpu, s_ram, present, n_nodes, 256u * i + l4);
     for (uint32_t base = 0; base < n_nodes; base += 256) {
         g[K10S_SCAN_PIPE] = scan_load(s_cpu, s_ram, present, n_nodes, base + 256u * K10S_SCAN_PIPE + l4);
-        scan_grp<W1>(g[0], base + l4, rc, rr, weight, first, best_s, best_n);
+        scan_grp<W1>(g[0], base + l4, n_nodes, rc, rr, frc, frr, weight, first, best_s, best_n);
 #pragma unroll
         for (int i = 0; i < K10S_SCAN_PIPE; i++) g[i] = g[i + 1];
     }

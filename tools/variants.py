@@ -6,6 +6,7 @@
   sN     -DK10S_SPLIT=N
   pN     -DK10S_SCAN_PIPE=N (scan loads N steps ahead)
   qN     -DK10S_FQW=N (delay-class FIFO window entries in LDS)
+  bfN    -DK10S_SCAN_BF=N (branch-free node scan)
 Usage: tools/variants.py prof w8 s1 ..."""
 import os
 import sys
@@ -25,6 +26,8 @@ def flags(name):
             out.append(f"-DK10S_SCAN_PIPE={int(part[1:])}")
         elif part.startswith("q"):
             out.append(f"-DK10S_FQW={int(part[1:])}")
+        elif part.startswith("bf"):
+            out.append(f"-DK10S_SCAN_BF={int(part[2:])}")
         elif part.startswith("s"):
             out.append(f"-DK10S_SPLIT={int(part[1:])}")
         else:
