@@ -101,10 +101,17 @@ enum k10s_counter {
     K10S_NUM_COUNTERS
 };
 
-/* `average` 0.15 Min/Max/Mean/Variance estimator state (collector.rs:15-74) */
+/* Fixed log2 bins of every value an estimator sees (engine addition; the reference keeps only
+   the four estimators).  Bin 0: x < 2^-10 s (also 0, negatives, NaN); bin k in 1..30:
+   2^(k-11) <= x < 2^(k-10); bin 31: x >= 2^20 s.  The bin is read off the f64 exponent, so it is
+   exact and identical on the host restatement.  Summed over replicas and over ranks (RCCL). */
+#define K10S_HIST_BINS 32
+
+/* `average` 0.15 Min/Max/Mean/Variance estimator state (collector.rs:15-74) + histogram */
 typedef struct k10s_estimator {
     uint64_t n;
     double min, max, mean, sum2; /* population variance = sum2 / n */
+    uint32_t hist[K10S_HIST_BINS];
 } k10s_estimator;
 
 #define K10S_EST_POD_DURATION 0

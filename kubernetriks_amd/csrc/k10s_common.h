@@ -93,6 +93,13 @@ K10S_HD uint64_t score_key(double x) {
     return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
 }
 
+// Histogram bin of an estimator value (K10S_HIST_BINS log2 bins, include/k10s.h).
+K10S_HD uint32_t hist_bin(double x) {
+    if (!(x >= 0.0009765625)) return 0;  // < 2^-10, NaN
+    const int32_t e = (int32_t)((f2u(x) >> 52) & 0x7FF) - 1023;
+    return e >= 20 ? 31u : (uint32_t)(e + 11);
+}
+
 // Rust `as` casts
 K10S_HD uint64_t f64_as_u64(double x) {
     if (is_nan(x) || x <= 0.0) return 0;

@@ -22,6 +22,7 @@ inline void hdr_to_result(const RepHdr& h, k10s_replica_result& r) {
         r.est[i].max = h.est[i].mx;
         r.est[i].mean = h.est[i].n ? h.est[i].avg : __builtin_nan("");
         r.est[i].sum2 = h.est[i].sum2;
+        for (int b = 0; b < K10S_HIST_BINS; b++) r.est[i].hist[b] = h.est[i].hist[b];
     }
     r.unschedulable_len = h.uq_size;
     r.active_len = h.aq_size;

@@ -102,9 +102,10 @@ struct Scenario {
 // Replica parameters as consumed by the device (k10s_replica_params with derived fields).
 typedef k10s_replica_params Params;
 
-struct Estimator {          // `average` 0.15 concatenate!(Min, Max, Mean, Variance)
+struct Estimator {          // `average` 0.15 concatenate!(Min, Max, Mean, Variance) + log2 bins
     uint64_t n;
     double mn, mx, avg, sum2;
+    uint32_t hist[K10S_HIST_BINS];
 };
 K10S_HD void est_reset(Estimator& e) {
     e.n = 0;
@@ -112,8 +113,10 @@ K10S_HD void est_reset(Estimator& e) {
     e.mx = -__builtin_inf();
     e.avg = 0.0;
     e.sum2 = 0.0;
+    for (int i = 0; i < K10S_HIST_BINS; i++) e.hist[i] = 0;
 }
 K10S_HELPER void est_add(Estimator& e, double x) {
+    e.hist[hist_bin(x)] += 1;
     e.mn = fmin_rs(e.mn, x);
     e.mx = fmax_rs(e.mx, x);
     e.n += 1;

@@ -7,6 +7,9 @@ group is "nccl", gloo on CPU):
   * the per-replica counter rows and estimator rows, all-gathered in rank order (R rows per rank),
     so that metrics.EnsembleSummary merges them in global replica order — the summary of the job
     is bit-identical for any world size;
+  * the log2 histograms of pod duration / scheduling latency / queue time (K10S_HIST_BINS bins per
+    estimator), summed over the rank's replicas and then all-reduced (SUM) — the RCCL all-reduce of
+    metric histograms;
   * scalar timings, max-reduced (`max_over_ranks`).
 The reference is single-process (no collective exists there); this is the ensemble layer around it.
 """
@@ -16,7 +19,7 @@ from typing import Optional, Sequence
 
 from . import workloads as wl
 from .metrics import EnsembleSummary, estimator_rows
-from .native import COUNTER_NAMES, EST_NAMES, NUM_COUNTERS, STATUS
+from .native import COUNTER_NAMES, EST_NAMES, HIST_BINS, NUM_COUNTERS, STATUS
 
 
 def replica_offset(rank: int, replicas_per_rank: int) -> int:
@@ -67,12 +70,34 @@ def ensemble_summary(raw_results: Sequence, group=None) -> EnsembleSummary:
     """Summary of every replica of the job (all ranks when torch.distributed is initialised; every
     rank must pass the same number of replicas).  Identical on every rank."""
     cnt, est, st = _rows(raw_results)
+    hist = histogram_sum(raw_results)
     if _dist_group_size(group) > 1:
         cnt, est, st = _gather(cnt, group), _gather(est, group), _gather(st, group)
+        hist = _all_reduce_sum(hist, group)
     s = EnsembleSummary(COUNTER_NAMES, EST_NAMES)
     for i in range(cnt.shape[0]):
         s.add_replica(cnt[i].tolist(), est[i].tolist(), STATUS.get(int(st[i]), str(int(st[i]))))
+    s.set_histograms(hist)
     return s
+
+
+def histogram_sum(raw_results):
+    """(len(EST_NAMES), HIST_BINS) int64: the replicas' estimator histograms summed."""
+    import numpy as np
+    h = np.zeros((len(EST_NAMES), HIST_BINS), dtype=np.int64)
+    for r in raw_results:
+        h += np.array([list(r.est[i].hist) for i in range(len(EST_NAMES))], dtype=np.int64)
+    return h
+
+
+def _all_reduce_sum(arr, group=None):
+    """Element-wise SUM of an int64 array over the group (RCCL over xGMI for "nccl", gloo on CPU)."""
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    t = torch.from_numpy(arr.copy()).to(dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t.cpu().numpy()
 
 
 def max_over_ranks(values: Sequence[float], group=None, device: Optional[str] = None):

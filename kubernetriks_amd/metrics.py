@@ -101,7 +101,7 @@ def serde_json_f64(x: float) -> str:
 
 # ---- printer.rs restatements ----------------------------------------------------------------------
 def _timing_values(result: dict, est_name: str):
-    _, mn, mx, mean, var = result["estimators"][est_name]
+    _, mn, mx, mean, var = result["estimators"][est_name][:5]
     return mn, mx, mean, var
 
 
@@ -175,6 +175,7 @@ class EnsembleSummary:
         self.est = {k: [0, math.inf, -math.inf, 0.0, 0.0] for k in self.est_names}
         self.replicas = 0
         self.status: Dict[str, int] = {}
+        self.hist = None  # {est name: [counts per log2 bin]} once set_histograms() ran
 
     def add_replica(self, counters: Sequence[int], est_rows: Sequence[Sequence[float]], status: str = "finished"):
         for i, v in enumerate(counters):
@@ -202,6 +203,10 @@ class EnsembleSummary:
         a[1] = min(a[1], mnb)
         a[2] = max(a[2], mxb)
 
+    def set_histograms(self, hist):
+        """hist: rows of K10S_HIST_BINS counts per estimator (summed over the job's replicas)."""
+        self.hist = {k: [int(v) for v in row] for k, row in zip(self.est_names, hist)}
+
     def as_dict(self) -> dict:
         out = {"replicas": self.replicas, "replica_status": dict(self.status),
                "counters": {k: v for k, v in zip(self.counter_names, self.counters)}, "timings": {}}
@@ -209,6 +214,9 @@ class EnsembleSummary:
             n, mn, mx, mean, m2 = self.est[k]
             out["timings"][k] = {"n": n, "min": mn if n else math.nan, "max": mx if n else math.nan,
                                  "mean": mean if n else math.nan, "variance": (m2 / n) if n else math.nan}
+        if self.hist is not None:
+            # bin 0: < 2^-10 s; bin k: [2^(k-11), 2^(k-10)) s; last bin: >= 2^20 s
+            out["histograms"] = {"log2_lower_edge_s": [None] + list(range(-10, 21)), **self.hist}
         return out
 
 

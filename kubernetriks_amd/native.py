@@ -29,9 +29,12 @@ RUN_UNTIL_TIME = 1
 STATUS = {0: "running", 1: "finished", 2: "error", 3: "time_limit"}
 
 
+HIST_BINS = 32  # K10S_HIST_BINS (include/k10s.h): log2 bins, 0: < 2^-10 s, k: [2^(k-11), 2^(k-10)), 31: >= 2^20 s
+
+
 class Estimator(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint64), ("min", ctypes.c_double), ("max", ctypes.c_double),
-                ("mean", ctypes.c_double), ("sum2", ctypes.c_double)]
+                ("mean", ctypes.c_double), ("sum2", ctypes.c_double), ("hist", ctypes.c_uint32 * HIST_BINS)]
 
 
 class ReplicaResult(ctypes.Structure):
@@ -84,7 +87,8 @@ def result_to_dict(r: ReplicaResult) -> dict:
         "error_seq": r.error_seq, "error_time": r.error_time, "time": r.clock,
         "counters": {COUNTER_NAMES[i]: int(r.counters[i]) for i in range(NUM_COUNTERS)},
         "estimators": {EST_NAMES[i]: [int(r.est[i].n), r.est[i].min, r.est[i].max, r.est[i].mean,
-                                      (r.est[i].sum2 / r.est[i].n) if r.est[i].n else math.nan]
+                                      (r.est[i].sum2 / r.est[i].n) if r.est[i].n else math.nan,
+                                      list(r.est[i].hist)]
                        for i in range(3)},
         "unschedulable_len": r.unschedulable_len, "active_len": r.active_len,
         "node_counts": [r.node_count_as, r.node_count_ps, r.node_count_s],

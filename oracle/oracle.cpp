@@ -71,10 +71,19 @@ static inline uint64_t f64_as_u64(double x) {
 /* `average` 0.15 estimators: concatenate!(Min, Max, Mean, Variance) (collector.rs:15-21).     */
 /* Mean: n += 1; avg += (x - avg) / n.  Variance: sum2 += d*d*n*(n-1), d = (x - avg_old)/n.    */
 /* ------------------------------------------------------------------------------------------ */
+/* Engine addition (no reference counterpart): 32 log2 bins of the same values, include/k10s.h
+   K10S_HIST_BINS.  Bin 0: x < 2^-10 or NaN; k: 2^(k-11) <= x < 2^(k-10); 31: x >= 2^20. */
+static int hist_bin(double x) {
+    if (!(x >= 0.0009765625)) return 0;
+    int e = std::ilogb(x);
+    return e >= 20 ? 31 : e + 11;
+}
 struct Estimator {
     uint64_t n = 0;
     double mn = INFINITY, mx = -INFINITY, avg = 0.0, sum2 = 0.0;
+    uint32_t hist[32] = {};
     void add(double x) {
+        hist[hist_bin(x)] += 1;
         mn = std::fmin(mn, x);
         mx = std::fmax(mx, x);
         n += 1;
@@ -1760,7 +1769,9 @@ static void jest(std::string& o, const char* name, const Estimator& e) {
     o += '"'; o += name; o += "\":[";
     o += std::to_string(e.n); o += ',';
     jnum(o, e.mn); o += ','; jnum(o, e.mx); o += ','; jnum(o, e.mean()); o += ','; jnum(o, e.population_variance());
-    o += ']';
+    o += ",[";
+    for (int i = 0; i < 32; i++) { if (i) o += ','; o += std::to_string(e.hist[i]); }
+    o += "]]";
 }
 
 static std::string dump_json(Sim& s, int status, int flags) {

@@ -71,7 +71,7 @@ def compare(od: dict, eng, r: int = 0, log: bool = True, check_status: bool = Tr
             bad.append(f"counter {k}: oracle={v} engine={er['counters'][k]}")
     for k, ov in od["estimators"].items():
         ev = er["estimators"][k]
-        if ov[0] != ev[0] or not all(feq(a, b) for a, b in zip(ov[1:], ev[1:])):
+        if ov[0] != ev[0] or not all(feq(a, b) for a, b in zip(ov[1:5], ev[1:5])) or list(ov[5]) != list(ev[5]):
             bad.append(f"estimator {k}: oracle={ov} engine={ev}")
     if od["unschedulable_len"] != er["unschedulable_len"]:
         bad.append(f"unschedulable_len: oracle={od['unschedulable_len']} engine={er['unschedulable_len']}")

@@ -45,7 +45,7 @@ def test_metrics_json_layout_and_values():
     assert list(d["timings"]) == ["pod_duration", "pod_schedule_time", "pod_queue_time"]
     for k in m.PRINTER_COUNTERS:
         assert d["counters"][k] == od["counters"][k]
-    n, mn, mx, mean, var = od["estimators"]["pod_duration"]
+    n, mn, mx, mean, var = od["estimators"]["pod_duration"][:5]
     assert n == 3 and (mn, mx) == (25.0, 100.0)
     assert d["timings"]["pod_duration"] == {"min": mn, "max": mx, "mean": mean, "variance": var}
     assert text.startswith('{\n  "counters": {\n    "total_nodes_in_trace": 1,')
@@ -95,3 +95,23 @@ def test_ensemble_summary_pools_estimators():
     assert abs(t["mean"] - mu) < 1e-12
     assert abs(t["variance"] - sum((x - mu) ** 2 for x in allx) / 6) < 1e-12
     assert s.as_dict()["counters"]["placements"] == 6
+
+
+def test_estimator_histograms_count_every_sample_and_match_oracle():
+    """K10S_HIST_BINS log2 histograms (engine addition): the oracle's and the engine's agree bin for
+    bin (parity.compare checks them), and each holds exactly n samples in the bins the pod
+    durations of the reference scenario fall into."""
+    import math
+    import parity
+    import scenarios as sc
+    from hostcheck_bridge import HostEngine
+    od, eng = parity.run_pair(HostEngine, sc.sc_c1_generic_example(), max_time=20000.0)
+    assert parity.compare(od, eng) == []
+    est = eng.results()[0]["estimators"]
+    for k, row in est.items():
+        assert sum(row[5]) == row[0], k
+    n, mn, mx = est["pod_duration"][:3]
+    lo = 0 if mn < 2 ** -10 else min(31, math.frexp(mn)[1] - 1 + 11)
+    hi = 0 if mx < 2 ** -10 else min(31, math.frexp(mx)[1] - 1 + 11)
+    h = est["pod_duration"][5]
+    assert h[lo] > 0 and h[hi] > 0 and sum(h[lo:hi + 1]) == n

@@ -97,6 +97,9 @@ def test_two_gloo_ranks_equal_one_rank(tmp_path):
     want = ensemble.ensemble_summary(eng.raw_results()).as_dict()
     assert got["summary"] == _canon(want)
     assert want["replicas"] == 2 * R and want["counters"]["placements"] > 0
+    # histograms went through the cross-rank SUM all-reduce and count every estimator sample
+    for k, t in want["timings"].items():
+        assert sum(want["histograms"][k]) == t["n"] > 0, k
     tot = [0.0] * NUM_COUNTERS
     for r in eng.raw_results():
         for k in range(NUM_COUNTERS):
