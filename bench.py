@@ -219,7 +219,7 @@ def main():
         "ensemble": {"replicas": summary["replicas"], "replica_status": summary["replica_status"],
                      "counters": {k: summary["counters"][k] for k in ("total_pods_in_trace", "pods_succeeded",
                                                                        "terminated_pods", "placements", "events")},
-                     "timings": summary["timings"]},
+                     "timings": summary["timings"], "histograms": summary.get("histograms")},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
