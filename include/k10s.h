@@ -159,7 +159,18 @@ typedef struct k10s_capacities {
     uint32_t pruned_scan;                /* 0 = every attempt scans every node (default);
                                             1 = exact block-bound pruned scan where it applies
                                              */
+    uint32_t gauge_log;                  /* rows of the 5-s gauge recorder kept per replica; 0 = off */
 } k10s_capacities;
+
+/* One row of the gauge recorder (MetricsCollector::record_gauge_metrics, collector.rs:352-407,
+   written every 5 s of simulated time as the reference's gauge CSV).  The two node averages sum
+   over the api server's created nodes in name order (the reference sums in HashMap order). */
+typedef struct k10s_gauge_row {
+    double time;
+    uint64_t current_nodes, current_pods, pods_in_scheduling_queues;
+    double node_average_cpu_utilization, node_average_ram_utilization;
+    double cluster_total_cpu_utilization, cluster_total_ram_utilization;
+} k10s_gauge_row;
 #define K10S_FIFO_OFF 0xFFFFFFFFu
 
 /* Parity event-log entry: one delivered event (time, id order). */
@@ -256,6 +267,10 @@ int32_t k10s_engine_step_async(k10s_engine* e, int32_t mode, double until_time, 
 int32_t k10s_engine_sync(k10s_engine* e);
 
 int32_t k10s_engine_results(const k10s_engine* e, k10s_replica_result* out /* [n_replicas] */);
+/* Gauge rows of one replica (k10s_capacities.gauge_log > 0): the first min(cap, recorded) rows;
+   *n = rows copied.  Result flags bit2 marks a gauge log overflow. */
+int32_t k10s_engine_gauges(const k10s_engine* e, uint32_t replica, k10s_gauge_row* out, uint32_t cap,
+                           uint32_t* n);
 int32_t k10s_engine_event_log(const k10s_engine* e, uint32_t replica, k10s_log_entry* out, uint32_t cap,
                               uint32_t* n);
 int32_t k10s_engine_placements(const k10s_engine* e, uint32_t replica, k10s_placement* out, uint32_t cap,

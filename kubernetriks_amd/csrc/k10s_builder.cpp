@@ -652,6 +652,7 @@ Layout make_layout(const HostScenario& hs, const k10s_capacities& caps) {
     L.cap_undo = hs.ca_enabled ? (uint32_t)(P + 16) : 0;
     L.cap_log = caps.event_log;
     L.cap_place = caps.placement_log;
+    L.cap_gauge = caps.gauge_log;
     L.rec_on = caps.pod_records ? 1 : 0;
     if (caps.delay_fifo == K10S_FIFO_OFF) {
         L.cap_fq = 0;
@@ -698,6 +699,9 @@ Layout make_layout(const HostScenario& hs, const k10s_capacities& caps) {
     L.log = take(sizeof(k10s_log_entry) * (uint64_t)L.cap_log);
     L.place = take(sizeof(k10s_placement) * (uint64_t)L.cap_place);
     L.fq = take(sizeof(HeapEv) * (uint64_t)L.cap_fq * K10S_NFQ);
+    L.gauge = take(sizeof(k10s_gauge_row) * (uint64_t)L.cap_gauge);
+    L.g_cpu = take(L.cap_gauge ? 4 * S : 0);
+    L.g_ram = take(L.cap_gauge ? 8 * S : 0);
     L.stride = (off + 4095) & ~(uint64_t)4095;
     return L;
 }

@@ -69,6 +69,9 @@ struct Rep {
     K10S_HD QInfo* uq() const { return at<QInfo>(L().uq); }
     K10S_HD k10s_log_entry* log() const { return L().cap_log ? at<k10s_log_entry>(L().log) : nullptr; }
     K10S_HD k10s_placement* place() const { return L().cap_place ? at<k10s_placement>(L().place) : nullptr; }
+    K10S_HD k10s_gauge_row* gauge() const { return at<k10s_gauge_row>(L().gauge); }
+    K10S_HD uint32_t* g_cpu() const { return at<uint32_t>(L().g_cpu); }
+    K10S_HD uint64_t* g_ram() const { return at<uint64_t>(L().g_ram); }
 };
 
 #if !K10S_DEVICE
@@ -540,6 +543,10 @@ K10S_HD void run_insert(Ctx& c, int32_t slot, uint32_t p) {
     if (h >= 0) c.V().pod(h).run_prev = (int32_t)p;
     c.V().slot(slot).head = (int32_t)p;
     c.V().pod(p).run_slot = slot;
+    if (c.Ly().cap_gauge) {  // allocate_pod_requests (node_component.rs:83-86): gauge recorder only
+        c.V().g_cpu()[slot] -= c.V().pod(p).req_cpu;
+        c.V().g_ram()[slot] -= c.V().pod(p).req_ram;
+    }
 }
 K10S_HD void run_remove(Ctx& c, uint32_t p) {
     int32_t slot = c.V().pod(p).run_slot;
@@ -547,6 +554,10 @@ K10S_HD void run_remove(Ctx& c, uint32_t p) {
     if (pr >= 0) c.V().pod(pr).run_next = nx;
     else c.V().slot(slot).head = nx;
     if (nx >= 0) c.V().pod(nx).run_prev = pr;
+    if (c.Ly().cap_gauge) {  // free_pod_requests (node_component.rs:88-91)
+        c.V().g_cpu()[slot] += c.V().pod(p).req_cpu;
+        c.V().g_ram()[slot] += c.V().pod(p).req_ram;
+    }
     c.V().pod(p).run_slot = -1;
     c.V().pod(p).finish_seq = 0;  // cancels a pending finish event (dslab cancel_event)
     int32_t g = c.S().pod_group[p];
@@ -887,6 +898,7 @@ K10S_HD int schedule_scan_pruned(Ctx& c, uint32_t rc, uint64_t rr, int32_t* chos
 K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
     double cycle_dur = 0.0;
     RepHdr* h = &c.H();
+    h->g_pods_q = (uint64_t)h->aq_size + (uint64_t)h->uq_size;  // scheduler.rs:256-259
     const double w = c.P().score_weight;
     while (c.H().aq_size > 0 && !c.H().error_code) {
         QInfo q = aq_pop(c);
@@ -1448,6 +1460,7 @@ K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
     case K10S_EV_AS_CREATE_NODE_REQ: {
         uint32_t def = e.b;
         uint32_t n = sc->def_node[def];
+        h->g_cur_nodes += 1;  // api_server.rs:133-137
         c.V().node(n).pend_def = (int32_t)def;
         emit(c, K10S_EV_PS_CREATE_NODE_REQ, pr->as_to_ps_network_delay, -1, n, def, 0.0, FQ_AS_TO_PS);
         break;
@@ -1475,10 +1488,15 @@ K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
         }
         c.V().node(n).as_slot = (int32_t)slot;
         h->as_node_count += 1;
+        if (c.Ly().cap_gauge) {  // the component's node: allocatable = capacity (api_server.rs:133)
+            c.V().g_cpu()[slot] = sc->def_cpu[def];
+            c.V().g_ram()[slot] = sc->def_ram[def];
+        }
         emit(c, K10S_EV_PS_NODE_ADDED, pr->as_to_ps_network_delay, -1, n, 0, e.time, FQ_AS_TO_PS);
         break;
     }
     case K10S_EV_AS_CREATE_POD_REQ:
+        h->g_cur_pods += 1;  // api_server.rs:151-155
         emit(c, K10S_EV_PS_CREATE_POD_REQ, pr->as_to_ps_network_delay, -1, e.a, 0, 0.0, FQ_AS_TO_PS);
         break;
     case K10S_EV_AS_ASSIGN_REQ: {
@@ -1508,6 +1526,7 @@ K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
     case K10S_EV_AS_POD_FINISHED:
         h->counters[K10S_C_TERMINATED_PODS] += 1;
         h->counters[K10S_C_PODS_SUCCEEDED] += 1;
+        h->g_cur_pods -= 1;  // api_server.rs:262-265
         emit(c, K10S_EV_PS_POD_FINISHED, pr->as_to_ps_network_delay, -1, e.a, e.b, e.x, FQ_AS_TO_PS);
         break;
     case K10S_EV_AS_REMOVE_NODE_REQ:
@@ -1532,6 +1551,7 @@ K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
         }
         c.V().node(n).as_slot = -1;
         h->as_node_count -= 1;
+        h->g_cur_nodes -= 1;  // api_server.rs:301-304
         // reclaim_component (node_component_pool.rs:68-77)
         c.V().slot(slot).node = -1;
         c.V().slot(slot).removed = 0;
@@ -1570,6 +1590,7 @@ K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
         if (e.b) {
             h->counters[K10S_C_TERMINATED_PODS] += 1;
             h->counters[K10S_C_PODS_REMOVED] += 1;
+            h->g_cur_pods -= 1;  // api_server.rs:388-391
         }
         emit(c, K10S_EV_PS_POD_REMOVED, pr->as_to_ps_network_delay, -1, e.a, e.b, e.x, FQ_AS_TO_PS);
         break;
@@ -1591,6 +1612,7 @@ K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
             fail(c, K10S_ERR_NAME_BOUND);
             return;
         }
+        h->g_cur_pods += init;  // api_server.rs:442-446
         for (uint32_t k = 0; k < init && !c.H().error_code; k++)
             emit(c, K10S_EV_PS_CREATE_POD_REQ, pr->as_to_ps_network_delay, -1, sc->g_pod[g * sc->group_bound + k], 0, 0.0, FQ_AS_TO_PS);
         if (sc->hpa_enabled) emit(c, K10S_EV_HPA_REGISTER_GROUP, pr->as_to_hpa_network_delay, -1, g, 0, e.time, FQ_AS_TO_HPA);
@@ -1640,6 +1662,10 @@ K10S_WARM void on_node(Ctx& c, HeapEv e) {
         SL.head = (int32_t)p;
         P.run_slot = slot;
         P.finish_seq = fseq;
+        if (c.Ly().cap_gauge) {  // allocate_pod_requests (node_component.rs:83-86, called at 164)
+            c.V().g_cpu()[slot] -= P.req_cpu;
+            c.V().g_ram()[slot] -= P.req_ram;
+        }
         if (g >= 0) c.V().grp()[g].running += 1;
         emit(c, K10S_EV_AS_POD_STARTED, pr->as_to_node_network_delay, -1, p, 0, e.time, FQ_AS_TO_NODE);
         break;
@@ -1814,9 +1840,87 @@ K10S_HD double usage_poll(const Scenario* sc, uint8_t kind, double usage, uint32
     return fmin_rs(1.0, sc->unit_load[uoff + idx] / (double)count);
 }
 
+// ---- gauge recorder (collector.rs:352-407), opt-in (k10s_capacities.gauge_log) ------------------
+#if K10S_DEVICE
+K10S_D double lane_f64(double v, int l) {
+    const uint64_t b = f2u(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return u2f((uint64_t)lo | ((uint64_t)hi << 32));
+}
+K10S_D uint64_t wave_sum_u64_cold(uint64_t v) {
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor((unsigned long long)v, o);
+    return v;
+}
+#endif
+// collect_utilizations + record_gauge_metrics: one row per 5-s tick.  The lanes load 64 consecutive
+// node indices at a time; the f64 node averages are then summed serially over the created nodes in
+// name order (ascending index), the integer cluster sums in any order (exact).
+K10S_COLD void gauge_record(Ctx& c, double t) {
+    RepHdr* h = &c.H();
+    if (h->gauge_n >= c.Ly().cap_gauge) {
+        h->flags |= 4u;
+        return;
+    }
+    const Scenario* sc = &c.S();
+    const uint32_t N = sc->n_nodes;
+    double navg_c = 0.0, navg_r = 0.0;
+    uint64_t rq_c = 0, rq_r = 0, cap_c = 0, cap_r = 0, cnt = 0;
+    for (uint32_t base = 0; base < N; base += K10S_LANES) {
+        const uint32_t n = base + (uint32_t)lane_id();
+        const int32_t slot = n < N ? c.V().node(n).as_slot : -1;
+        double fc = 0.0, fr = 0.0;
+        if (slot >= 0) {
+            const uint32_t def = c.V().slot(slot).def;
+            const uint64_t cc = sc->def_cpu[def], cr = sc->def_ram[def];
+            const uint64_t qc = cc - (uint64_t)c.V().g_cpu()[slot], qr = cr - c.V().g_ram()[slot];
+            fc = (double)qc / (double)cc;
+            fr = (double)qr / (double)cr;
+            rq_c += qc;
+            rq_r += qr;
+            cap_c += cc;
+            cap_r += cr;
+        }
+#if K10S_DEVICE
+        uint64_t m = __ballot(slot >= 0);
+        cnt += (uint64_t)__popcll(m);
+        while (m) {
+            const int l = (int)uniform_u32((uint32_t)__builtin_ctzll(m));
+            m &= m - 1;
+            navg_c += lane_f64(fc, l);
+            navg_r += lane_f64(fr, l);
+        }
+#else
+        if (slot >= 0) {
+            cnt += 1;
+            navg_c += fc;
+            navg_r += fr;
+        }
+#endif
+    }
+#if K10S_DEVICE
+    rq_c = wave_sum_u64_cold(rq_c);
+    rq_r = wave_sum_u64_cold(rq_r);
+    cap_c = wave_sum_u64_cold(cap_c);
+    cap_r = wave_sum_u64_cold(cap_r);
+#endif
+    k10s_gauge_row row;
+    row.time = t;
+    row.current_nodes = h->g_cur_nodes;
+    row.current_pods = h->g_cur_pods;
+    row.pods_in_scheduling_queues = h->g_pods_q;
+    row.node_average_cpu_utilization = navg_c / (double)cnt;
+    row.node_average_ram_utilization = navg_r / (double)cnt;
+    row.cluster_total_cpu_utilization = (double)rq_c / (double)cap_c;
+    row.cluster_total_ram_utilization = (double)rq_r / (double)cap_r;
+    c.V().gauge()[h->gauge_n] = row;
+    h->gauge_n += 1;
+}
+
 K10S_COLD void on_metrics(Ctx& c, HeapEv e) {
     uniform_event(e);
     if (e.kind == K10S_EV_M_GAUGE_TICK) {  // CSV gauge record: no simulation state (collector.rs:392-407)
+        if (c.Ly().cap_gauge) gauge_record(c, e.time);
         emit0(c, K10S_EV_M_GAUGE_TICK, 5.0);
         return;
     }
@@ -1953,6 +2057,10 @@ K10S_HD void init_replica(Ctx& c) {
         nd.as_slot = (int32_t)slot;
         v.slot((int32_t)slot).node = (int32_t)n;
         v.slot((int32_t)slot).def = def;
+        if (L->cap_gauge) {
+            v.g_cpu()[slot] = sc->def_cpu[def];
+            v.g_ram()[slot] = sc->def_ram[def];
+        }
         s_cpu[n] = sc->def_cpu[def];
         s_ram[n] = sc->def_ram[def];
         bit_set(v.s_present(), n);
@@ -1963,6 +2071,7 @@ K10S_HD void init_replica(Ctx& c) {
     h->counters[K10S_C_NODES_READ] = 0;
     h->ps_node_count = sc->n_default;
     h->as_node_count = sc->n_default;
+    h->g_cur_nodes = sc->n_default;  // simulator.rs:339-342
     h->cur_kind = 0xFFFF;
     emit0(c, K10S_EV_M_POD_METRICS_TICK, 0.0);  // id 0 (simulator.rs:156-158)
     emit0(c, K10S_EV_M_GAUGE_TICK, 0.0);        // id 1 (simulator.rs:159-161)

@@ -397,6 +397,18 @@ int32_t k10s_engine_event_log(const k10s_engine* e, uint32_t r, k10s_log_entry* 
     return K10S_OK;
 }
 
+int32_t k10s_engine_gauges(const k10s_engine* e, uint32_t r, k10s_gauge_row* out, uint32_t cap, uint32_t* n) {
+    if (!e || !n) return set_err(K10S_E_INVALID, "null");
+    RepHdr h;
+    int32_t rc = read_hdr(e, r, h);
+    if (rc) return rc;
+    uint32_t k = e->L.cap_gauge ? (h.gauge_n < cap ? h.gauge_n : cap) : 0;
+    if (k) HIPCHK(hipMemcpy(out, e->d_state + (size_t)r * e->L.stride + e->L.gauge, sizeof(k10s_gauge_row) * k,
+                            hipMemcpyDeviceToHost));
+    *n = k;
+    return K10S_OK;
+}
+
 int32_t k10s_engine_placements(const k10s_engine* e, uint32_t r, k10s_placement* out, uint32_t cap, uint32_t* n) {
     if (!e || !n) return set_err(K10S_E_INVALID, "null");
     RepHdr h;

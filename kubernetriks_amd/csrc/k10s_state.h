@@ -178,7 +178,8 @@ struct RepHdr {
     uint32_t flags;
     uint32_t unsched_cache_count;
     uint32_t cur_kind, cur_seq;   // event being handled (panic attribution)
-    uint32_t pad;
+    uint32_t gauge_n;             // gauge rows recorded
+    uint64_t g_cur_nodes, g_cur_pods, g_pods_q;   // GaugeMetrics counters (collector.rs:169-190)
     // event queue: delay-class FIFO rings (head/tail counters, newest time, cached head entries)
     // and the cached root of the heap (valid while heap_size > 0)
     uint32_t fq_head[K10S_NFQ], fq_tail[K10S_NFQ];
@@ -276,13 +277,14 @@ struct Layout {
     uint64_t grp, grp_bits;
     uint64_t cag, ca_act, ca_cpu, ca_ram, ca_undo;
     uint64_t heap, aq, uq, log, place, fq;
+    uint64_t gauge, g_cpu, g_ram;        // gauge rows; node-component allocatable per slot
     uint32_t cap_fq;      // entries per delay-class ring (power of two; 0 = no rings)
     uint32_t pruned;      // 1: block bounds maintained, exact pruned scan where it applies
     uint32_t cap_heap, cap_aq, cap_uq, cap_act, cap_log, cap_place, cap_undo, rec_on;
     uint32_t words_nodes, words_uids, words_group;
     uint32_t bshift;      // block = 2^bshift consecutive node indices (>= 64, <= 64 blocks)
     uint32_t nblocks;
-    uint32_t pad;
+    uint32_t cap_gauge;   // gauge rows per replica (0 = gauge recorder off)
 };
 
 // Everything a launch reads but never writes, as one block (device: __constant__ memory).

@@ -160,6 +160,22 @@ def assert_and_print(result: dict, fmt: str = "json") -> str:
     return metrics_json(result) if fmt == "json" else metrics_table(result)
 
 
+# ---- gauge recorder CSV (collector.rs:215-226 header, 392-407 rows) -----------------------------
+GAUGE_COLUMNS = ["timestamp", "current_nodes", "current_pods", "pods_in_scheduling_queues",
+                 "node_average_cpu_utilization", "node_average_ram_utilization",
+                 "cluster_total_cpu_utilization", "cluster_total_ram_utilization"]
+
+
+def gauge_csv(rows) -> str:
+    """experiments/gauge_metrics.csv as the reference writes it (csv crate, `to_string()` of each
+    value: Rust Display for f64, decimal for u64) from Engine.gauges() rows."""
+    out = [",".join(GAUGE_COLUMNS)]
+    for r in rows:
+        out.append(",".join([rust_display(float(r[0]))] + [str(int(v)) for v in r[1:4]] +
+                            [rust_display(float(v)) for v in r[4:8]]))
+    return "\n".join(out) + "\n"
+
+
 # ---- cross-replica summary (SURVEY.md §8(e)) ----------------------------------------------------
 class EnsembleSummary:
     """Counters summed over replicas; estimators merged in the order replicas are added.

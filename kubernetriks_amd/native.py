@@ -64,7 +64,14 @@ class Capacities(ctypes.Structure):
                 ("unschedulable", ctypes.c_uint32), ("group_name_bound", ctypes.c_uint32),
                 ("ca_name_bound", ctypes.c_uint32), ("event_log", ctypes.c_uint32),
                 ("placement_log", ctypes.c_uint32), ("pod_records", ctypes.c_uint32),
-                ("delay_fifo", ctypes.c_uint32), ("pruned_scan", ctypes.c_uint32)]
+                ("delay_fifo", ctypes.c_uint32), ("pruned_scan", ctypes.c_uint32), ("gauge_log", ctypes.c_uint32)]
+
+
+class GaugeRow(ctypes.Structure):  # k10s_gauge_row (collector.rs:392-407 CSV columns)
+    _fields_ = [("time", ctypes.c_double), ("current_nodes", ctypes.c_uint64), ("current_pods", ctypes.c_uint64),
+                ("pods_in_scheduling_queues", ctypes.c_uint64), ("node_average_cpu_utilization", ctypes.c_double),
+                ("node_average_ram_utilization", ctypes.c_double), ("cluster_total_cpu_utilization", ctypes.c_double),
+                ("cluster_total_ram_utilization", ctypes.c_double)]
 
 
 class LogEntry(ctypes.Structure):
@@ -104,6 +111,7 @@ def _decl(L, prefix: str):
         "results": (i32, [vp, P(ReplicaResult)]),
         "event_log": (i32, [vp, u32, P(LogEntry), u32, P(u32)]),
         "placements": (i32, [vp, u32, P(Placement), u32, P(u32)]),
+        "gauges": (i32, [vp, u32, P(GaugeRow), u32, P(u32)]),
         "pod_records": (i32, [vp, u32, P(PodRecord), u32, P(u32)]),
         "group_sizes": (i32, [vp, u32, P(u32), P(u32), u32, P(u32)]),
         "num_nodes": (u32, [vp]), "num_pods": (u32, [vp]), "num_groups": (u32, [vp]),
@@ -167,6 +175,14 @@ class EngineBase:
         nn, pn, _ = self._names()
         return [(e.seq, e.time, e.kind, pn[e.pod] if e.pod >= 0 else "", nn[e.node] if e.node >= 0 else "", e.slot)
                 for e in buf[: n.value]]
+
+    def gauges(self, r: int, cap: int = 1 << 20) -> List[tuple]:
+        """Gauge recorder rows (time, current_nodes, current_pods, pods_in_scheduling_queues,
+        node_average_cpu, node_average_ram, cluster_total_cpu, cluster_total_ram)."""
+        buf = (GaugeRow * cap)()
+        n = ctypes.c_uint32()
+        self._check(self._fn["gauges"](self._h, r, buf, cap, ctypes.byref(n)))
+        return [tuple(getattr(g, f) for f, _ in GaugeRow._fields_) for g in buf[: n.value]]
 
     def placements(self, r: int, cap: int = 1 << 22) -> List[tuple]:
         buf = (Placement * cap)()

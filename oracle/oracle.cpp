@@ -22,6 +22,7 @@
  * Every handler cites the reference file:line it follows.
  */
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -78,6 +79,10 @@ static int hist_bin(double x) {
     int e = std::ilogb(x);
     return e >= 20 ? 31 : e + 11;
 }
+/* GaugeMetrics (collector.rs:169-190): the three counters the api server / scheduler maintain */
+struct GaugeMetrics {
+    uint64_t current_nodes = 0, current_pods = 0, pods_in_scheduling_queues = 0;
+};
 struct Estimator {
     uint64_t n = 0;
     double mn = INFINITY, mx = -INFINITY, avg = 0.0, sum2 = 0.0;
@@ -454,6 +459,9 @@ public:
     std::map<std::string, PodGroupInfo> hpa_groups;
 
     /* metrics collector (collector.rs) */
+    GaugeMetrics gauge;                 /* collector.rs:169-190 */
+    size_t gauge_cap = 0;               /* rows kept (0 = gauge recording off) */
+    std::vector<std::array<double, 8>> gauge_rows;
     Counters c;
     Estimator pod_duration, sched_latency, queue_time;
     std::map<std::string, std::pair<Estimator, Estimator>> pod_utilization;
@@ -575,6 +583,7 @@ void Sim::initialize() {
                 total_nodes++;
             }
         }
+        gauge.current_nodes += to_add.size();   /* simulator.rs:339-342 */
         for (auto& n0 : to_add) {   /* KubernetriksSimulation::add_node, simulator.rs:277-301 */
             Node n = n0;
             n.alloc_cpu = n.cap_cpu;
@@ -714,7 +723,29 @@ void Sim::on_metrics(Ev& e) {
         collect_pod_metrics(e.time);
         emit(K10S_EV_M_POD_METRICS_TICK, 60.0);
     } else {
-        /* record_gauge_metrics writes a CSV row; no simulation state changes (collector.rs:392-407) */
+        /* record_gauge_metrics (collector.rs:352-407): a CSV row, no simulation state changes.
+           collect_utilizations sums over api_server.all_created_nodes() — HashMap order in the
+           reference (not bit-stable); here name order (= the engine's order, defined). */
+        if (gauge_rows.size() < gauge_cap) {
+            double navg_c = 0.0, navg_r = 0.0;
+            uint64_t rq_c = 0, rq_r = 0, cap_c = 0, cap_r = 0;
+            for (auto& cn : created_nodes) {
+                const Node& n = comps[cn.second].node;
+                uint64_t cr = (uint64_t)n.cap_cpu - (uint64_t)n.alloc_cpu;
+                uint64_t rr = (uint64_t)n.cap_ram - (uint64_t)n.alloc_ram;
+                navg_c += (double)cr / (double)n.cap_cpu;
+                navg_r += (double)rr / (double)n.cap_ram;
+                rq_c += cr;
+                rq_r += rr;
+                cap_c += (uint64_t)n.cap_cpu;
+                cap_r += (uint64_t)n.cap_ram;
+            }
+            navg_c /= (double)created_nodes.size();
+            navg_r /= (double)created_nodes.size();
+            gauge_rows.push_back({e.time, (double)gauge.current_nodes, (double)gauge.current_pods,
+                                  (double)gauge.pods_in_scheduling_queues, navg_c, navg_r,
+                                  (double)rq_c / (double)cap_c, (double)rq_r / (double)cap_r});
+        }
         emit(K10S_EV_M_GAUGE_TICK, 5.0);
     }
 }
@@ -725,6 +756,7 @@ void Sim::on_metrics(Ev& e) {
 void Sim::on_as(Ev& e) {
     switch (e.kind) {
     case K10S_EV_AS_CREATE_NODE_REQ: {            /* 132-146 */
+        gauge.current_nodes += 1;
         Node n = *e.node_obj;
         n.alloc_cpu = n.cap_cpu;
         n.alloc_ram = n.cap_ram;
@@ -752,6 +784,7 @@ void Sim::on_as(Ev& e) {
         break;
     }
     case K10S_EV_AS_CREATE_POD_REQ: {             /* 151-162 */
+        gauge.current_pods += 1;
         auto f = emit(K10S_EV_PS_CREATE_POD_REQ, cfg.as_to_ps);
         f->pod_obj = e.pod_obj;
         f->pod = e.pod;
@@ -791,6 +824,7 @@ void Sim::on_as(Ev& e) {
     case K10S_EV_AS_POD_FINISHED: {               /* 247-277 */
         c.terminated_pods++;
         c.pods_succeeded++;
+        gauge.current_pods -= 1;
         auto f = emit(K10S_EV_PS_POD_FINISHED, cfg.as_to_ps);
         f->pod = e.pod;
         f->node = e.node;
@@ -814,6 +848,7 @@ void Sim::on_as(Ev& e) {
     case K10S_EV_AS_NODE_REMOVED: {               /* 297-319 */
         auto it = created_nodes.find(e.node);
         if (it == created_nodes.end()) panic("created_nodes.remove(node).unwrap()");
+        gauge.current_nodes -= 1;
         int slot = it->second;
         created_nodes.erase(it);
         NodeComponent& nc = comps[slot];             /* reclaim_component, node_component_pool.rs:68-77 */
@@ -862,6 +897,7 @@ void Sim::on_as(Ev& e) {
         if (e.flag) {
             c.terminated_pods++;
             c.pods_removed++;
+            gauge.current_pods -= 1;
         }
         auto f = emit(K10S_EV_PS_POD_REMOVED, cfg.as_to_ps);
         f->pod = e.pod;
@@ -875,6 +911,7 @@ void Sim::on_as(Ev& e) {
         auto info = std::make_shared<PodGroupInfo>();
         info->creation_time = e.time;
         info->group = g;
+        gauge.current_pods += g->initial;
         for (uint64_t idx = 0; idx < g->initial; idx++) {
             Pod p = g->tmpl;
             p.name = g->name + "_" + std::to_string(idx);
@@ -1126,6 +1163,7 @@ void Sim::s_release(const Pod& pod) {                                     /* 153
 }
 
 void Sim::run_scheduling_cycle(double t) {                                /* 246-334 */
+    gauge.pods_in_scheduling_queues = (uint64_t)action_queue.data.size() + (uint64_t)unschedulable.size();  /* 256-259 */
     double cycle_dur = 0.0;
     QueuedPodInfo next;
     while (action_queue.pop(next)) {
@@ -1299,6 +1337,8 @@ void Sim::on_node(Ev& e) {
         }
         info.cpu = p.cpu;
         info.ram = p.ram;
+        nc.node.alloc_cpu -= p.cpu;               /* allocate_pod_requests (83-86, called at 164) */
+        nc.node.alloc_ram -= p.ram;
         nc.running_pods[p.name] = info;
         auto f = emit(K10S_EV_AS_POD_STARTED, cfg.as_to_node);
         f->pod = p.name;
@@ -1308,6 +1348,8 @@ void Sim::on_node(Ev& e) {
     case K10S_EV_N_POD_FINISHED: {                /* 227-246 */
         auto it = nc.running_pods.find(e.pod);
         if (it == nc.running_pods.end()) panic("running_pods.remove(pod).unwrap() on finish");
+        nc.node.alloc_cpu += it->second.cpu;      /* free_pod_requests (88-91, called at 235) */
+        nc.node.alloc_ram += it->second.ram;
         nc.running_pods.erase(it);
         auto f = emit(K10S_EV_AS_POD_FINISHED, 0.0);
         f->pod = e.pod;
@@ -1318,6 +1360,8 @@ void Sim::on_node(Ev& e) {
     case K10S_EV_N_REMOVE_NODE: {                 /* 247-274 */
         if (!nc.has_runtime || e.node != nc.node.name) panic("Trying to remove other node than self");
         for (auto& rp : nc.running_pods) {        /* cancel_all_running_pods 95-112 */
+            nc.node.alloc_cpu += rp.second.cpu;   /* free_pod_requests at 108 */
+            nc.node.alloc_ram += rp.second.ram;
             nc.canceled_pods.insert(rp.first);
             if (rp.second.has_event) cancel(rp.second.event_id);
         }
@@ -1336,6 +1380,8 @@ void Sim::on_node(Ev& e) {
         if (it != nc.running_pods.end()) {
             bool he = it->second.has_event;
             uint64_t id = it->second.event_id;
+            nc.node.alloc_cpu += it->second.cpu;  /* free_pod_requests at 279 */
+            nc.node.alloc_ram += it->second.ram;
             nc.running_pods.erase(it);
             if (he) cancel(id);
             f = emit(K10S_EV_AS_POD_REMOVED, cfg.as_to_node);
@@ -1781,6 +1827,14 @@ static std::string dump_json(Sim& s, int status, int flags) {
     o += ",\"panic\":"; jstr(o, s.panic_msg);
     o += ",\"time\":"; jnum(o, s.clock);
     o += ",\"next_id\":" + std::to_string(s.next_id);
+    o += ",\"gauges\":[";
+    for (size_t i = 0; i < s.gauge_rows.size(); i++) {
+        if (i) o += ',';
+        o += '[';
+        for (int j = 0; j < 8; j++) { if (j) o += ','; jnum(o, s.gauge_rows[i][j]); }
+        o += ']';
+    }
+    o += ']';
     const Counters& c = s.c;
     o += ",\"counters\":{";
     o += "\"total_nodes_in_trace\":" + std::to_string(c.total_nodes_in_trace);
@@ -1902,6 +1956,7 @@ void* orc_new(const char* text, char* err, int errlen) {
 }
 void orc_free(void* p) { delete (Handle*)p; }
 void orc_set_log(void* p, int on) { ((Handle*)p)->sim.log_events = on != 0; }
+void orc_set_gauges(void* p, uint32_t cap) { ((Handle*)p)->sim.gauge_cap = cap; }
 int orc_run(void* p, double max_time) {
     auto* h = (Handle*)p;
     h->status = h->sim.run_until_all_finished(max_time);

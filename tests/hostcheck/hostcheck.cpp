@@ -111,6 +111,14 @@ int hc_event_log(void* p, uint32_t r, k10s_log_entry* out, uint32_t cap, uint32_
     *n = v.log() ? k : 0;
     return 0;
 }
+int hc_gauges(void* p, uint32_t r, k10s_gauge_row* out, uint32_t cap, uint32_t* n) {
+    HC* h = (HC*)p;
+    Rep v = make_rep(h->state.data(), h->L, r);
+    uint32_t k = h->L.cap_gauge ? (v.h()->gauge_n < cap ? v.h()->gauge_n : cap) : 0;
+    if (k) std::memcpy(out, v.gauge(), sizeof(k10s_gauge_row) * k);
+    *n = k;
+    return 0;
+}
 int hc_placements(void* p, uint32_t r, k10s_placement* out, uint32_t cap, uint32_t* n) {
     HC* h = (HC*)p;
     Rep v = make_rep(h->state.data(), h->L, r);

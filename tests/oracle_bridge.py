@@ -33,6 +33,7 @@ def lib():
         L.orc_new.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
         L.orc_free.argtypes = [ctypes.c_void_p]
         L.orc_set_log.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.orc_set_gauges.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         L.orc_run.argtypes = [ctypes.c_void_p, ctypes.c_double]
         L.orc_run.restype = ctypes.c_int
         L.orc_step_until.argtypes = [ctypes.c_void_p, ctypes.c_double]
@@ -64,7 +65,7 @@ def lib():
 class OracleSim:
     """One reference-semantics simulation (KubernetriksSimulation restated)."""
 
-    def __init__(self, scenario: str, log: bool = False):
+    def __init__(self, scenario: str, log: bool = False, gauges: int = 0):
         L = lib()
         err = ctypes.create_string_buffer(512)
         h = L.orc_new(scenario.encode(), err, 512)
@@ -73,6 +74,8 @@ class OracleSim:
         self._h = h
         if log:
             L.orc_set_log(h, 1)
+        if gauges:
+            L.orc_set_gauges(h, gauges)
 
     def __del__(self):
         if getattr(self, "_h", None):

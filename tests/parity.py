@@ -26,8 +26,12 @@ def feq(a: float, b: float) -> bool:
     return fbits(a) == fbits(b)
 
 
-def parity_caps(log: bool = True, fifo: int = 0, pruned: int = 0) -> Capacities:
+GAUGE_ROWS = 1 << 14  # gauge recorder rows kept by run_pair's oracle and engine
+
+
+def parity_caps(log: bool = True, fifo: int = 0, pruned: int = 0, gauges: int = 0) -> Capacities:
     c = Capacities()
+    c.gauge_log = gauges
     c.delay_fifo = fifo
     c.pruned_scan = pruned
     c.event_log = (1 << 20) if log else 0
@@ -40,14 +44,14 @@ def run_pair(engine_cls, scenario: str, mode: int = RUN_UNTIL_ALL_FINISHED, unti
              max_time: float = 1e7, budget: int = 0, log: bool = True, params=None, fifo: int = 0,
              pruned: int = 0):
     """Run the oracle and one engine replica on the same scenario; return (oracle dict, engine, res)."""
-    o = ob.OracleSim(scenario, log=log)
+    o = ob.OracleSim(scenario, log=log, gauges=GAUGE_ROWS)
     if mode == RUN_UNTIL_ALL_FINISHED:
         st = o.run_until_all_finished(max_time)
     else:
         st = o.step_until_time(until)
     od = o.result(placements=True, log=log)
     od["status_name"] = ORACLE_STATUS[st] if not od["panicked"] else "error"
-    eng = engine_cls(scenario, 1, params=params, caps=parity_caps(log, fifo, pruned))
+    eng = engine_cls(scenario, 1, params=params, caps=parity_caps(log, fifo, pruned, GAUGE_ROWS))
     if mode == RUN_UNTIL_ALL_FINISHED:
         eng.run_until_all_finished(max_time, budget)
     else:
@@ -79,6 +83,16 @@ def compare(od: dict, eng, r: int = 0, log: bool = True, check_status: bool = Tr
         bad.append(f"active_len: oracle={od['active_len']} engine={er['active_len']}")
     if od["node_counts"] != er["node_counts"]:
         bad.append(f"node_counts: oracle={od['node_counts']} engine={er['node_counts']}")
+    # gauge recorder rows (when both sides recorded them)
+    og = od.get("gauges") or []
+    if og:
+        eg = eng.gauges(r)
+        if len(og) != len(eg):
+            bad.append(f"gauges: oracle={len(og)} rows engine={len(eg)}")
+        for i, (a, b) in enumerate(zip(og, eg)):
+            if not all(feq(float(x), float(y)) for x, y in zip(a, b)):
+                bad.append(f"gauge row #{i}: oracle={a} engine={b}")
+                break
     # placements
     ep = eng.placements(r)
     op = [tuple(x) for x in od["placements"]]

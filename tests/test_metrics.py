@@ -115,3 +115,22 @@ def test_estimator_histograms_count_every_sample_and_match_oracle():
     hi = 0 if mx < 2 ** -10 else min(31, math.frexp(mx)[1] - 1 + 11)
     h = est["pod_duration"][5]
     assert h[lo] > 0 and h[hi] > 0 and sum(h[lo:hi + 1]) == n
+
+
+def test_gauge_recorder_rows_and_csv():
+    """The 5-s gauge recorder (collector.rs:352-407): engine rows equal the oracle's bit for bit
+    (parity.compare), one row per tick from t = 0, and the CSV has the reference's header."""
+    import parity
+    import scenarios as sc
+    from hostcheck_bridge import HostEngine
+    from kubernetriks_amd.metrics import GAUGE_COLUMNS, gauge_csv
+    od, eng = parity.run_pair(HostEngine, sc.sc_c1_generic_example(), max_time=20000.0)
+    assert parity.compare(od, eng) == []
+    rows = eng.gauges(0)
+    assert len(rows) == len(od["gauges"]) > 0
+    assert [r[0] for r in rows[:3]] == [0.0, 5.0, 10.0]
+    # 4 pods of 4000 mcpu / 8 GiB on one 16000 mcpu / 16 GiB node: cpu 0.5 (2 pods fit by ram), ram 1.0
+    assert (565.0, 1, 4, 4, 0.5, 1.0, 0.5, 1.0) in rows
+    text = gauge_csv(rows[113:114])
+    assert text.splitlines()[0] == ",".join(GAUGE_COLUMNS)
+    assert text.splitlines()[1] == "565,1,4,4,0.5,1,0.5,1"
