@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-workers", type=int, default=0, help="0 = min(16, cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-scan-kernel", action="store_true", help="skip the scheduling-kernel-alone measurement")
     ap.add_argument("--pruned-scan", action="store_true", help="exact block-bound pruned scan (DESIGN.md §3)")
     ap.add_argument("--profile", action="store_true", help="print the K10S_PROF cycle attribution (variant builds)")
     return ap.parse_args()
@@ -227,6 +228,14 @@ def main():
         except Exception as ex:  # the GPU number stands on its own
             log("cpu baseline failed:", ex)
             out["cpu_baseline"] = None
+    if rank == 0 and not args.no_scan_kernel:
+        # the scheduling-cycle kernel alone (k10s_schedule_one_batch over C3-sized node caches in HBM)
+        try:
+            from kubernetriks_amd.scanbench import measure
+            out["scheduling_kernel"] = measure(R, args.nodes)
+        except Exception as ex:
+            log("scan kernel measurement failed:", ex)
+            out["scheduling_kernel"] = None
     if args.profile:
         prof = eng.profile()
         tot = {k: float(sum(p[k] for p in prof)) for k in prof[0]}
