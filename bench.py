@@ -205,7 +205,7 @@ def main():
         "config": {"workload": f"C3: {R} replicas/GPU x {args.nodes}-node Alibaba-like cluster, {args.pods} pods/replica, "
                                "run until all pods finished (RunUntilAllPodsAreFinished)",
                    "replicas_per_gpu": R, "total_replicas": R * world, "nodes": args.nodes, "pods_per_replica": args.pods,
-                   "parallelism": f"replica-sharded x{world} (RCCL all-reduce of counters only)"},
+                   "parallelism": f"replica-sharded x{world} (RCCL all-reduce of counters and histograms only)"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK, "traffic": traffic,
                      "kernel": "k10s_run_kernel", "kernel_ms_per_launch": mean_kernel_ms,
