@@ -91,7 +91,9 @@ def cpu_baseline(args, cfg, cluster, workload, params):
               f"seed-perturbed), each run ~{args.cpu_seconds:.0f}s of wall time from t=0; "
               f"{sum(r[0] for r in res)} placements, {sum(r[2] for r in res)} events in total")
     return {"value": rate, "unit": "placements/s", "cores": workers, "kind": "port", "sample": sample,
-            "per_core_placements_per_s": rate / workers}
+            "per_core_placements_per_s": rate / workers,
+            "attempts_per_s": sum(a / w for _, a, _, w, _ in res),
+            "events_per_s": sum(e / w for _, _, e, w, _ in res)}
 
 
 def main():
@@ -214,6 +216,7 @@ def main():
                      "touched_bytes_per_launch": touched_bytes,
                      "touched_GBps": touched_bytes / (mean_kernel_ms * 1e-3) / 1e9},
         "engine": version(),
+        "rates": {"placements_per_s": value, "attempts_per_s": attempts / elapsed, "events_per_s": events / elapsed},
         "totals": {"placements": placements, "attempts": attempts, "events": events, "nodes_scanned": scanned,
                    "nodes_read": nread,
                    "replica_status": {str(k): v for k, v in statuses.items()}, "replica_errors": errors},
