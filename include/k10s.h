@@ -242,6 +242,16 @@ typedef struct k10s_engine k10s_engine;
  * and perturb = 0).  caps may be NULL.  Returns NULL on failure (k10s_last_error). */
 k10s_engine* k10s_engine_create(const char* scenario_text, const k10s_replica_params* params,
                                 uint32_t n_replicas, const k10s_capacities* caps, int32_t device);
+/* Same as k10s_engine_create, plus a bulk block of create_pod workload events as a binary SoA blob
+   (large traces without one text line per pod; the host converter is
+   kubernetriks_amd/scenario.py:pods_blob).  Layout, little-endian:
+     "K10SPOD1" | u64 n | f64 ts[n] | u32 cpu[n] | u32 pad (n odd) | u64 ram[n] | f64 duration[n]
+     (NaN = long-running) | u32 name_off[n + 1] | name bytes[name_off[n]]
+   The events are appended after the text's workload lines, in blob order (= trace position for
+   the stable timestamp sort, generic.rs:78-107, and for seed perturbation). */
+k10s_engine* k10s_engine_create_bulk(const char* scenario_text, const void* pods_blob, uint64_t blob_len,
+                                     const k10s_replica_params* params, uint32_t n_replicas,
+                                     const k10s_capacities* caps, int32_t device);
 void k10s_engine_destroy(k10s_engine* e);
 
 /* Scenario-derived defaults for replica parameters. */

@@ -126,8 +126,52 @@ BModel model(const std::string& s) {
 
 }  // namespace
 
+// Bulk create_pod events (k10s_engine_create_bulk): a little-endian SoA blob
+//   "K10SPOD1" | u64 n | f64 ts[n] | u32 cpu[n] | u32 pad if n odd | u64 ram[n] | f64 dur[n] (NaN: none)
+//   | u32 name_off[n + 1] | name bytes[name_off[n]]
+// Each entry becomes the same BTrace a "workload <ts> create_pod <name> <cpu> <ram> <dur|none>" line
+// would, so the compiled scenario is identical to the all-text one.
+static void parse_bulk_pods(const uint8_t* b, uint64_t len, std::vector<BTrace>& workload) {
+    uint64_t at = 0;
+    auto need = [&](uint64_t bytes) {
+        if (bytes > len || at > len - bytes) throw std::runtime_error("bulk pod blob truncated");
+    };
+    need(16);
+    if (std::memcmp(b, "K10SPOD1", 8) != 0) throw std::runtime_error("bulk pod blob: bad magic");
+    uint64_t n;
+    std::memcpy(&n, b + 8, 8);
+    at = 16;
+    if (n > (1ull << 32)) throw std::runtime_error("bulk pod blob: too many pods");
+    const uint64_t o_ts = at, o_cpu = o_ts + 8 * n, o_ram = o_cpu + 4 * n + 4 * (n & 1), o_dur = o_ram + 8 * n,
+                   o_off = o_dur + 8 * n, o_chr = o_off + 4 * (n + 1);
+    at = 0;
+    need(o_chr);
+    at = o_off;
+    std::vector<uint32_t> off(n + 1);
+    std::memcpy(off.data(), b + o_off, 4 * (n + 1));
+    at = o_chr;
+    need(off[n]);
+    for (uint64_t i = 0; i < n; i++) {
+        if (off[i] > off[i + 1] || off[i + 1] > off[n]) throw std::runtime_error("bulk pod blob: bad name offsets");
+        BTrace t;
+        std::memcpy(&t.ts, b + o_ts + 8 * i, 8);
+        std::memcpy(&t.cpu, b + o_cpu + 4 * i, 4);
+        std::memcpy(&t.ram, b + o_ram + 8 * i, 8);
+        double d;
+        std::memcpy(&d, b + o_dur + 8 * i, 8);
+        t.has_dur = d == d;
+        if (t.has_dur) t.dur = d;
+        t.kind = K10S_EV_AS_CREATE_POD_REQ;
+        t.name.assign(reinterpret_cast<const char*>(b + o_chr + off[i]), off[i + 1] - off[i]);
+        if (t.name.empty() || t.name.find_first_of(" \t\r\n#") != std::string::npos)
+            throw std::runtime_error("bulk pod blob: invalid pod name");
+        t.pos = (uint32_t)workload.size();
+        workload.push_back(t);
+    }
+}
+
 bool build_scenario(const std::string& text, uint32_t group_bound_in, uint32_t ca_bound_in, HostScenario& hs,
-                    std::string& err) {
+                    std::string& err, const uint8_t* bulk, uint64_t bulk_len) {
     try {
         Params& d = hs.defaults;
         std::memset(&d, 0, sizeof d);
@@ -282,6 +326,7 @@ bool build_scenario(const std::string& text, uint32_t group_bound_in, uint32_t c
             }
         }
         if (!header) throw std::runtime_error("empty scenario");
+        if (bulk) parse_bulk_pods(bulk, bulk_len, workload);
         if (hs.ca_enabled && cagroups.empty()) throw std::runtime_error("node groups cannot be empty for CA");
 
         auto by_ts = [](const BTrace& a, const BTrace& b) { return a.ts < b.ts; };

@@ -58,8 +58,10 @@ struct HostScenario {
 
 // Parse + compile.  group_bound / ca_bound: 0 = derive.  Returns false with a message on
 // malformed or unsupported input.
+// `bulk` / `bulk_len`: optional K10S_PODS_MAGIC blob of create_pod workload events (include/k10s.h,
+// k10s_engine_create_bulk), appended after the text's workload lines in blob order.
 bool build_scenario(const std::string& text, uint32_t group_bound, uint32_t ca_bound, HostScenario& out,
-                    std::string& err);
+                    std::string& err, const uint8_t* bulk = nullptr, uint64_t bulk_len = 0);
 
 // Point a device-side Scenario view at arrays laid out by `pack_scenario` in one buffer.
 // pack_scenario returns the byte image; the Scenario's pointers are offsets relative to `base`.

@@ -226,6 +226,12 @@ int32_t k10s_scheduler_schedule(k10s_scheduler* s, const uint32_t* alloc_cpu, co
 
 k10s_engine* k10s_engine_create(const char* scenario_text, const k10s_replica_params* params, uint32_t n_replicas,
                                 const k10s_capacities* caps, int32_t device) {
+    return k10s_engine_create_bulk(scenario_text, nullptr, 0, params, n_replicas, caps, device);
+}
+
+k10s_engine* k10s_engine_create_bulk(const char* scenario_text, const void* pods_blob, uint64_t blob_len,
+                                     const k10s_replica_params* params, uint32_t n_replicas,
+                                     const k10s_capacities* caps, int32_t device) {
     if (!scenario_text || n_replicas == 0) {
         set_err(K10S_E_INVALID, "scenario_text is NULL or n_replicas == 0");
         return nullptr;
@@ -246,7 +252,8 @@ k10s_engine* k10s_engine_create(const char* scenario_text, const k10s_replica_pa
     e->device = device;
     e->R = n_replicas;
     std::string err;
-    if (!build_scenario(scenario_text, c.group_name_bound, c.ca_name_bound, e->hs, err)) {
+    if (!build_scenario(scenario_text, c.group_name_bound, c.ca_name_bound, e->hs, err,
+                        static_cast<const uint8_t*>(pods_blob), blob_len)) {
         set_err(K10S_E_INVALID, "scenario: " + err);
         delete e;
         return nullptr;

@@ -252,6 +252,10 @@ def lib():
         L.k10s_engine_create.argtypes = [ctypes.c_char_p, ctypes.POINTER(ReplicaParams), ctypes.c_uint32,
                                          ctypes.POINTER(Capacities), ctypes.c_int32]
         L.k10s_engine_destroy.argtypes = [ctypes.c_void_p]
+        L.k10s_engine_create_bulk.restype = ctypes.c_void_p
+        L.k10s_engine_create_bulk.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64,
+                                              ctypes.POINTER(ReplicaParams), ctypes.c_uint32,
+                                              ctypes.POINTER(Capacities), ctypes.c_int32]
         L.k10s_engine_reset.argtypes = [ctypes.c_void_p]
         L.k10s_engine_reset.restype = ctypes.c_int32
         L.k10s_engine_run.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
@@ -282,7 +286,8 @@ class Engine(EngineBase):
     """A batch of independent kubernetriks replicas on one MI355X (one wavefront per replica)."""
 
     def __init__(self, scenario: str, n_replicas: int, params: Optional[Sequence[ReplicaParams]] = None,
-                 caps: Optional[Capacities] = None, device: int = 0):
+                 caps: Optional[Capacities] = None, device: int = 0, pods_blob: Optional[bytes] = None):
+        """pods_blob: optional binary create_pod block (scenario.scenario_bulk / k10s_engine_create_bulk)."""
         L = lib()
         self._L = L
         self._fn = _decl(L, "k10s_engine_")
@@ -290,7 +295,9 @@ class Engine(EngineBase):
         parr = None
         if params is not None:
             parr = (ReplicaParams * n_replicas)(*params)
-        h = L.k10s_engine_create(scenario.encode(), parr, n_replicas, ctypes.byref(caps) if caps else None, device)
+        blob = pods_blob or b""
+        h = L.k10s_engine_create_bulk(scenario.encode(), blob if pods_blob else None, len(blob), parr, n_replicas,
+                                      ctypes.byref(caps) if caps else None, device)
         if not h:
             raise RuntimeError("k10s_engine_create failed: " + L.k10s_last_error().decode())
         self._h = h

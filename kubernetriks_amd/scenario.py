@@ -460,3 +460,34 @@ def scenario_text(config: SimulationConfig, cluster: GenericClusterTrace, worklo
                          f"{_model_token(g.cpu_model)} {_model_token(g.ram_model)}")
     lines.append("end")
     return "\n".join(lines) + "\n"
+
+
+def pods_blob(pods: Sequence[Tuple[float, "Pod"]]) -> bytes:
+    """Binary SoA block of create_pod events for k10s_engine_create_bulk (include/k10s.h): ts f64,
+    cpu u32, ram u64, duration f64 (NaN = long-running), names as one offset table + bytes.  Pods
+    with labels must go through the text format."""
+    import numpy as np
+    n = len(pods)
+    ts = np.array([float(t) for t, _ in pods], dtype="<f8")
+    cpu = np.array([int(p.cpu) for _, p in pods], dtype="<u4")
+    ram = np.array([int(p.ram) for _, p in pods], dtype="<u8")
+    dur = np.array([math.nan if p.duration is None else float(p.duration) for _, p in pods], dtype="<f8")
+    names = [_check_name(p.name).encode() for _, p in pods]
+    if any(p.labels for _, p in pods):
+        raise ValueError("pods with labels are not supported in the bulk blob")
+    off = np.zeros(n + 1, dtype="<u4")
+    off[1:] = np.cumsum([len(b) for b in names], dtype=np.uint64)
+    pad = b"\0" * (4 * (n & 1))
+    return (b"K10SPOD1" + np.array([n], dtype="<u8").tobytes() + ts.tobytes() + cpu.tobytes() + pad +
+            ram.tobytes() + dur.tobytes() + off.tobytes() + b"".join(names))
+
+
+def scenario_bulk(config: SimulationConfig, cluster: GenericClusterTrace,
+                  workload: GenericWorkloadTrace) -> Tuple[str, bytes]:
+    """(scenario text, pods blob) for k10s_engine_create_bulk: the workload's create_pod events go
+    into the binary blob, everything else stays text.  The engine appends the blob after the text's
+    workload lines, so the result equals scenario_text(...) when the create_pod events come last in
+    the workload trace (e.g. a pure pod trace)."""
+    pods = [(e.timestamp, e.pod) for e in workload.events if e.kind == "create_pod"]
+    rest = GenericWorkloadTrace([e for e in workload.events if e.kind != "create_pod"])
+    return scenario_text(config, cluster, rest), pods_blob(pods)

@@ -38,14 +38,21 @@ static Ctx make_ctx(HC* h, uint32_t r, RepHdr* work) {
 
 extern "C" {
 
+void* hc_create_bulk(const char* text, const void* blob, uint64_t blob_len, const k10s_replica_params* params,
+                     uint32_t R, const k10s_capacities* caps, char* err, int errlen);
 void* hc_create(const char* text, const k10s_replica_params* params, uint32_t R, const k10s_capacities* caps,
                 char* err, int errlen) {
+    return hc_create_bulk(text, nullptr, 0, params, R, caps, err, errlen);
+}
+void* hc_create_bulk(const char* text, const void* blob, uint64_t blob_len, const k10s_replica_params* params,
+                     uint32_t R, const k10s_capacities* caps, char* err, int errlen) {
     HC* h = new HC();
     std::string e;
     k10s_capacities c;
     std::memset(&c, 0, sizeof c);
     if (caps) c = *caps;
-    if (!build_scenario(text, c.group_name_bound, c.ca_name_bound, h->hs, e)) {
+    if (!build_scenario(text, c.group_name_bound, c.ca_name_bound, h->hs, e, static_cast<const uint8_t*>(blob),
+                        blob_len)) {
         if (err) std::snprintf(err, (size_t)errlen, "%s", e.c_str());
         delete h;
         return nullptr;

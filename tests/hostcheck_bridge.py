@@ -28,6 +28,9 @@ def lib():
         L.hc_create.restype = ctypes.c_void_p
         L.hc_create.argtypes = [ctypes.c_char_p, ctypes.POINTER(ReplicaParams), ctypes.c_uint32,
                                 ctypes.POINTER(Capacities), ctypes.c_char_p, ctypes.c_int]
+        L.hc_create_bulk.restype = ctypes.c_void_p
+        L.hc_create_bulk.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.POINTER(ReplicaParams),
+                                     ctypes.c_uint32, ctypes.POINTER(Capacities), ctypes.c_char_p, ctypes.c_int]
         L.hc_free.argtypes = [ctypes.c_void_p]
         L.hc_run.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_uint64]
         L.hc_run.restype = ctypes.c_int
@@ -37,14 +40,16 @@ def lib():
 
 class HostEngine(EngineBase):
     def __init__(self, scenario: str, n_replicas: int = 1, params: Optional[Sequence[ReplicaParams]] = None,
-                 caps: Optional[Capacities] = None):
+                 caps: Optional[Capacities] = None, pods_blob: Optional[bytes] = None):
         L = lib()
         self._L = L
         self._fn = _decl(L, "hc_")
         self.n_replicas = n_replicas
         parr = (ReplicaParams * n_replicas)(*params) if params is not None else None
         err = ctypes.create_string_buffer(512)
-        h = L.hc_create(scenario.encode(), parr, n_replicas, ctypes.byref(caps) if caps else None, err, 512)
+        blob = pods_blob or b""
+        h = L.hc_create_bulk(scenario.encode(), blob if pods_blob else None, len(blob), parr, n_replicas,
+                             ctypes.byref(caps) if caps else None, err, 512)
         if not h:
             raise ValueError("hostcheck rejected scenario: " + err.value.decode())
         self._h = h

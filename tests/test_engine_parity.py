@@ -360,3 +360,45 @@ def test_score_batch_bit_exact(weight):
     assert nan_e[0] and nan_e.sum() >= 1
     bad = np.nonzero(got[~nan_e].view(np.uint64) != exp[~nan_e].view(np.uint64))[0]
     assert bad.size == 0, (bad[:5], got[~nan_e][bad[:5]], exp[~nan_e][bad[:5]])
+
+
+# ---- binary create_pod block (k10s_engine_create_bulk) --------------------------
+def _bulk_pair(engine_cls, **kw):
+    from kubernetriks_amd.scenario import scenario_bulk
+    cfg = SimulationConfig()
+    c, w = wl.c3_traces(n_nodes=48, n_pods=400, arrival_window=120.0, seed=5)
+    text = scenario_text(cfg, c, w)
+    btext, blob = scenario_bulk(cfg, c, w)
+    assert "create_pod " not in btext and blob[:8] == b"K10SPOD1"
+    R = 3
+    caps = parity.parity_caps(log=True)
+    a = engine_cls(text, R, caps=caps, **kw)
+    b = engine_cls(btext, R, caps=caps, pods_blob=blob, **kw)
+    for e in (a, b):
+        e.run_until_all_finished(1e7)
+    for r in range(R):
+        assert a.results()[r] == b.results()[r] or repr(a.results()[r]) == repr(b.results()[r]), r
+        assert a.placements(r) == b.placements(r)
+        assert a.event_log(r) == b.event_log(r)
+    assert a.results()[0]["counters"]["placements"] == 400
+    return a, b
+
+
+def test_bulk_pod_blob_equals_text_host():
+    _bulk_pair(HostEngine)
+
+
+def test_bulk_pod_blob_rejects_malformed():
+    from kubernetriks_amd.scenario import scenario_bulk
+    cfg = SimulationConfig()
+    c, w = wl.c3_traces(n_nodes=4, n_pods=10, arrival_window=10.0, seed=1)
+    btext, blob = scenario_bulk(cfg, c, w)
+    for bad in (blob[:-3], b"K10SPODX" + blob[8:], blob[:16]):
+        with pytest.raises(ValueError):
+            HostEngine(btext, 1, pods_blob=bad)
+
+
+@pytest.mark.gpu
+def test_bulk_pod_blob_equals_text_gpu():
+    from kubernetriks_amd.native import Engine
+    _bulk_pair(Engine)
