@@ -112,20 +112,21 @@ def main():
     from kubernetriks_amd import ensemble
     from kubernetriks_amd import workloads as wl
     from kubernetriks_amd.native import NUM_COUNTERS, Capacities, Engine, version
-    from kubernetriks_amd.scenario import SimulationConfig, scenario_text
+    from kubernetriks_amd.scenario import SimulationConfig, scenario_bulk
 
     cfg = SimulationConfig()
     cluster, workload = wl.c3_traces(args.nodes, args.pods, args.arrival_window)
-    scn = scenario_text(cfg, cluster, workload)
+    # cluster trace as text, the 16k create_pod events as the binary block (k10s_engine_create_bulk)
+    scn, blob = scenario_bulk(cfg, cluster, workload)
     R = args.replicas
-    probe = Engine(scn, 1, device=local_rank)
+    probe = Engine(scn, 1, device=local_rank, pods_blob=blob)
     defaults = probe.default_params()
     probe.close()
     params = ensemble.shard_params(defaults, R, rank, base_seed=123, perturb=True)  # replicas [rank*R, (rank+1)*R)
     t = time.perf_counter()
     caps = Capacities()
     caps.pruned_scan = 1 if args.pruned_scan else 0
-    eng = Engine(scn, R, params=params, caps=caps, device=local_rank)
+    eng = Engine(scn, R, params=params, caps=caps, device=local_rank, pods_blob=blob)
     log(f"[rank {rank}] engine: {R} replicas x {eng.replica_bytes / 2**20:.1f} MiB, init {time.perf_counter() - t:.2f}s")
 
     def one_step():
