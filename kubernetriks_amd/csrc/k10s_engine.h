@@ -663,7 +663,7 @@ K10S_D double la_score_d(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr) {
 // the score_key order, NaN never compares true (= "NaN is never selected"), and -inf as the start
 // value accepts the first non-NaN score like score_key's 0.  W1: weight == 1.0, where 0.0 + s·1.0
 // is the identity on scores >= +0 and NaN.
-template <bool W1>
+template <bool W1, bool TF>
 K10S_D void scan_node_d(uint32_t n, bool present, uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr, double frc,
                         double frr, double weight, int32_t& first, double& best_s, int32_t& best_n) {
 #if K10S_SCAN_BF
@@ -685,7 +685,7 @@ K10S_D void scan_node_d(uint32_t n, bool present, uint32_t ac, uint64_t ar, uint
     best_n = take ? (int32_t)n : best_n;
 #else
     if (rc <= ac && rr <= ar && present) {
-        first = (int32_t)n < first ? (int32_t)n : first;
+        if (TF) first = (int32_t)n < first ? (int32_t)n : first;
         const double fac = (double)ac;
         const double cs = div_rn((fac - frc) * 100.0, fac);
         const uint2 w = __builtin_bit_cast(uint2, ar);
@@ -701,18 +701,18 @@ K10S_D void scan_node_d(uint32_t n, bool present, uint32_t ac, uint64_t ar, uint
     }
 #endif
 }
-template <bool W1>
+template <bool W1, bool TF>
 K10S_D void scan_grp(const ScanGrp& g, uint32_t n0, uint32_t n_nodes, uint32_t rc, uint64_t rr, double frc,
                      double frr, double weight, int32_t& first, double& best_s, int32_t& best_n) {
     const uint32_t bits = grp_bits(g, n0, n_nodes);
     if (bits) {
-        scan_node_d<W1>(n0, bits & 1u, g.cv.x, g.r01.x, rc, rr, frc, frr, weight, first, best_s, best_n);
-        scan_node_d<W1>(n0 + 1, bits & 2u, g.cv.y, g.r01.y, rc, rr, frc, frr, weight, first, best_s, best_n);
-        scan_node_d<W1>(n0 + 2, bits & 4u, g.cv.z, g.r23.x, rc, rr, frc, frr, weight, first, best_s, best_n);
-        scan_node_d<W1>(n0 + 3, bits & 8u, g.cv.w, g.r23.y, rc, rr, frc, frr, weight, first, best_s, best_n);
+        scan_node_d<W1, TF>(n0, bits & 1u, g.cv.x, g.r01.x, rc, rr, frc, frr, weight, first, best_s, best_n);
+        scan_node_d<W1, TF>(n0 + 1, bits & 2u, g.cv.y, g.r01.y, rc, rr, frc, frr, weight, first, best_s, best_n);
+        scan_node_d<W1, TF>(n0 + 2, bits & 4u, g.cv.z, g.r23.x, rc, rr, frc, frr, weight, first, best_s, best_n);
+        scan_node_d<W1, TF>(n0 + 3, bits & 8u, g.cv.w, g.r23.y, rc, rr, frc, frr, weight, first, best_s, best_n);
     }
 }
-template <bool W1>
+template <bool W1, bool TF>
 K10S_D void scan_lanes(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
                        uint32_t rc, uint64_t rr, double weight, int32_t& first, double& best_s, int32_t& best_n) {
     const uint32_t l4 = 4u * (uint32_t)lane_id();
@@ -727,7 +727,7 @@ K10S_D void scan_lanes(const uint32_t* s_cpu, const uint64_t* s_ram, const uint6
     for (int i = 0; i < K10S_SCAN_PIPE; i++) g[i] = scan_load(s_cpu, s_ram, present, n_nodes, 256u * i + l4);
     for (uint32_t base = 0; base < n_nodes; base += 256) {
         g[K10S_SCAN_PIPE] = scan_load(s_cpu, s_ram, present, n_nodes, base + 256u * K10S_SCAN_PIPE + l4);
-        scan_grp<W1>(g[0], base + l4, n_nodes, rc, rr, frc, frr, weight, first, best_s, best_n);
+        scan_grp<W1, TF>(g[0], base + l4, n_nodes, rc, rr, frc, frr, weight, first, best_s, best_n);
 #pragma unroll
         for (int i = 0; i < K10S_SCAN_PIPE; i++) g[i] = g[i + 1];
     }
@@ -741,8 +741,19 @@ K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const ui
     int32_t first = 0x7fffffff;
 #if K10S_DEVICE
     double best_s = -__builtin_inf();
-    if (weight == 1.0) scan_lanes<true>(s_cpu, s_ram, present, n_nodes, rc, rr, weight, first, best_s, best_n);
-    else scan_lanes<false>(s_cpu, s_ram, present, n_nodes, rc, rr, weight, first, best_s, best_n);
+    if (weight == 1.0 && rc > 0 && rr > 0) {
+        // A fitting node has alloc >= request > 0 in both resources, so neither term is 0/0 and every
+        // score is a finite number >= 0: filtered[0] is never NaN, "some node fits" <=> best_n >= 0,
+        // and neither filtered[0] nor its re-scored value is needed (kube_scheduler.rs:140-148).
+        scan_lanes<true, false>(s_cpu, s_ram, present, n_nodes, rc, rr, weight, first, best_s, best_n);
+        best_key = best_n >= 0 ? score_key(best_s) : 0;
+        wave_argmax(best_key, best_n);
+        if (best_n < 0) return K10S_SCHED_NO_SUFFICIENT_RESOURCES;
+        *chosen = best_n;
+        return K10S_SCHED_OK;
+    }
+    if (weight == 1.0) scan_lanes<true, true>(s_cpu, s_ram, present, n_nodes, rc, rr, weight, first, best_s, best_n);
+    else scan_lanes<false, true>(s_cpu, s_ram, present, n_nodes, rc, rr, weight, first, best_s, best_n);
     best_key = best_n >= 0 ? score_key(best_s) : 0;
 #else
     for (uint32_t n = 0; n < n_nodes; n++)
