@@ -1,0 +1,147 @@
+"""Binary SoA pod traces at scale.
+
+A pod trace of tens of millions of Alibaba instances is too large to go through per-event Python
+objects and the ``k10s_scenario 1`` text.  This module streams the Alibaba v2017 CSVs straight into
+the engine's binary create_pod block (``K10SPOD1``, ``include/k10s.h`` /
+``scenario.pods_blob``), column by column, and decodes such a block back into numpy columns.
+
+Semantics follow ``AlibabaWorkloadTraceV2017`` in the reference:
+  * row filtering, pod naming ``{job}_{task}_{pod_no}``, cpu ``santicores * 10`` truncated to u32,
+    ram ``normalized * 128 GiB`` as a saturating ``f64 as u64``, duration ``end - start``
+    (src/trace/alibaba_cluster_trace_v2017/workload.rs:56-120);
+  * the events are stable-sorted by start timestamp (workload.rs:140), so the block is sorted;
+  * duplicated task ids are an error (workload.rs:160-161).
+The result is byte-identical to ``scenario.pods_blob`` over the stable-sorted events of
+``scenario.alibaba_workload_trace_from_csv`` (tests/test_trace_soa.py).
+"""
+from __future__ import annotations
+
+import csv
+import io
+from array import array
+from typing import Dict, Iterable, Optional, Tuple, Union
+
+import numpy as np
+
+from .scenario import DENORMALIZATION_BASE, U32_MAX, _check_name, _f64_as_u64, _opt_float, _opt_int
+
+MAGIC = b"K10SPOD1"
+_HEADER = 16
+
+
+def _tasks_from_rows(rows: Iterable[list]) -> Dict[int, Tuple[Optional[int], Optional[float]]]:
+    """read_batch_trace_from_str (workload.rs:150-166): task_id -> (cpus, normalized memory)."""
+    tasks = {}
+    for row in rows:
+        if not row:
+            continue
+        tid = int(row[3])
+        if tid in tasks:
+            raise ValueError(f"duplicated task id: {tid}")
+        tasks[tid] = (_opt_int(row[6]), _opt_float(row[7]))
+    return tasks
+
+
+def _open_text(src: Union[str, io.TextIOBase]):
+    return open(src, newline="") if isinstance(src, str) else src
+
+
+def alibaba_pods_blob(instances: Union[str, io.TextIOBase], tasks: Union[str, io.TextIOBase]) -> bytes:
+    """Stream batch_instance.csv (path or text stream) into a sorted K10SPOD1 block.
+
+    Only the task table is held as a dict; instance rows are reduced to four packed columns and the
+    name bytes as they are read, so memory is ~30 B + name length per pod."""
+    tf = _open_text(tasks)
+    try:
+        task_map = _tasks_from_rows(csv.reader(tf))
+    finally:
+        if tf is not tasks:
+            tf.close()
+    ts, cpu, ram, dur = array("d"), array("I"), array("Q"), array("d")
+    name_len = array("I")
+    names = bytearray()
+    pod_no = 0
+    f = _open_text(instances)
+    try:
+        for row in csv.reader(f):
+            if not row:
+                continue
+            start, end, job, task = _opt_int(row[0]), _opt_int(row[1]), _opt_int(row[2]), _opt_int(row[3])
+            if start is None or end is None or task is None or task not in task_map:
+                continue
+            cpu_sc, mem = task_map[task]
+            if cpu_sc is None or mem is None:
+                continue
+            if start <= 0 or end <= 0 or start >= end:
+                continue
+            if job is None:   # workload.rs:91 unwraps job_id
+                raise ValueError(f"instance of task {task} has no job id")
+            name = _check_name(f"{job}_{task}_{pod_no}").encode()
+            pod_no += 1
+            ts.append(float(start))
+            cpu.append((cpu_sc * 10) & U32_MAX)
+            ram.append(_f64_as_u64(mem * float(DENORMALIZATION_BASE)))
+            dur.append(float(end - start))
+            name_len.append(len(name))
+            names += name
+    finally:
+        if f is not instances:
+            f.close()
+    return _pack_sorted(np.frombuffer(ts, "<f8"), np.frombuffer(cpu, "<u4"), np.frombuffer(ram, "<u8"),
+                        np.frombuffer(dur, "<f8"), np.frombuffer(name_len, "<u4"), bytes(names))
+
+
+def _pack_sorted(ts, cpu, ram, dur, name_len, names: bytes) -> bytes:
+    n = ts.size
+    if len(names) > U32_MAX:
+        raise ValueError("pod names exceed the 4 GiB offset range of a K10SPOD1 block")
+    src_off = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(name_len, out=src_off[1:])
+    order = np.argsort(ts, kind="stable")                       # workload.rs:140 (stable sort_by)
+    lens = name_len[order].astype(np.int64)
+    off = np.zeros(n + 1, dtype="<u4")
+    off[1:] = np.cumsum(lens)
+    if n:
+        # gather the name bytes in sorted order: byte j of pod k comes from src_off[order[k]] + j
+        starts = np.repeat(src_off[:-1][order], lens)
+        within = np.arange(int(off[-1]), dtype=np.int64) - np.repeat(off[:-1].astype(np.int64), lens)
+        sorted_names = np.frombuffer(names, np.uint8)[starts + within].tobytes()
+    else:
+        sorted_names = b""
+    pad = b"\0" * (4 * (n & 1))
+    return (MAGIC + np.array([n], dtype="<u8").tobytes() + ts[order].tobytes() + cpu[order].tobytes() + pad +
+            ram[order].tobytes() + dur[order].tobytes() + off.tobytes() + sorted_names)
+
+
+def read_pods_blob(blob: bytes) -> dict:
+    """Decode a K10SPOD1 block into numpy columns (ts, cpu, ram, duration; NaN = long-running) and
+    the list of pod names.  Raises ValueError on a malformed block, like k10s_engine_create_bulk."""
+    if len(blob) < _HEADER or blob[:8] != MAGIC:
+        raise ValueError("not a K10SPOD1 block")
+    n = int(np.frombuffer(blob, "<u8", 1, 8)[0])
+    fixed = n * (8 + 4 + 8 + 8) + 4 * (n & 1) + 4 * (n + 1)
+    if len(blob) < _HEADER + fixed:
+        raise ValueError("truncated K10SPOD1 block")
+    p = _HEADER
+    ts = np.frombuffer(blob, "<f8", n, p); p += 8 * n
+    cpu = np.frombuffer(blob, "<u4", n, p); p += 4 * n + 4 * (n & 1)
+    ram = np.frombuffer(blob, "<u8", n, p); p += 8 * n
+    dur = np.frombuffer(blob, "<f8", n, p); p += 8 * n
+    off = np.frombuffer(blob, "<u4", n + 1, p); p += 4 * (n + 1)
+    if off[0] != 0 or np.any(np.diff(off.astype(np.int64)) < 0) or p + int(off[-1]) != len(blob):
+        raise ValueError("bad name offsets in K10SPOD1 block")
+    raw = blob[p:]
+    names = [raw[off[i]:off[i + 1]].decode() for i in range(n)]
+    return {"ts": ts, "cpu": cpu, "ram": ram, "duration": dur, "names": names}
+
+
+def write_pods_blob(path: str, blob: bytes) -> None:
+    with open(path, "wb") as f:
+        f.write(blob)
+
+
+def load_pods_blob(path: str) -> bytes:
+    with open(path, "rb") as f:
+        blob = f.read()
+    read_pods_blob(blob)   # validate
+    return blob
