@@ -145,3 +145,35 @@ def load_pods_blob(path: str) -> bytes:
         blob = f.read()
     read_pods_blob(blob)   # validate
     return blob
+
+
+def _splitmix64(x: np.ndarray) -> np.ndarray:
+    """workloads.splitmix64 over a uint64 column (wrapping arithmetic)."""
+    x = x + np.uint64(0x9E3779B97F4A7C15)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def perturb_pods_blob(blob: bytes, seed: int, key_offset: int = 0) -> bytes:
+    """Column-wise restatement of the engine's per-replica perturb_pod (k10s_engine.h,
+    workloads.perturb_pod) over a K10SPOD1 block: pod k gets key ``key_offset + k`` (its position in
+    the replica's workload events).  Materialises one replica's perturbed trace as a block."""
+    d = read_pods_blob(blob)
+    n = d["ts"].size
+    key = np.arange(n, dtype=np.uint64) + np.uint64(key_offset)
+    u = _splitmix64(np.uint64(seed & 0xFFFFFFFFFFFFFFFF) ^ (np.uint64(0xD1B54A32D192ED03) * (key + np.uint64(1))))
+    kd = (np.uint64(8) + u % np.uint64(17)).astype(np.float64)
+    kc = np.uint64(12) + (u >> np.uint64(20)) % np.uint64(9)
+    kr = np.uint64(12) + (u >> np.uint64(40)) % np.uint64(9)
+    dur = (d["duration"] * kd) * 0.0625                          # NaN (long-running) stays NaN
+    cpu = ((d["cpu"].astype(np.uint64) * kc) >> np.uint64(4)).astype("<u4")
+    ram = ((d["ram"] >> np.uint64(4)) * kr).astype("<u8")
+    p_cpu = _HEADER + 8 * n
+    p_ram = p_cpu + 4 * n + 4 * (n & 1)
+    p_dur = p_ram + 8 * n
+    out = bytearray(blob)
+    out[p_cpu:p_cpu + 4 * n] = cpu.tobytes()
+    out[p_ram:p_ram + 8 * n] = ram.tobytes()
+    out[p_dur:p_dur + 8 * n] = dur.astype("<f8").tobytes()
+    return bytes(out)

@@ -121,3 +121,20 @@ def test_streamed_blob_runs_like_text(backend):
         assert a.placements(r) == b.placements(r)
         assert a.event_log(r) == b.event_log(r)
     assert a.results()[0]["counters"]["placements"] > 0
+
+
+def test_perturb_blob_matches_perturb_pod():
+    import math
+    from kubernetriks_amd.scenario import Pod
+    rng = random.Random(9)
+    pods = [(float(rng.randint(0, 99)), Pod(f"p{i}", rng.choice([0, 1, 1000, 2 ** 32 - 1]),
+                                            rng.choice([0, 15, 2 ** 64 - 1, rng.getrandbits(40)]),
+                                            None if i % 7 == 0 else rng.random() * 1e4)) for i in range(301)]
+    blob = pods_blob(pods)
+    for seed, off in ((123, 0), (2 ** 64 - 1, 17)):
+        d = trace_soa.read_pods_blob(trace_soa.perturb_pods_blob(blob, seed, off))
+        for k, (_, p) in enumerate(pods):
+            cpu, ram, dur = wl.perturb_pod(seed, off + k, p.cpu, p.ram, p.duration)
+            assert (int(d["cpu"][k]), int(d["ram"][k])) == (cpu, ram), k
+            got = float(d["duration"][k])
+            assert (dur is None and math.isnan(got)) or got == dur, k
