@@ -1,26 +1,38 @@
 #!/usr/bin/env python3
 """Benchmark: pod placements/sec of the MI355X batched-ensemble engine on 4k-node clusters.
 
-Workload (BASELINE.json configs[2] shape, the metric's "4k-node clusters"): C3 — every GPU runs
-R replicas (default 8,192) of a 4,096-node Alibaba-like cluster, each replica a seed-perturbed copy
-of one synthetic 16,384-pod Alibaba-like trace (integer arrival seconds); a step simulates every
-replica from initialize() until RunUntilAllPodsAreFinished stops it.  Replicas are sharded over
-ranks with distinct seeds (weak scaling: R per GPU); the only collective is one RCCL all-reduce of
-the counter vector per measurement (the reference has no data-path exchange).
+Workloads (BASELINE.json configs[2] shape, the metric's "4k-node clusters"):
+  c3          every GPU runs R replicas (default 8,192) of a 4,096-node Alibaba-like cluster, each a
+              seed-perturbed copy of one synthetic 16,384-pod Alibaba-like trace (integer arrival
+              seconds, notebook statistics); light load, every attempt places its pod.
+  c3_backlog  the same cluster under load (rho ~ 1 of the RAM-bound capacity):
+              pods of 0.3-0.5 of a node's RAM staying ~1,200 s, so attempts fail, pods wait in the
+              unschedulable map, are moved back on every pod finish and flushed after 300 s.
+A step simulates every replica from initialize() until RunUntilAllPodsAreFinished stops it.
+Replicas are sharded over ranks with distinct seeds (weak scaling: R per GPU); nothing is exchanged
+while they run; at the end one RCCL all-reduce of the int64 counter vector (+ the estimator rows and
+histograms, all-gathered / all-reduced) combines them.
+
+`python bench.py --gpus N`: with N > 1 and no WORLD_SIZE in the environment this process (which has
+not touched the GPU) starts N rank processes of itself with RANK/LOCAL_RANK/WORLD_SIZE set, one per
+GPU, and exits with their status; under torch.distributed.run WORLD_SIZE must equal N.
 
 Prints ONE JSON line (rank 0).  `value` = placements of all ranks / max-over-ranks wall time of
 the timed steps.  `roofline`: the dominant kernel is k10s_run_kernel (the whole event loop incl. the
 scheduling scans); algorithmic bytes per launch = Σ_attempts (12·|node cache| + 12) + 12·placements
 (SURVEY.md §8(d)), divided by the launch's HIP-event time, against the 8 TB/s HBM3E peak.
 `cpu_baseline`: the repo's CPU oracle (a string-keyed restatement of the reference, kind "port";
-the Rust reference cannot be built here) on a bounded sample of the same workload, one process
-per core.
+the Rust reference cannot be built here), one process per usable host core, each running one
+replica of the same workload to completion.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,6 +40,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK = 8.0e12  # MI355X HBM3E peak, MI355X_MICROARCH.md "Chip-level parameters"
+METRIC = "pod placements/sec (whole node, 1/2/4/8 GPUs) at 4k-node clusters; % HBM roofline"
 
 
 def log(*a):
@@ -39,98 +52,201 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", choices=("c3", "c3_backlog"), default="c3")
     ap.add_argument("--replicas", type=int, default=8192, help="replicas per GPU")
     ap.add_argument("--nodes", type=int, default=4096)
     ap.add_argument("--pods", type=int, default=16384)
     ap.add_argument("--arrival-window", type=float, default=1200.0)
     ap.add_argument("--budget", type=int, default=0, help="max events per replica per launch (0 = one launch)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-workers", type=int, default=0, help="0 = min(16, cores)")
+    ap.add_argument("--cpu-seconds", type=float, default=90.0,
+                    help="wall-time cap per CPU-baseline replica (a replica that hits it is extrapolated)")
+    ap.add_argument("--cpu-workers", type=int, default=0, help="0 = the usable host cores (cgroup quota / affinity)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scan-kernel", action="store_true", help="skip the scheduling-kernel-alone measurement")
     ap.add_argument("--pruned-scan", action="store_true", help="exact block-bound pruned scan (DESIGN.md §3)")
     ap.add_argument("--profile", action="store_true", help="print the K10S_PROF cycle attribution (variant builds)")
+    ap.add_argument("--selftest-host", action="store_true",
+                    help="TEST ONLY: run the launcher and the cross-rank reduction on CPU (gloo) over the "
+                         "test-only host-check build; the numbers are not a measurement")
     return ap.parse_args()
 
 
+# ---- N-rank launcher ---------------------------------------------------------------------------
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """Start n rank processes of this script (one per GPU) and return the worst exit status.  The
+    parent never initialises the GPU (an exec/fork after GPU init is unsafe), it only waits."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        log(f"[launcher] rank exit codes {rcs}")
+    return bad[0] if bad else 0
+
+
+# ---- CPU baseline (oracle, one process per usable core) -----------------------------------------
+def host_cores():
+    """(usable cores, description): the cgroup CPU quota when there is one, else the affinity set."""
+    nproc = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(math.ceil(int(q) / int(period))))
+    except (OSError, ValueError):
+        pass
+    usable = min(aff, quota) if quota else aff
+    return usable, {"nproc": nproc, "affinity": aff, "cgroup_cpu_quota": quota}
+
+
 def cpu_worker(args_tuple):
-    """One core: the oracle on one replica's materialized trace for ~`seconds` of wall time."""
-    scn, seconds = args_tuple
+    """One core: the oracle runs one replica's materialized trace from t=0 until
+    RunUntilAllPodsAreFinished (or the wall cap)."""
+    scn, cap = args_tuple
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_bridge as ob
     o = ob.OracleSim(scn)
     t0 = time.perf_counter()
+    done = False
     t_sim = 0.0
-    while time.perf_counter() - t0 < seconds:
-        t_sim += 20.0
+    while time.perf_counter() - t0 < cap:
+        t_sim += 100.0
         o.step_until_time(t_sim)
         r = o.result()
-        if r["panicked"] or t_sim > 1e6:
+        if r["panicked"] or r["counters"]["terminated_pods"] >= r["counters"]["total_pods_in_trace"]:
+            done = True
             break
-        if r["counters"]["terminated_pods"] >= r["counters"]["total_pods_in_trace"]:
+        if t_sim > 1e7:
             break
+    if done:  # finish exactly as the engine does (the %1000 stop rule)
+        o.run_until_all_finished(1e7)
     wall = time.perf_counter() - t0
-    c = o.result()["counters"]
-    return c["placements"], c["attempts"], c["events"], wall, t_sim
+    r = o.result()
+    c = r["counters"]
+    return c["placements"], c["attempts"], c["events"], wall, r["time"], done, c["terminated_pods"], \
+        c["total_pods_in_trace"]
 
 
 def cpu_baseline(args, cfg, cluster, workload, params):
     from multiprocessing import get_context
     from kubernetriks_amd import workloads as wl
     from kubernetriks_amd.scenario import scenario_text
-    workers = args.cpu_workers or min(16, os.cpu_count() or 1)
-    jobs = [(scenario_text(cfg, cluster, wl.perturb_workload(workload, params[i].seed)), args.cpu_seconds)
+    usable, cores_info = host_cores()
+    workers = args.cpu_workers or usable
+    jobs = [(scenario_text(cfg, cluster, wl.perturb_workload(workload, params[i % len(params)].seed)), args.cpu_seconds)
             for i in range(workers)]
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_bridge as ob
     ob.build_oracle()
     with get_context("fork").Pool(workers) as pool:
         res = pool.map(cpu_worker, jobs)
-    rate = sum(p / w for p, _, _, w, _ in res)
-    sample = (f"{workers} processes x 1 replica of the same C3 workload ({args.nodes} nodes, {args.pods} pods, "
-              f"seed-perturbed), each run ~{args.cpu_seconds:.0f}s of wall time from t=0; "
-              f"{sum(r[0] for r in res)} placements, {sum(r[2] for r in res)} events in total")
+    rate = sum(p / w for p, _, _, w, *_ in res)
+    n_done = sum(1 for r in res if r[5])
+    horizon = max(r[4] for r in res)
+    frac = sum(r[6] / max(r[7], 1) for r in res) / len(res)
+    how = ("each run from t=0 to RunUntilAllPodsAreFinished (the whole simulated horizon, up to "
+           f"t={horizon:.0f} s)") if n_done == len(res) else \
+        (f"{n_done}/{len(res)} run to RunUntilAllPodsAreFinished, the others stopped at the {args.cpu_seconds:.0f} s "
+         f"wall cap (on average {100 * frac:.0f}% of the pods terminated; their rate is extrapolated from that prefix)")
+    sample = (f"{workers} processes (host: nproc {cores_info['nproc']}, affinity {cores_info['affinity']}, "
+              f"cgroup CPU quota {cores_info['cgroup_cpu_quota']}) x 1 seed-perturbed replica each of the same "
+              f"{args.workload} workload ({args.nodes} nodes, {args.pods} pods), {how}; "
+              f"{sum(r[0] for r in res)} placements, {sum(r[1] for r in res)} attempts, "
+              f"{sum(r[2] for r in res)} events in total")
     return {"value": rate, "unit": "placements/s", "cores": workers, "kind": "port", "sample": sample,
+            "host": cores_info, "replicas_completed": n_done,
             "per_core_placements_per_s": rate / workers,
-            "attempts_per_s": sum(a / w for _, a, _, w, _ in res),
-            "events_per_s": sum(e / w for _, _, e, w, _ in res)}
+            "attempts_per_s": sum(a / w for _, a, _, w, *_ in res),
+            "events_per_s": sum(e / w for _, _, e, w, *_ in res)}
+
+
+# ---- the measurement ------------------------------------------------------------------------------
+def build_workload(args):
+    from kubernetriks_amd import workloads as wl
+    if args.workload == "c3_backlog":
+        cluster, workload = wl.c3_backlog_traces(args.nodes, args.pods, args.arrival_window)
+        desc = (f"C3 backlog: {args.replicas} replicas/GPU x {args.nodes}-node Alibaba-like cluster, {args.pods} pods/replica "
+                "of 0.3-0.5 node RAM for ~1200 s (rho ~ 1: failed attempts, unschedulable map, move-all on pod "
+                "finish, 300-s flush), run until all pods finished (RunUntilAllPodsAreFinished)")
+    else:
+        cluster, workload = wl.c3_traces(args.nodes, args.pods, args.arrival_window)
+        desc = (f"C3: {args.replicas} replicas/GPU x {args.nodes}-node Alibaba-like cluster, {args.pods} pods/replica, "
+                "run until all pods finished (RunUntilAllPodsAreFinished)")
+    return cluster, workload, desc
 
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        log(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
     import torch
     import torch.distributed as dist
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
-    torch.cuda.set_device(local_rank)
 
-    from kubernetriks_amd.build import build
-    build()
     from kubernetriks_amd import ensemble
-    from kubernetriks_amd import workloads as wl
-    from kubernetriks_amd.native import NUM_COUNTERS, Capacities, Engine, version
+    from kubernetriks_amd.native import NUM_COUNTERS, Capacities
     from kubernetriks_amd.scenario import SimulationConfig, scenario_bulk
 
+    if args.selftest_host:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        from hostcheck_bridge import HostEngine as EngineCls  # test-only build, no GPU
+        backend, version = "gloo", (lambda: "host-check selftest (not a measurement)")
+
+        def make_engine(scn, R, params=None, caps=None, blob=None):
+            return EngineCls(scn, R, params=params, caps=caps, pods_blob=blob)
+    else:
+        from kubernetriks_amd.build import build
+        build()
+        from kubernetriks_amd.native import Engine, version
+        backend = "nccl"
+        torch.cuda.set_device(local_rank)
+
+        def make_engine(scn, R, params=None, caps=None, blob=None):
+            return Engine(scn, R, params=params, caps=caps, device=local_rank, pods_blob=blob)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+        else:
+            dist.init_process_group("gloo")
+
     cfg = SimulationConfig()
-    cluster, workload = wl.c3_traces(args.nodes, args.pods, args.arrival_window)
-    # cluster trace as text, the 16k create_pod events as the binary block (k10s_engine_create_bulk)
+    cluster, workload, desc = build_workload(args)
+    # cluster trace as text, the create_pod events as the binary block (k10s_engine_create_bulk)
     scn, blob = scenario_bulk(cfg, cluster, workload)
     R = args.replicas
-    probe = Engine(scn, 1, device=local_rank, pods_blob=blob)
+    probe = make_engine(scn, 1, blob=blob)
     defaults = probe.default_params()
-    probe.close()
+    del probe
     params = ensemble.shard_params(defaults, R, rank, base_seed=123, perturb=True)  # replicas [rank*R, (rank+1)*R)
     t = time.perf_counter()
     caps = Capacities()
     caps.pruned_scan = 1 if args.pruned_scan else 0
-    eng = Engine(scn, R, params=params, caps=caps, device=local_rank, pods_blob=blob)
+    eng = make_engine(scn, R, params=params, caps=caps, blob=blob)
     log(f"[rank {rank}] engine: {R} replicas x {eng.replica_bytes / 2**20:.1f} MiB, init {time.perf_counter() - t:.2f}s")
 
     def one_step():
-        eng.reset()
+        if hasattr(eng, "reset"):
+            eng.reset()
         return eng.run_until_all_finished(max_time=1e7, max_events_per_launch=args.budget)
 
     for i in range(args.warmup):
@@ -138,22 +254,21 @@ def main():
         one_step()
         log(f"[rank {rank}] warmup {i}: {time.perf_counter() - t:.2f}s")
 
-    import numpy as np
-    counters = np.zeros(NUM_COUNTERS, dtype=np.float64)
+    counters = np.zeros(NUM_COUNTERS, dtype=np.int64)
     kernel_ms = []
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    if backend == "nccl":
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         ms = one_step()
         kernel_ms.append(ms)
-        res = eng.raw_results()
-        for r in res:
-            for k in range(NUM_COUNTERS):
-                counters[k] += r.counters[k]
+        for r in eng.raw_results():
+            counters += np.array([int(r.counters[k]) for k in range(NUM_COUNTERS)], dtype=np.int64)
         log(f"[rank {rank}] step {i}: run {ms:.1f} ms")
-    torch.cuda.synchronize()
+    if backend == "nccl":
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -167,46 +282,49 @@ def main():
     if statuses.get(2):
         log(f"[rank {rank}] WARNING: {statuses[2]} replicas ended in error: {errors}")
 
-    # cross-rank reduction (RCCL over xGMI): max of the timings, sum of the counters; the per-replica
-    # estimators of the last step are gathered in rank order into the job's ensemble summary
-    elapsed, mean_kernel_ms = ensemble.max_over_ranks([elapsed, sum(kernel_ms) / len(kernel_ms)])
+    # cross-rank reduction (RCCL over xGMI): max of the timings, int64 sum of the counters; the
+    # per-replica estimators of the last step are gathered in rank order into the job's ensemble summary
+    elapsed, mean_kernel_ms = ensemble.max_over_ranks([elapsed, sum(kernel_ms) / max(len(kernel_ms), 1)])
     c = ensemble.sum_over_ranks(counters.tolist())
     summary = ensemble.ensemble_summary(eng.raw_results()).as_dict()
+    st_all = ensemble.sum_over_ranks([statuses.get(s, 0) for s in range(5)])  # replica status histogram, all ranks
+    statuses = {s: n for s, n in enumerate(st_all) if n}
     placements, attempts, events, scanned, nread = c[12], c[13], c[14], c[15], c[16]
     value = placements / elapsed
 
     # roofline for the dominant kernel (per launch, this rank's launch time, all-rank bytes / world)
     per_launch_bytes = (12.0 * scanned + 12.0 * attempts + 12.0 * placements) / (args.steps * world)
-    achieved = per_launch_bytes / (mean_kernel_ms * 1e-3)
+    achieved = per_launch_bytes / (mean_kernel_ms * 1e-3) if mean_kernel_ms > 0 else 0.0
     # what the scans actually read (pruned scan: block bounds + scanned blocks + bound upkeep)
     touched_bytes = (12.0 * nread + 12.0 * attempts + 12.0 * placements) / (args.steps * world)
     traffic = None
     pmc_path = os.path.join(REPO, "profiles", "pmc_run_kernel.json")
-    if os.path.exists(pmc_path):
+    if os.path.exists(pmc_path) and not args.selftest_host:
         try:
             pm = json.load(open(pmc_path))
-            # only a PMC pass over this exact kernel build, config and scan mode counts
+            # only a PMC pass over this exact kernel build, config, workload and scan mode counts
             if pm.get("config") == [R, args.nodes, args.pods] and pm.get("engine") == version() and \
+                    pm.get("workload", "c3") == args.workload and \
                     pm.get("scan_mode") == ("pruned" if args.pruned_scan else "full"):
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
     out = {
-        "metric": "pod placements/sec (whole node, 1/2/4/8 GPUs) at 4k-node clusters; % HBM roofline",
+        "metric": METRIC,
         "value": value,
         "unit": "placements/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": elapsed / max(args.steps, 1) * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: Alibaba-like 4096-node clusters and 16384-pod traces (notebook statistics), seed-perturbed per replica",
-        "config": {"workload": f"C3: {R} replicas/GPU x {args.nodes}-node Alibaba-like cluster, {args.pods} pods/replica, "
-                               "run until all pods finished (RunUntilAllPodsAreFinished)",
+        "data": ("synthetic: Alibaba-like 4096-node clusters and 16384-pod traces (notebook statistics), "
+                 "seed-perturbed per replica") if not args.selftest_host else "selftest (host-check build on CPU)",
+        "config": {"workload": desc, "workload_name": args.workload,
                    "replicas_per_gpu": R, "total_replicas": R * world, "nodes": args.nodes, "pods_per_replica": args.pods,
                    "parallelism": f"replica-sharded x{world} (RCCL all-reduce of counters and histograms only)"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
@@ -215,7 +333,7 @@ def main():
                      "algorithmic_bytes_per_launch": per_launch_bytes,
                      "scan_mode": "pruned" if args.pruned_scan else "full",
                      "touched_bytes_per_launch": touched_bytes,
-                     "touched_GBps": touched_bytes / (mean_kernel_ms * 1e-3) / 1e9},
+                     "touched_GBps": touched_bytes / (mean_kernel_ms * 1e-3) / 1e9 if mean_kernel_ms > 0 else 0.0},
         "engine": version(),
         "rates": {"placements_per_s": value, "attempts_per_s": attempts / elapsed, "events_per_s": events / elapsed},
         "totals": {"placements": placements, "attempts": attempts, "events": events, "nodes_scanned": scanned,
@@ -223,7 +341,8 @@ def main():
                    "replica_status": {str(k): v for k, v in statuses.items()}, "replica_errors": errors},
         "ensemble": {"replicas": summary["replicas"], "replica_status": summary["replica_status"],
                      "counters": {k: summary["counters"][k] for k in ("total_pods_in_trace", "pods_succeeded",
-                                                                       "terminated_pods", "placements", "events")},
+                                                                       "terminated_pods", "placements", "attempts",
+                                                                       "events")},
                      "timings": summary["timings"], "histograms": summary.get("histograms")},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -232,7 +351,7 @@ def main():
         except Exception as ex:  # the GPU number stands on its own
             log("cpu baseline failed:", ex)
             out["cpu_baseline"] = None
-    if rank == 0 and not args.no_scan_kernel:
+    if rank == 0 and not args.no_scan_kernel and not args.selftest_host:
         # the scheduling-cycle kernel alone (k10s_schedule_one_batch over C3-sized node caches in HBM)
         try:
             from kubernetriks_amd.scanbench import measure

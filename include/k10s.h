@@ -55,6 +55,11 @@ extern "C" {
 #define K10S_REPLICA_FINISHED 1   /* all trace pods terminated at a clock multiple of 1000 */
 #define K10S_REPLICA_ERROR 2      /* reference panic or engine capacity overflow: see error_code */
 #define K10S_REPLICA_TIME_LIMIT 3 /* next event beyond the run's max_time guard */
+#define K10S_REPLICA_STALLED 4    /* opt-in stall guard (k10s_capacities.stall_guard): at a gauge tick
+                                     the trace was exhausted and only the periodic ticks were pending
+                                     (no running pod will finish, no node event, no CA/HPA), so the
+                                     replica can only retry its unschedulable pods forever and would
+                                     reach TIME_LIMIT; it stops there instead */
 
 /* ---- per-replica error codes (reference panic sites) ------------------------- */
 #define K10S_PANIC_NONE 0
@@ -98,6 +103,9 @@ enum k10s_counter {
     K10S_C_NODES_SCANNED,    /* Σ |scheduler cache| over attempts: algorithmic scan volume */
     K10S_C_NODES_READ,       /* scheduler-cache entries actually read (block bounds, scanned blocks,
                                 bound maintenance): the pruned scan's real volume, engine-only */
+    K10S_C_REQUEUED,         /* unschedulable_pods entries moved back to the action queue by any
+                                policy (scheduler.rs:174-185): the retry volume under backlog */
+    K10S_C_FLUSHED,          /* ... of which by the 30-s flush of entries older than 300 s (188-203) */
     K10S_NUM_COUNTERS
 };
 
@@ -160,6 +168,9 @@ typedef struct k10s_capacities {
                                             1 = exact block-bound pruned scan where it applies
                                              */
     uint32_t gauge_log;                  /* rows of the 5-s gauge recorder kept per replica; 0 = off */
+    uint32_t stall_guard;                /* 1 = stop a run-until-all-finished replica that can no longer
+                                            make progress with K10S_REPLICA_STALLED; 0 = off (reference
+                                            behaviour: it runs to max_time) */
 } k10s_capacities;
 
 /* One row of the gauge recorder (MetricsCollector::record_gauge_metrics, collector.rs:352-407,
@@ -199,6 +210,10 @@ typedef struct k10s_pod_record {
  * [r*node_stride, r*node_stride + n_nodes) in name order; present_bits marks which of them are in
  * the scheduler cache (bit i of word (r*node_stride + i)/64 — node_stride must be a multiple
  * of 64).  Writes out_node[r] (index within the problem, -1 on error) and out_status[r].
+ * Buffer contract (the scan reads 4 consecutive nodes per lane with 16-byte vector loads):
+ * alloc_cpu and alloc_ram must be 16-byte aligned and hold n_problems * node_stride elements
+ * (every row padded to node_stride; padding values are ignored), present_bits
+ * n_problems * node_stride / 64 words.  A misaligned pointer returns K10S_E_INVALID.
  * stream: a hipStream_t or NULL.  Returns K10S_OK or a negative K10S_E_* code. */
 int32_t k10s_schedule_one_batch(const uint32_t* alloc_cpu, const uint64_t* alloc_ram,
                                 const uint64_t* present_bits, uint32_t n_nodes, uint32_t node_stride,

@@ -131,6 +131,8 @@ BModel model(const std::string& s) {
 //   | u32 name_off[n + 1] | name bytes[name_off[n]]
 // Each entry becomes the same BTrace a "workload <ts> create_pod <name> <cpu> <ram> <dur|none>" line
 // would, so the compiled scenario is identical to the all-text one.
+// Bytes a name in a binary block may not contain (scenario-text separators; trace_soa.BLOB_NAME_FORBIDDEN).
+#define K10S_BLOB_NAME_FORBIDDEN " \t\n\v\f\r#="
 static void parse_bulk_pods(const uint8_t* b, uint64_t len, std::vector<BTrace>& workload) {
     uint64_t at = 0;
     auto need = [&](uint64_t bytes) {
@@ -151,6 +153,9 @@ static void parse_bulk_pods(const uint8_t* b, uint64_t len, std::vector<BTrace>&
     std::memcpy(off.data(), b + o_off, 4 * (n + 1));
     at = o_chr;
     need(off[n]);
+    // the same rules as trace_soa.read_pods_blob: offsets start at 0, never decrease, and the name
+    // bytes end exactly at the end of the block
+    if (off[0] != 0 || o_chr + off[n] != len) throw std::runtime_error("bulk pod blob: bad name offsets or trailing bytes");
     for (uint64_t i = 0; i < n; i++) {
         if (off[i] > off[i + 1] || off[i + 1] > off[n]) throw std::runtime_error("bulk pod blob: bad name offsets");
         BTrace t;
@@ -163,7 +168,7 @@ static void parse_bulk_pods(const uint8_t* b, uint64_t len, std::vector<BTrace>&
         if (t.has_dur) t.dur = d;
         t.kind = K10S_EV_AS_CREATE_POD_REQ;
         t.name.assign(reinterpret_cast<const char*>(b + o_chr + off[i]), off[i + 1] - off[i]);
-        if (t.name.empty() || t.name.find_first_of(" \t\r\n#") != std::string::npos)
+        if (t.name.empty() || t.name.find_first_of(K10S_BLOB_NAME_FORBIDDEN) != std::string::npos)
             throw std::runtime_error("bulk pod blob: invalid pod name");
         t.pos = (uint32_t)workload.size();
         workload.push_back(t);
@@ -719,6 +724,7 @@ Layout make_layout(const HostScenario& hs, const k10s_capacities& caps) {
     L.s_ram = take(8 * N);
     L.s_present = take(8 * (uint64_t)L.words_nodes);
     L.pruned = caps.pruned_scan ? 1u : 0u;
+    L.stall = caps.stall_guard ? 1u : 0u;
     L.bshift = 6;
     while (((N + (1ull << L.bshift) - 1) >> L.bshift) > 64) L.bshift++;
     L.nblocks = (uint32_t)((N + (1ull << L.bshift) - 1) >> L.bshift);

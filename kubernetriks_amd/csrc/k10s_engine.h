@@ -524,6 +524,8 @@ K10S_HELPER void s_move(Ctx& c, int mode, double t, uint32_t cpu, uint64_t ram) 
             q.attempts += 1;
             aq_push(c, q);
             if (c.H().error_code) return;
+            c.H().counters[K10S_C_REQUEUED] += 1;
+            if (mode == 1) c.H().counters[K10S_C_FLUSHED] += 1;
         } else {
             d[w++] = q;  // kept (not selected, or stale entry of a deleted pod)
         }
@@ -2200,6 +2202,22 @@ K10S_HD void consume_source(Ctx& c, int src) {
     }
 }
 
+// Stall guard (opt-in, k10s_capacities.stall_guard), evaluated after a gauge tick: the trace is
+// exhausted, the heap holds only the four periodic ticks (pod metrics, gauge, scheduling cycle,
+// flush; a pending pod finish, even a lazily canceled one, counts as progress), every delay-class
+// ring is empty, the action queue is empty and neither autoscaler runs.  Then no node's
+// allocatable can change again, every retry of an unschedulable pod fails as before, and the
+// replica would cycle until max_time (TIME_LIMIT) without terminating another pod.
+K10S_HD bool replica_stalled(Ctx& c) {
+    const RepHdr& H = c.H();
+    if (H.counters[K10S_C_TERMINATED_PODS] >= c.S().total_pods_in_trace) return false;
+    if (H.trace_cursor < c.S().n_trace || H.heap_size != 4 || H.aq_size != 0) return false;
+    if (c.S().ca_enabled || c.S().hpa_enabled) return false;
+    for (int q = 0; q < K10S_NFQ; q++)
+        if (H.fq_head[q] != H.fq_tail[q]) return false;
+    return true;
+}
+
 // ---- the event loop -----------------------------------------------------------------------------
 // Returns 1 if the replica still has work (event budget exhausted), else 0.  The working header
 // c.H() is LDS on the device (staged by the kernel) and the replica's header in place on the host.
@@ -2331,6 +2349,11 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
         const uint64_t t_dis = prof_now();
         dispatch(c, e);
         K10S_PROF_ADD(c, PROF_DISPATCH, t_dis);
+        if (e.kind == K10S_EV_M_GAUGE_TICK && c.Ly().stall && mode == K10S_RUN_UNTIL_ALL_FINISHED &&
+            replica_stalled(c)) {
+            status = K10S_REPLICA_STALLED;
+            break;
+        }
     }
     K10S_PROF_ADD(c, PROF_LOOP, t_loop);
     if (h->error_code) status = K10S_REPLICA_ERROR;

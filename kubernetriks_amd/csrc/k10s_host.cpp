@@ -105,6 +105,8 @@ int32_t k10s_schedule_one_batch(const uint32_t* alloc_cpu, const uint64_t* alloc
     if (!alloc_cpu || !alloc_ram || !present_bits || !req_cpu || !req_ram || !out_node || !out_status)
         return set_err(K10S_E_INVALID, "null pointer");
     if (node_stride % 64 != 0 || node_stride < n_nodes) return set_err(K10S_E_INVALID, "node_stride must be a multiple of 64 and >= n_nodes");
+    if (((uintptr_t)alloc_cpu & 15) || ((uintptr_t)alloc_ram & 15) || ((uintptr_t)present_bits & 7))
+        return set_err(K10S_E_INVALID, "alloc_cpu / alloc_ram must be 16-byte aligned (present_bits 8-byte)");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return set_err(K10S_E_NO_DEVICE, "no HIP device");
     HIPCHK(k10s_launch_schedule(alloc_cpu, alloc_ram, present_bits, n_nodes, node_stride, req_cpu, req_ram, weight,

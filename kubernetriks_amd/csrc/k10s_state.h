@@ -285,6 +285,7 @@ struct Layout {
     uint32_t bshift;      // block = 2^bshift consecutive node indices (>= 64, <= 64 blocks)
     uint32_t nblocks;
     uint32_t cap_gauge;   // gauge rows per replica (0 = gauge recorder off)
+    uint32_t stall;       // 1: stall guard on (k10s_capacities.stall_guard)
 };
 
 // Everything a launch reads but never writes, as one block (device: __constant__ memory).

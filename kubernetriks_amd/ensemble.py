@@ -112,13 +112,15 @@ def max_over_ranks(values: Sequence[float], group=None, device: Optional[str] = 
     return t.cpu().tolist()
 
 
-def sum_over_ranks(values: Sequence[float], group=None, device: Optional[str] = None):
-    """Element-wise sum of a counter vector over the group (RCCL all-reduce on GPUs)."""
+def sum_over_ranks(values: Sequence[int], group=None, device: Optional[str] = None):
+    """Element-wise sum of a u64 counter vector over the group (RCCL all-reduce on GPUs), in int64:
+    exact for every count below 2^63 (a float64 sum would round above 2^53)."""
+    vals = [int(v) for v in values]
     if _dist_group_size(group) <= 1:
-        return list(values)
+        return vals
     import torch
     import torch.distributed as dist
     dev = device or ("cuda" if dist.get_backend(group) == "nccl" else "cpu")
-    t = torch.tensor(list(values), dtype=torch.float64, device=dev)
+    t = torch.tensor(vals, dtype=torch.int64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-    return t.cpu().tolist()
+    return [int(v) for v in t.cpu().tolist()]

@@ -14,19 +14,19 @@ from typing import Dict, List, Optional, Sequence
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("K10S_LIB") or os.path.join(REPO, "build", "libk10s.so")
 
-NUM_COUNTERS = 17
+NUM_COUNTERS = 19
 COUNTER_NAMES = [
     "total_nodes_in_trace", "total_pods_in_trace", "pods_succeeded", "pods_unschedulable", "pods_failed",
     "pods_removed", "total_scaled_up_nodes", "total_scaled_down_nodes", "total_scaled_up_pods",
     "total_scaled_down_pods", "processed_nodes", "terminated_pods", "placements", "attempts", "events",
-    "nodes_scanned", "nodes_read",
+    "nodes_scanned", "nodes_read", "requeued", "flushed",
 ]
 EST_NAMES = ["pod_duration", "pod_schedule_time", "pod_queue_time"]
 
 RUN_UNTIL_ALL_FINISHED = 0
 RUN_UNTIL_TIME = 1
 
-STATUS = {0: "running", 1: "finished", 2: "error", 3: "time_limit"}
+STATUS = {0: "running", 1: "finished", 2: "error", 3: "time_limit", 4: "stalled"}
 
 
 HIST_BINS = 32  # K10S_HIST_BINS (include/k10s.h): log2 bins, 0: < 2^-10 s, k: [2^(k-11), 2^(k-10)), 31: >= 2^20 s
@@ -64,7 +64,8 @@ class Capacities(ctypes.Structure):
                 ("unschedulable", ctypes.c_uint32), ("group_name_bound", ctypes.c_uint32),
                 ("ca_name_bound", ctypes.c_uint32), ("event_log", ctypes.c_uint32),
                 ("placement_log", ctypes.c_uint32), ("pod_records", ctypes.c_uint32),
-                ("delay_fifo", ctypes.c_uint32), ("pruned_scan", ctypes.c_uint32), ("gauge_log", ctypes.c_uint32)]
+                ("delay_fifo", ctypes.c_uint32), ("pruned_scan", ctypes.c_uint32), ("gauge_log", ctypes.c_uint32),
+                ("stall_guard", ctypes.c_uint32)]
 
 
 class GaugeRow(ctypes.Structure):  # k10s_gauge_row (collector.rs:392-407 CSV columns)

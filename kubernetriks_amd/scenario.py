@@ -395,7 +395,8 @@ def alibaba_cluster_trace_from_csv(text: str) -> GenericClusterTrace:
 
 
 def alibaba_workload_trace_from_csv(instances_text: str, tasks_text: str) -> GenericWorkloadTrace:
-    """AlibabaWorkloadTraceV2017::make_pods_from_instances (workload.rs:56-120)."""
+    """AlibabaWorkloadTraceV2017::convert_to_simulator_events (workload.rs:124-141) over
+    make_pods_from_instances (56-120): the create_pod events stable-sorted by start time."""
     tasks = {}
     for row in csv.reader(io.StringIO(tasks_text)):
         if not row:
@@ -417,10 +418,15 @@ def alibaba_workload_trace_from_csv(instances_text: str, tasks_text: str) -> Gen
             continue
         if start <= 0 or end <= 0 or start >= end:
             continue
+        if job is None:   # workload.rs:91 `instance.job_id.unwrap()` panics
+            raise ValueError(f"instance of task {task} has no job id")
         name = f"{job}_{task}_{pod_no}"
         pod_no += 1
         pod = Pod(name, (cpu_sc * 10) & U32_MAX, _f64_as_u64(mem * float(DENORMALIZATION_BASE)), float(end - start))
         out.events.append(WorkloadEvent(float(start), "create_pod", pod=pod))
+    # convert_to_simulator_events (workload.rs:124-141) returns the events stable-sorted by start
+    # time; positions in this list are the engine's perturbation keys, as in the binary block
+    out.events.sort(key=lambda e: e.timestamp)
     return out
 
 

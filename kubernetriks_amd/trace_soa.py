@@ -26,6 +26,8 @@ import numpy as np
 from .scenario import DENORMALIZATION_BASE, U32_MAX, _check_name, _f64_as_u64, _opt_float, _opt_int
 
 MAGIC = b"K10SPOD1"
+# bytes a block name may not contain (k10s_builder.cpp K10S_BLOB_NAME_FORBIDDEN)
+BLOB_NAME_FORBIDDEN = frozenset(b" \t\n\v\f\r#=")
 _HEADER = 16
 
 
@@ -50,7 +52,8 @@ def alibaba_pods_blob(instances: Union[str, io.TextIOBase], tasks: Union[str, io
     """Stream batch_instance.csv (path or text stream) into a sorted K10SPOD1 block.
 
     Only the task table is held as a dict; instance rows are reduced to four packed columns and the
-    name bytes as they are read, so memory is ~30 B + name length per pod."""
+    name bytes as they are read (~32 B + name length per pod); packing adds the sorted output
+    (the same size again, written once) and O(n) index words (_pack_sorted)."""
     tf = _open_text(tasks)
     try:
         task_map = _tasks_from_rows(csv.reader(tf))
@@ -88,29 +91,49 @@ def alibaba_pods_blob(instances: Union[str, io.TextIOBase], tasks: Union[str, io
         if f is not instances:
             f.close()
     return _pack_sorted(np.frombuffer(ts, "<f8"), np.frombuffer(cpu, "<u4"), np.frombuffer(ram, "<u8"),
-                        np.frombuffer(dur, "<f8"), np.frombuffer(name_len, "<u4"), bytes(names))
+                        np.frombuffer(dur, "<f8"), np.frombuffer(name_len, "<u4"), names)
 
 
-def _pack_sorted(ts, cpu, ram, dur, name_len, names: bytes) -> bytes:
+def _pack_sorted(ts, cpu, ram, dur, name_len, names) -> bytes:
+    """The sorted K10SPOD1 block, written into one preallocated buffer.  The name bytes are gathered
+    in sorted order in bounded chunks of pods, so the extra memory is O(n) words for the columns
+    plus one chunk's byte indices, not several int64 arrays per name byte."""
     n = ts.size
-    if len(names) > U32_MAX:
+    nbytes = len(names)
+    if nbytes > U32_MAX:
         raise ValueError("pod names exceed the 4 GiB offset range of a K10SPOD1 block")
-    src_off = np.zeros(n + 1, dtype=np.int64)
-    np.cumsum(name_len, out=src_off[1:])
     order = np.argsort(ts, kind="stable")                       # workload.rs:140 (stable sort_by)
     lens = name_len[order].astype(np.int64)
     off = np.zeros(n + 1, dtype="<u4")
     off[1:] = np.cumsum(lens)
+    pad = 4 * (n & 1)
+    p_ts = _HEADER
+    p_cpu = p_ts + 8 * n
+    p_ram = p_cpu + 4 * n + pad
+    p_dur = p_ram + 8 * n
+    p_off = p_dur + 8 * n
+    p_chr = p_off + 4 * (n + 1)
+    out = bytearray(p_chr + nbytes)
+    out[:8] = MAGIC
+    out[8:16] = np.array([n], dtype="<u8").tobytes()
+    for p, col, dt in ((p_ts, ts, "<f8"), (p_cpu, cpu, "<u4"), (p_ram, ram, "<u8"), (p_dur, dur, "<f8")):
+        np.frombuffer(out, dt, n, p)[:] = col[order]
+    np.frombuffer(out, "<u4", n + 1, p_off)[:] = off
     if n:
-        # gather the name bytes in sorted order: byte j of pod k comes from src_off[order[k]] + j
-        starts = np.repeat(src_off[:-1][order], lens)
-        within = np.arange(int(off[-1]), dtype=np.int64) - np.repeat(off[:-1].astype(np.int64), lens)
-        sorted_names = np.frombuffer(names, np.uint8)[starts + within].tobytes()
-    else:
-        sorted_names = b""
-    pad = b"\0" * (4 * (n & 1))
-    return (MAGIC + np.array([n], dtype="<u8").tobytes() + ts[order].tobytes() + cpu[order].tobytes() + pad +
-            ram[order].tobytes() + dur[order].tobytes() + off.tobytes() + sorted_names)
+        src = np.frombuffer(names, np.uint8)
+        src_off = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum(name_len, out=src_off[1:], dtype=np.int64)
+        dst = np.frombuffer(out, np.uint8, nbytes, p_chr)
+        CH = 1 << 16
+        for a in range(0, n, CH):                               # bounded per-chunk byte gather
+            o = order[a:a + CH]
+            ln = lens[a:a + CH]
+            base = int(off[a])
+            tot = int(off[min(a + CH, n)]) - base
+            starts = np.repeat(src_off[o], ln)
+            within = np.arange(tot, dtype=np.int64) - np.repeat(off[a:a + o.size].astype(np.int64) - base, ln)
+            dst[base:base + tot] = src[starts + within]
+    return bytes(out)
 
 
 def read_pods_blob(blob: bytes) -> dict:
@@ -131,7 +154,12 @@ def read_pods_blob(blob: bytes) -> dict:
     if off[0] != 0 or np.any(np.diff(off.astype(np.int64)) < 0) or p + int(off[-1]) != len(blob):
         raise ValueError("bad name offsets in K10SPOD1 block")
     raw = blob[p:]
-    names = [raw[off[i]:off[i + 1]].decode() for i in range(n)]
+    names = []
+    for i in range(n):   # the rules of k10s_builder.cpp parse_bulk_pods
+        b = raw[off[i]:off[i + 1]]
+        if not b or any(ch in BLOB_NAME_FORBIDDEN for ch in b):
+            raise ValueError(f"invalid pod name {b!r} in K10SPOD1 block")
+        names.append(b.decode())
     return {"ts": ts, "cpu": cpu, "ram": ram, "duration": dur, "names": names}
 
 

@@ -160,6 +160,31 @@ def c3_traces(n_nodes: int = 4096, n_pods: int = 16384, arrival_window: float = 
     return c, w
 
 
+def c3_backlog_traces(n_nodes: int = 4096, n_pods: int = 16384, arrival_window: float = 1200.0, seed: int = 2018,
+                      mean_duration: float = 1500.0, ram_frac=(0.3, 0.5)):
+    """C3 under load (rho ~ 0.9-1.2 of the RAM-bound capacity, "so backlogs and
+    retries occur").  Same 4,096 Alibaba-like nodes; each pod asks for a fraction `ram_frac` of a
+    modal node's RAM, so a node holds 2-4 pods, and stays for an exponential duration (mean
+    `mean_duration` s, integer seconds).  With 16,384 arrivals over 1,200 s the concurrent demand
+    (~ 13.7 pods/s x 1,500 s x (1 - e^-0.8) = 11.3 k pods at t = 1,200 s) exceeds what ~ 4,096
+    nodes x 2-3 pods hold, so pods fail attempts (~7 attempts per placement), wait in the
+    unschedulable map and are moved back on every pod finish (scheduler.rs:174-244, 289-304,
+    422-440); with the conditional move enabled they stay there and the 300-s flush moves them."""
+    rng = random.Random(seed)
+    c = GenericClusterTrace()
+    for k in range(1, n_nodes + 1):
+        ram = int(_machine_mem(rng) * float(GIB128))
+        c.create_node(0.0, Node(f"alibaba_node_{k}", 64 * 1000, ram))
+    node_ram = ALIBABA_NODE_MEM * float(GIB128)
+    w = GenericWorkloadTrace()
+    for i in range(n_pods):
+        start = float(int(rng.random() * arrival_window) + 1)
+        dur = float(max(1, int(rng.expovariate(1.0 / mean_duration))))
+        ram = int(rng.uniform(ram_frac[0], ram_frac[1]) * node_ram)
+        w.create_pod(start, Pod(f"{1000 + i // 64}_{i}_{i}", _task_cpu(rng), ram, dur))
+    return c, w
+
+
 def c3_scenario(n_nodes: int = 4096, n_pods: int = 16384, arrival_window: float = 1200.0, seed: int = 2017) -> str:
     cfg = SimulationConfig()
     c, w = c3_traces(n_nodes, n_pods, arrival_window, seed)

@@ -415,6 +415,7 @@ struct Counters {
              total_scaled_down_nodes = 0, total_scaled_up_pods = 0, total_scaled_down_pods = 0,
              processed_nodes = 0, terminated_pods = 0;
     uint64_t placements = 0, attempts = 0, events = 0;
+    uint64_t requeued = 0, flushed = 0; /* unschedulable -> action queue moves (all / flush) */
 };
 
 class Sim {
@@ -1127,6 +1128,7 @@ void Sim::s_move_pods_to_active(const std::vector<UnschedKey>& keys) {   /* 174-
         unschedulable.erase(it);
         q.attempts += 1;
         action_queue.push(q);
+        c.requeued++;
     }
 }
 void Sim::s_move_all() {                                                  /* 235-244 */
@@ -1213,7 +1215,9 @@ void Sim::on_sched(Ev& e) {
         std::vector<UnschedKey> keys;
         for (auto& kv : unschedulable)
             if (e.time - kv.second.timestamp > 5.0 * 60.0) keys.push_back(kv.first);
+        const uint64_t before = c.requeued;
         s_move_pods_to_active(keys);
+        c.flushed += c.requeued - before;
         emit(K10S_EV_S_FLUSH, 30.0);
         break;
     }
@@ -1852,6 +1856,8 @@ static std::string dump_json(Sim& s, int status, int flags) {
     o += ",\"placements\":" + std::to_string(c.placements);
     o += ",\"attempts\":" + std::to_string(c.attempts);
     o += ",\"events\":" + std::to_string(c.events);
+    o += ",\"requeued\":" + std::to_string(c.requeued);
+    o += ",\"flushed\":" + std::to_string(c.flushed);
     o += "},\"estimators\":{";
     jest(o, "pod_duration", s.pod_duration); o += ',';
     jest(o, "pod_schedule_time", s.sched_latency); o += ',';

@@ -39,3 +39,23 @@ def test_no_cpu_fallback_without_gpu():
     import scenarios
     with pytest.raises(RuntimeError, match="no HIP device"):
         Engine(scenarios.sc_c1_generic_example(), 1)
+
+
+def test_schedule_one_batch_rejects_misaligned_buffers():
+    """k10s.h buffer contract: 16-byte aligned alloc_cpu / alloc_ram (checked before any device
+    call, so this runs on CPU too)."""
+    from kubernetriks_amd.native import lib
+    import numpy as np
+    L = lib()
+    cpu = np.zeros(128 + 4, dtype=np.uint32)
+    ram = np.zeros(128, dtype=np.uint64)
+    bits = np.zeros(2, dtype=np.uint64)
+    req_c = np.ones(1, dtype=np.uint32)
+    req_r = np.ones(1, dtype=np.uint64)
+    out = np.zeros(2, dtype=np.int32)
+    base = cpu.ctypes.data + (16 - cpu.ctypes.data % 16) % 16
+    rc = L.k10s_schedule_one_batch(ctypes.c_void_p(base + 4), ctypes.c_void_p(ram.ctypes.data),
+                                   ctypes.c_void_p(bits.ctypes.data), 64, 64, ctypes.c_void_p(req_c.ctypes.data),
+                                   ctypes.c_void_p(req_r.ctypes.data), ctypes.c_double(1.0), 1,
+                                   ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(out.ctypes.data + 4), None)
+    assert rc != 0 and b"aligned" in L.k10s_last_error()

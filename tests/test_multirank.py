@@ -63,10 +63,10 @@ def _worker(rank, world, port, R, out_path):
     try:
         eng = _run_shard(R, rank)
         summary = ensemble.ensemble_summary(eng.raw_results()).as_dict()
-        local = [0.0] * NUM_COUNTERS
+        local = [0] * NUM_COUNTERS
         for r in eng.raw_results():
             for k in range(NUM_COUNTERS):
-                local[k] += float(r.counters[k])
+                local[k] += int(r.counters[k])
         summed = ensemble.sum_over_ranks(local)
         mx = ensemble.max_over_ranks([float(rank), 1.5])
         if rank == 0:
@@ -100,13 +100,52 @@ def test_two_gloo_ranks_equal_one_rank(tmp_path):
     # histograms went through the cross-rank SUM all-reduce and count every estimator sample
     for k, t in want["timings"].items():
         assert sum(want["histograms"][k]) == t["n"] > 0, k
-    tot = [0.0] * NUM_COUNTERS
+    tot = [0] * NUM_COUNTERS
     for r in eng.raw_results():
         for k in range(NUM_COUNTERS):
-            tot[k] += float(r.counters[k])
+            tot[k] += int(r.counters[k])
     assert got["summed"] == tot
     assert got["max"] == [1.0, 1.5]
     # the merged estimators are a proper pooling of the replicas' samples
     pd = want["timings"]["pod_duration"]
     assert pd["n"] == sum(int(r.est[0].n) for r in eng.raw_results())
     assert not math.isnan(pd["mean"]) and pd["min"] <= pd["mean"] <= pd["max"]
+
+
+def _bench(args, env_extra=None):
+    import subprocess
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], env=env, capture_output=True,
+                       text=True, timeout=600)
+    return p
+
+
+def test_bench_gpus_2_launches_two_ranks():
+    """bench.py --gpus 2 (no WORLD_SIZE): the parent spawns 2 rank processes that combine over
+    torch.distributed; their int64 counter totals equal one rank running both shards' replicas."""
+    common = ["--selftest-host", "--nodes", "64", "--pods", "120", "--arrival-window", "60", "--steps", "1",
+              "--warmup", "0", "--no-cpu-baseline"]
+    p2 = _bench(["--gpus", "2", "--replicas", "2", *common])
+    assert p2.returncode == 0, p2.stderr[-2000:]
+    lines = [json.loads(x) for x in p2.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p2.stdout  # rank 0 prints the one line
+    two = lines[0]
+    assert two["n_gpus"] == 2 and two["config"]["total_replicas"] == 4
+    assert "[rank 1]" in p2.stderr and "[rank 0]" in p2.stderr
+    p1 = _bench(["--gpus", "1", "--replicas", "4", *common])
+    assert p1.returncode == 0, p1.stderr[-2000:]
+    one = json.loads([x for x in p1.stdout.splitlines() if x.startswith("{")][0])
+    assert one["n_gpus"] == 1
+    for k in ("placements", "attempts", "events", "nodes_scanned"):
+        assert isinstance(two["totals"][k], int) and two["totals"][k] == one["totals"][k] > 0, k
+    assert two["ensemble"]["counters"] == one["ensemble"]["counters"]
+    assert two["totals"]["replica_status"] == one["totals"]["replica_status"] == {"1": 4}
+
+
+def test_bench_world_size_mismatch_fails():
+    p = _bench(["--gpus", "2", "--selftest-host", "--replicas", "1", "--nodes", "8", "--pods", "4", "--steps", "1",
+                "--warmup", "0", "--no-cpu-baseline"], {"WORLD_SIZE": "1", "RANK": "0"})
+    assert p.returncode == 2 and "WORLD_SIZE=1" in p.stderr

@@ -25,9 +25,10 @@ REF_TASKS = ("10718,12897,15,64,2003,Terminated,50,0.01600704061294748\n"
              "1,2,120,686,1,Terminated,100,0.5\n")
 
 
-def _synthetic_csv(n_inst=3000, n_tasks=200, seed=11, fits=False):
+def _synthetic_csv(n_inst=3000, n_tasks=200, seed=11, fits=False, no_job_row=False):
     """fits=True keeps every request within a C3 node, so an engine run finishes every pod (a pod that
-    can never fit keeps the unschedulable flush cycling until max_time)."""
+    can never fit keeps the unschedulable flush cycling until max_time).  no_job_row appends a row
+    that passes every filter but has an empty job id (workload.rs:91 unwraps it: an error)."""
     rng = random.Random(seed)
     tasks, inst = [], []
     for t in range(n_tasks):
@@ -41,6 +42,9 @@ def _synthetic_csv(n_inst=3000, n_tasks=200, seed=11, fits=False):
         cells = [str(start), "" if rng.random() < 0.03 else str(end), str(task % 37),
                  "" if rng.random() < 0.02 else str(task), "9", "Terminated", "1", "1", "", "", "", ""]
         inst.append(",".join(cells))
+    if no_job_row:
+        tasks.append(f"0,1,3,{n_tasks + 100},5,Terminated,50,0.01")
+        inst.append(f"10,20,,{n_tasks + 100},9,Terminated,1,1,,,,")
     return "\n".join(inst) + "\n", "\n".join(tasks) + "\n"
 
 
@@ -79,10 +83,39 @@ def test_reference_rows_values():
 def test_duplicated_task_and_malformed_blob():
     with pytest.raises(ValueError):
         trace_soa.alibaba_pods_blob(io.StringIO(REF_INSTANCES), io.StringIO(REF_TASKS + REF_TASKS))
+    # an instance that passes the filters without a job id: both paths refuse it (workload.rs:91)
+    inst, tasks = _synthetic_csv(n_inst=50, n_tasks=10, seed=4, no_job_row=True)
+    with pytest.raises(ValueError):
+        trace_soa.alibaba_pods_blob(io.StringIO(inst), io.StringIO(tasks))
+    with pytest.raises(ValueError):
+        alibaba_workload_trace_from_csv(inst, tasks)
     blob = trace_soa.alibaba_pods_blob(io.StringIO(REF_INSTANCES), io.StringIO(REF_TASKS))
     for bad in (blob[:-1], b"K10SPODX" + blob[8:], blob[:10], blob + b"x"):
         with pytest.raises(ValueError):
             trace_soa.read_pods_blob(bad)
+
+
+@pytest.mark.parametrize("bad", ["trailing", "space", "hash", "offset0"])
+def test_malformed_blob_rejected_by_engine_and_reader(bad):
+    """k10s_engine_create_bulk (host build) and trace_soa.read_pods_blob apply the same rules."""
+    from kubernetriks_amd.scenario import Pod
+    blob = bytearray(pods_blob([(1.0, Pod("ab", 1, 1, 1.0)), (2.0, Pod("cd", 1, 1, 1.0))]))
+    if bad == "trailing":
+        blob += b"x"
+    elif bad == "space":
+        blob[-1:] = b" "
+    elif bad == "hash":
+        blob[-3:-2] = b"#"
+    else:
+        p = 16 + 2 * (8 + 4 + 8 + 8)
+        blob[p:p + 4] = (1).to_bytes(4, "little")
+    blob = bytes(blob)
+    with pytest.raises(ValueError):
+        trace_soa.read_pods_blob(blob)
+    cluster, _ = wl.c3_traces(n_nodes=4, n_pods=1, arrival_window=1.0, seed=5)
+    btext, _ = scenario_bulk(SimulationConfig(), cluster, GenericWorkloadTrace([]))
+    with pytest.raises(ValueError):
+        HostEngine(btext, 1, pods_blob=blob)
 
 
 def test_file_round_trip(tmp_path):
@@ -101,29 +134,74 @@ def _engine(backend):
     return Engine
 
 
+@pytest.mark.parametrize("perturb", [False, True])
 @pytest.mark.parametrize("backend", ["host", pytest.param("gpu", marks=pytest.mark.gpu)])
-def test_streamed_blob_runs_like_text(backend):
-    """The converter's block fed to k10s_engine_create_bulk == the same pods as scenario text."""
+def test_streamed_blob_runs_like_text(backend, perturb):
+    """The converter's block fed to k10s_engine_create_bulk: bit-exact with the ORACLE on the same
+    pods as scenario text, and identical to the engine's own text run — with pods that can never fit
+    a node (2^31 santicores, 3.5e8 x 128 GiB), so the replica retries them until the max_time guard
+    (TIME_LIMIT), and with seed-perturbed replicas (the block's sorted position is the perturbation
+    key on both paths)."""
+    import oracle_jobs
     E = _engine(backend)
-    inst, tasks = _synthetic_csv(n_inst=400, n_tasks=60, seed=5, fits=True)
+    inst, tasks = _synthetic_csv(n_inst=400, n_tasks=60, seed=5)
     blob = trace_soa.alibaba_pods_blob(io.StringIO(inst), io.StringIO(tasks))
     _, ev = _object_path_blob(inst, tasks)
     assert ev
     cfg = SimulationConfig()
     cluster, _ = wl.c3_traces(n_nodes=48, n_pods=1, arrival_window=1.0, seed=5)
-    text = scenario_text(cfg, cluster, GenericWorkloadTrace(ev))
+    workload = GenericWorkloadTrace(ev)
+    text = scenario_text(cfg, cluster, workload)
     btext, _ = scenario_bulk(cfg, cluster, GenericWorkloadTrace([]))
     caps = parity.parity_caps(log=True)
-    a = E(text, 2, caps=caps)
-    b = E(btext, 2, caps=caps, pods_blob=blob)
+    params = wl.replica_params(E(text, 1).default_params(), 2, base_seed=31, perturb=perturb)
+    max_time = 20000.0
+    a = E(text, 2, params=params, caps=caps)
+    b = E(btext, 2, params=params, caps=caps, pods_blob=blob)
     for e in (a, b):
-        e.run_until_all_finished(1e6)
+        e.run_until_all_finished(max_time)
+    ods = oracle_jobs.replay_many([wl.replica_scenario(cfg, cluster, workload, p) for p in params], max_time, workers=1)
     for r in range(2):
         assert repr(a.results()[r]) == repr(b.results()[r])
         assert a.placements(r) == b.placements(r)
         assert a.event_log(r) == b.event_log(r)
-    c = a.results()[0]["counters"]
-    assert c["placements"] == len(ev) and c["pods_succeeded"] == len(ev)
+        assert parity.compare(ods[r], b, r=r, log=False) == [], r
+        assert b.results()[r]["status"] == "time_limit"
+    unfit = sum(1 for e in ev if e.pod.cpu > 64000 or e.pod.ram > (1 << 37))
+    c = b.results()[0]["counters"]
+    assert unfit > 0 and c["pods_succeeded"] == len(ev) - unfit and c["attempts"] > c["placements"]
+
+
+@pytest.mark.parametrize("backend", ["host", pytest.param("gpu", marks=pytest.mark.gpu)])
+def test_stall_guard_stops_a_replica_that_cannot_finish(backend):
+    """k10s_capacities.stall_guard: once only periodic ticks are pending, a replica whose remaining
+    pods can never fit stops with K10S_REPLICA_STALLED instead of cycling to max_time; up to that
+    point it is the run without the guard (a prefix of its event log)."""
+    E = _engine(backend)
+    inst, tasks = _synthetic_csv(n_inst=300, n_tasks=40, seed=8)
+    blob = trace_soa.alibaba_pods_blob(io.StringIO(inst), io.StringIO(tasks))
+    cfg = SimulationConfig()
+    cluster, _ = wl.c3_traces(n_nodes=32, n_pods=1, arrival_window=1.0, seed=8)
+    btext, _ = scenario_bulk(cfg, cluster, GenericWorkloadTrace([]))
+    caps = parity.parity_caps(log=True)
+    full = E(btext, 1, caps=caps, pods_blob=blob)
+    full.run_until_all_finished(1e5)
+    caps.stall_guard = 1
+    g = E(btext, 1, caps=caps, pods_blob=blob)
+    g.run_until_all_finished(1e5)
+    rf, rg = full.results()[0], g.results()[0]
+    assert rf["status"] == "time_limit" and rg["status"] == "stalled"
+    assert rg["time"] < rf["time"] and rg["counters"]["events"] < rf["counters"]["events"] / 10
+    log_g = g.event_log(0)
+    assert full.event_log(0)[:len(log_g)] == log_g
+    for k in ("placements", "pods_succeeded", "terminated_pods"):
+        assert rg["counters"][k] == rf["counters"][k], k
+    # a replica that does finish is not affected by the guard
+    c2, w2 = wl.c3_traces(n_nodes=16, n_pods=40, arrival_window=30.0, seed=2)
+    scn = scenario_text(cfg, c2, w2)
+    h = E(scn, 1, caps=caps)
+    h.run_until_all_finished(1e6)
+    assert h.results()[0]["status"] == "finished"
 
 
 def test_perturb_blob_matches_perturb_pod():
