@@ -361,11 +361,20 @@ def main():
             out["scheduling_kernel"] = None
     if args.profile:
         prof = eng.profile()
-        tot = {k: float(sum(p[k] for p in prof)) for k in prof[0]}
+        scal = [k for k in prof[0] if not k.startswith("kind_")]
+        tot = {k: float(sum(p[k] for p in prof)) for k in scal}
         loop = tot["loop"] or 1.0
-        out["profile"] = {"cycles_total": tot, "share_of_loop": {k: v / loop for k, v in tot.items() if k != "scans"},
+        out["profile"] = {"cycles_total": tot, "share_of_loop": {k: v / loop for k, v in tot.items() if not k.startswith("n")
+                                                                 and k != "scans"},
                           "cycles_per_event": loop / max(events / args.steps / world, 1.0),
                           "scan_cycles_per_scan": tot["scan"] / max(tot["scans"], 1.0)}
+        if "kind_cycles" in prof[0]:
+            from kubernetriks_amd.native import EVENT_KIND_NAMES
+            kc = [sum(p["kind_cycles"][k] for p in prof) for k in range(len(prof[0]["kind_cycles"]))]
+            kn = [sum(p["kind_count"][k] for p in prof) for k in range(len(prof[0]["kind_count"]))]
+            out["profile"]["by_kind"] = {EVENT_KIND_NAMES.get(k, str(k)): {"count": kn[k], "share_of_loop": kc[k] / loop,
+                                                                         "cycles_per_event": kc[k] / max(kn[k], 1)}
+                                         for k in range(len(kc)) if kn[k]}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

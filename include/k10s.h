@@ -321,7 +321,9 @@ uint64_t k10s_engine_replica_bytes(const k10s_engine* e);
 /* Tooling: per-replica cycle attribution of the event loop, 8 words per replica
    (loop, select, consume, dispatch, scheduling cycle, scan, scans, bound maintenance; s_memtime
    cycles).  All zero unless the library was built with -DK10S_PROF=1 (variant builds only). */
-int32_t k10s_engine_profile(const k10s_engine* e, uint64_t* out /* [n_replicas * 8] */);
+int32_t k10s_engine_profile(const k10s_engine* e, uint64_t* out /* [n_replicas * width] */);
+/* Slots per replica k10s_engine_profile writes (8 in product builds; more in K10S_PROF builds). */
+uint32_t k10s_engine_profile_width(void);
 
 const char* k10s_last_error(void);
 const char* k10s_version(void);

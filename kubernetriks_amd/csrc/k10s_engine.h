@@ -141,11 +141,9 @@ K10S_HD void uniform_event(HeapEv& e) {
 
 // ---- cycle attribution (K10S_PROF builds: tooling only, semantics-neutral) ----------------------
 // s_memtime deltas per loop phase, accumulated in RepHdr::prof and read by k10s_engine_profile.
-#ifndef K10S_PROF
-#define K10S_PROF 0
-#endif
 enum : int { PROF_LOOP = 0, PROF_SELECT = 1, PROF_CONSUME = 2, PROF_DISPATCH = 3, PROF_CYCLE = 4, PROF_SCAN = 5,
-             PROF_NSCAN = 6, PROF_BOUNDS = 7 };
+             PROF_NSCAN = 6, PROF_BOUNDS = 7, PROF_AQPOP = 8, PROF_HEAPPOP = 9, PROF_NHEAPPOP = 10, PROF_EMIT = 11,
+             PROF_NEMIT = 12, PROF_AQPUSH = 13 };
 K10S_HD uint64_t prof_now() {
 #if K10S_PROF && K10S_DEVICE
     return (uint64_t)__builtin_readcyclecounter();
@@ -914,7 +912,9 @@ K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
     h->g_pods_q = (uint64_t)h->aq_size + (uint64_t)h->uq_size;  // scheduler.rs:256-259
     const double w = c.P().score_weight;
     while (c.H().aq_size > 0 && !c.H().error_code) {
+        const uint64_t t_aq = prof_now();
         QInfo q = aq_pop(c);
+        K10S_PROF_ADD(c, PROF_AQPOP, t_aq);
         uint32_t p = q.pod;
         if (!pod_in_s(c, p)) continue;
         double queue_t = t - q.initial + cycle_dur;
@@ -2191,7 +2191,10 @@ K10S_HD void consume_source(Ctx& c, int src) {
         H.trace_cursor = cur;
         trace_head_load(c, cur);
     } else if (src == SRC_HEAP) {
+        const uint64_t t_hp = prof_now();
         heap_pop(c);
+        K10S_PROF_ADD(c, PROF_HEAPPOP, t_hp);
+        if (K10S_PROF) H.prof[PROF_NHEAPPOP] += 1;
     } else {
         const uint32_t hd = H.fq_head[src] + 1;
         H.fq_head[src] = hd;
@@ -2349,6 +2352,10 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
         const uint64_t t_dis = prof_now();
         dispatch(c, e);
         K10S_PROF_ADD(c, PROF_DISPATCH, t_dis);
+#if K10S_PROF
+        h->prof[K10S_PROF_KIND0 + e.kind] += prof_now() - t_dis;
+        h->prof[K10S_PROF_KIND0 + K10S_EV_NUM_KINDS + e.kind] += 1;
+#endif
         if (e.kind == K10S_EV_M_GAUGE_TICK && c.Ly().stall && mode == K10S_RUN_UNTIL_ALL_FINISHED &&
             replica_stalled(c)) {
             status = K10S_REPLICA_STALLED;

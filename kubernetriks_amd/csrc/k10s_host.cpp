@@ -383,9 +383,11 @@ int32_t k10s_engine_profile(const k10s_engine* e, uint64_t* out) {
     HIPCHK(hipMemcpy2D(hdr.data(), sizeof(RepHdr), e->d_state + e->L.hdr, e->L.stride, sizeof(RepHdr), e->R,
                        hipMemcpyDeviceToHost));
     for (uint32_t r = 0; r < e->R; r++)
-        for (int i = 0; i < 8; i++) out[(size_t)r * 8 + i] = hdr[r].prof[i];
+        for (int i = 0; i < K10S_PROF_SLOTS; i++) out[(size_t)r * K10S_PROF_SLOTS + i] = hdr[r].prof[i];
     return K10S_OK;
 }
+
+uint32_t k10s_engine_profile_width(void) { return K10S_PROF_SLOTS; }
 
 static int32_t read_hdr(const k10s_engine* e, uint32_t r, RepHdr& h) {
     if (r >= e->R) return set_err(K10S_E_INVALID, "replica index out of range");

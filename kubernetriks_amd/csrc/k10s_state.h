@@ -152,6 +152,16 @@ static_assert((K10S_FQW & (K10S_FQW - 1)) == 0 && K10S_FQW <= 64, "K10S_FQW: pow
 #define K10S_HEAP_TOP 73
 #endif
 
+#ifndef K10S_PROF
+#define K10S_PROF 0
+#endif
+#define K10S_PROF_KIND0 16   // prof[16 + k]: dispatch cycles of kind k; prof[16 + 46 + k]: count
+#if K10S_PROF
+#define K10S_PROF_SLOTS (K10S_PROF_KIND0 + 2 * K10S_EV_NUM_KINDS)
+#else
+#define K10S_PROF_SLOTS 8
+#endif
+
 struct RepHdr {
     double clock;
     uint32_t next_seq;
@@ -191,8 +201,9 @@ struct RepHdr {
     uint32_t tr_seq, tr_pad;      // trace_cursor < n_trace)
     HeapEv fq_win[K10S_NFQ * K10S_FQW];
     HeapEv heap_lds[K10S_HEAP_TOP];
-    // cycle attribution of the event loop (K10S_PROF builds only, zero otherwise): K10S_PROF_*
-    uint64_t prof[8];
+    // cycle attribution of the event loop (K10S_PROF builds only, zero otherwise): PROF_* phases,
+    // then per event kind the dispatch cycles and the count (K10S_PROF builds only hold those)
+    uint64_t prof[K10S_PROF_SLOTS];
 };
 
 struct QInfo {              // QueuedPodInfo (queue.rs:13-27), 24 B

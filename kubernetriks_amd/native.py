@@ -23,6 +23,20 @@ COUNTER_NAMES = [
 ]
 EST_NAMES = ["pod_duration", "pod_schedule_time", "pod_queue_time"]
 
+
+def _event_kind_names():
+    """{kind id: name} from include/k10s_events.h (K10S_EV_AS_CREATE_POD_REQ = 4 -> "AS_CREATE_POD_REQ")."""
+    import re
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "k10s_events.h")
+    try:
+        text = open(path).read()
+    except OSError:
+        return {}
+    return {int(v): k for k, v in re.findall(r"K10S_EV_([A-Z0-9_]+)\s*=\s*(\d+)", text) if k != "NUM_KINDS"}
+
+
+EVENT_KIND_NAMES = _event_kind_names()
+
 RUN_UNTIL_ALL_FINISHED = 0
 RUN_UNTIL_TIME = 1
 
@@ -332,14 +346,27 @@ class Engine(EngineBase):
 
     def profile(self):
         """Per-replica cycle attribution (K10S_PROF variant builds; zeros otherwise): a list of
-        dicts with loop/select/consume/dispatch/cycle/scan/scans/bounds."""
-        n = self.n_replicas * 8
-        buf = (ctypes.c_uint64 * n)()
+        dicts with the loop phases (loop/select/consume/dispatch/cycle/scan/scans/bounds, and in
+        profiling builds aqpop/heappop/nheappop) and, in profiling builds, per event kind
+        "kind_cycles" / "kind_count" lists."""
+        self._L.k10s_engine_profile_width.restype = ctypes.c_uint32
+        w = int(self._L.k10s_engine_profile_width())
+        buf = (ctypes.c_uint64 * (self.n_replicas * w))()
         self._L.k10s_engine_profile.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         self._L.k10s_engine_profile.restype = ctypes.c_int32
         self._check(self._L.k10s_engine_profile(self._h, buf))
-        keys = ["loop", "select", "consume", "dispatch", "cycle", "scan", "scans", "bounds"]
-        return [dict(zip(keys, buf[r * 8:(r + 1) * 8])) for r in range(self.n_replicas)]
+        keys = ["loop", "select", "consume", "dispatch", "cycle", "scan", "scans", "bounds", "aqpop", "heappop",
+                "nheappop", "emit", "nemit", "aqpush"]
+        out = []
+        for r in range(self.n_replicas):
+            row = list(buf[r * w:(r + 1) * w])
+            d = dict(zip(keys, row[:min(w, 14)]))
+            if w > 16:
+                nk = (w - 16) // 2
+                d["kind_cycles"] = row[16:16 + nk]
+                d["kind_count"] = row[16 + nk:16 + 2 * nk]
+            out.append(d)
+        return out
 
     def step_async(self, mode: int, until_time: float, max_time: float, budget: int):
         self._check(self._L.k10s_engine_step_async(self._h, mode, until_time, max_time, budget))

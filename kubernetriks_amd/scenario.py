@@ -191,6 +191,7 @@ class SimulationConfig:
     hpa_target_threshold_tolerance: float = 0.1
     default_cluster: List[DefaultNodeGroup] = field(default_factory=list)
     score_weight: float = 1.0  # LeastAllocatedResources weight (kube_scheduler.rs:55)
+    trace_config: Optional["TraceConfig"] = None   # config.rs:16, 53-71 (host-side only)
 
     @staticmethod
     def from_dict(d: dict) -> "SimulationConfig":
@@ -223,6 +224,8 @@ class SimulationConfig:
         for g in d.get("default_cluster") or []:
             c.default_cluster.append(DefaultNodeGroup(None if g.get("node_count") is None else int(g["node_count"]),
                                                       Node.from_dict(g["node_template"])))
+        if d.get("trace_config") is not None:
+            c.trace_config = TraceConfig.from_dict(d["trace_config"])
         return c
 
     @staticmethod
@@ -253,6 +256,60 @@ class SimulationConfig:
             out.append(f"default_group {'-' if g.node_count is None else int(g.node_count)} "
                        f"{_check_name(t.name) if t.name else '-'} {int(t.cpu)} {int(t.ram)}{lab}")
         return out
+
+
+@dataclass
+class TraceConfig:
+    """TraceConfig (config.rs:53-71): exactly one of the two must be set (main.rs:62-65)."""
+    generic_cluster_trace_path: Optional[str] = None
+    generic_workload_trace_path: Optional[str] = None
+    alibaba_batch_instance_trace_path: Optional[str] = None
+    alibaba_batch_task_trace_path: Optional[str] = None
+    alibaba_machine_events_trace_path: Optional[str] = None
+    has_generic: bool = False
+    has_alibaba: bool = False
+
+    @staticmethod
+    def from_dict(d: dict) -> "TraceConfig":
+        t = TraceConfig()
+        g = d.get("generic_trace")
+        if g is not None:
+            t.has_generic = True
+            t.generic_cluster_trace_path = str(g["cluster_trace_path"])
+            t.generic_workload_trace_path = str(g["workload_trace_path"])
+        a = d.get("alibaba_cluster_trace_v2017")
+        if a is not None:
+            t.has_alibaba = True
+            t.alibaba_batch_instance_trace_path = str(a["batch_instance_trace_path"])
+            t.alibaba_batch_task_trace_path = str(a["batch_task_trace_path"])
+            m = a.get("machine_events_trace_path")
+            t.alibaba_machine_events_trace_path = None if m is None else str(m)
+        return t
+
+
+def load_traces(config: SimulationConfig, base_dir: str = ".") -> Tuple["GenericClusterTrace", "GenericWorkloadTrace"]:
+    """The trace-selection flow of main.rs:58-95: exactly one trace kind; the Alibaba v2017 kind
+    reads batch_instance / batch_task CSVs and, when given, machine events (else an empty cluster
+    trace); the generic kind reads the two YAML traces.  Relative paths are taken from base_dir
+    (the reference resolves them from its working directory)."""
+    import os
+    tc = config.trace_config
+    if tc is None:
+        raise ValueError("config has no trace_config (main.rs:60 unwraps it)")
+    if tc.has_alibaba == tc.has_generic:
+        raise ValueError("only one of trace config must be set")   # main.rs:62-65
+
+    def rd(p):
+        with open(os.path.join(base_dir, p), newline="") as f:
+            return f.read()
+
+    if tc.has_alibaba:
+        cluster = (alibaba_cluster_trace_from_csv(rd(tc.alibaba_machine_events_trace_path))
+                   if tc.alibaba_machine_events_trace_path else GenericClusterTrace())
+        return cluster, alibaba_workload_trace_from_csv(rd(tc.alibaba_batch_instance_trace_path),
+                                                        rd(tc.alibaba_batch_task_trace_path))
+    return (GenericClusterTrace.from_yaml(rd(tc.generic_cluster_trace_path)),
+            GenericWorkloadTrace.from_yaml(rd(tc.generic_workload_trace_path)))
 
 
 def test_simulation_config(**overrides) -> SimulationConfig:
@@ -366,19 +423,43 @@ def _opt_float(s: str) -> Optional[float]:
     return None if s == "" else float(s)
 
 
-def alibaba_cluster_trace_from_csv(text: str) -> GenericClusterTrace:
-    """AlibabaClusterTraceV2017::convert_to_simulator_events (cluster.rs:59-107)."""
-    out = GenericClusterTrace()
-    created, removed = set(), set()
+@dataclass
+class MachineEvent:
+    """One server_event.csv row (cluster.rs:16-38)."""
+    timestamp: int
+    machine_id: int
+    event_type: str
+    event_detail: Optional[str]
+    number_of_cpus: Optional[int]
+    normalized_memory: Optional[float]
+    normalized_disk_space: Optional[float]
+
+
+def read_machine_events_from_str(text: str) -> List[MachineEvent]:
+    """read_machine_events_from_str (cluster.rs:106-118): header-less CSV, empty cells -> None."""
+    out = []
     for row in csv.reader(io.StringIO(text)):
         if not row:
             continue
-        ts, mid, etype = int(row[0]), int(row[1]), row[2]
+        row = row + [""] * (7 - len(row))
+        out.append(MachineEvent(int(row[0]), int(row[1]), row[2], row[3] if row[3] != "" else None,
+                                _opt_int(row[4]), _opt_float(row[5]), _opt_float(row[6])))
+    return out
+
+
+def alibaba_cluster_trace_from_csv(text: str) -> GenericClusterTrace:
+    """AlibabaClusterTraceV2017::convert_to_simulator_events (cluster.rs:54-101): nodes named
+    alibaba_node_{machine_id}; a soft/hard error removes a node once, and only one that was
+    added; the events are stable-sorted by timestamp."""
+    out = GenericClusterTrace()
+    created, removed = set(), set()
+    for me in read_machine_events_from_str(text):
+        ts, mid, etype = me.timestamp, me.machine_id, me.event_type
         name = f"alibaba_node_{mid}"
         if etype == "add":
             created.add(name)
-            cpu = _opt_int(row[4])
-            mem = _opt_float(row[5])
+            cpu = me.number_of_cpus
+            mem = me.normalized_memory
             if cpu is None or mem is None:
                 raise ValueError("add event without cpus/memory (reference unwrap panics)")
             conv_cpu = (cpu * CPU_BASE) & U32_MAX                      # `as u32` truncation
@@ -391,6 +472,7 @@ def alibaba_cluster_trace_from_csv(text: str) -> GenericClusterTrace:
             out.events.append(ClusterEvent(float(ts), "remove_node", node_name=name))
         else:
             raise ValueError(f"Unsupported operation for a node in alibaba cluster trace: {etype}")
+    out.events.sort(key=lambda e: e.timestamp)   # cluster.rs:99 (stable)
     return out
 
 

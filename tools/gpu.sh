@@ -7,6 +7,7 @@
 #   bench[:ARGS]   python bench.py ARGS (default: --steps 5 --warmup 2); ARGS use ',' for spaces
 #   stats[:ARGS]   rocprofv3 --kernel-trace --stats over bench.py ARGS
 #   pmc:NAME:C1,C2,...[:ARGS]   one rocprofv3 --pmc pass (kernel trace only) over bench.py ARGS
+#   env:K=V        export K=V for the following steps (e.g. env:K10S_LIB=build/libk10s_prof.so)
 
 # Outputs go to gpurun_out/<tag>/.
 set -u
@@ -49,6 +50,8 @@ for step in "$@"; do
         --pmc $(echo "$ctrs" | tr ',' ' ') -- python3 "$R/bench.py" $(args_of "$bargs") \
         > "$O/pmc_$name.json" 2> "$O/pmc_$name.err") || { echo "PMC $name FAILED"; tail -20 "$O/pmc_$name.err"; exit 1; }
       echo "PMC $name ok" ;;
+    env)
+      export "$rest"; echo "exported $rest" ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
