@@ -257,13 +257,17 @@ typedef struct k10s_engine k10s_engine;
  * and perturb = 0).  caps may be NULL.  Returns NULL on failure (k10s_last_error). */
 k10s_engine* k10s_engine_create(const char* scenario_text, const k10s_replica_params* params,
                                 uint32_t n_replicas, const k10s_capacities* caps, int32_t device);
-/* Same as k10s_engine_create, plus a bulk block of create_pod workload events as a binary SoA blob
-   (large traces without one text line per pod; the host converter is
-   kubernetriks_amd/scenario.py:pods_blob).  Layout, little-endian:
+/* Same as k10s_engine_create, plus binary trace blocks for traces too large for one text line per
+   event (host converters: kubernetriks_amd/scenario.py pods_blob / nodes_blob, trace_soa.py).  The
+   blob is a sequence of self-delimiting little-endian SoA blocks with nothing after the last one:
      "K10SPOD1" | u64 n | f64 ts[n] | u32 cpu[n] | u32 pad (n odd) | u64 ram[n] | f64 duration[n]
-     (NaN = long-running) | u32 name_off[n + 1] | name bytes[name_off[n]]
-   The events are appended after the text's workload lines, in blob order (= trace position for
-   the stable timestamp sort, generic.rs:78-107, and for seed perturbation). */
+       (NaN = long-running) | u32 name_off[n + 1] | name bytes[name_off[n]]        -> create_pod
+     "K10SNOD1" | u64 n | f64 ts[n] | u32 cpu[n] | u32 pad (n odd) | u64 ram[n] | u32 op[n]
+       (0 create_node with capacity cpu/ram, 1 remove_node) | u32 pad (n odd)
+       | u32 name_off[n + 1] | name bytes                                           -> cluster events
+   Names are non-empty and contain none of " \t\n\v\f\r#=".  The events of each block are
+   appended after the text's lines of the same trace (workload / cluster), in block order (= trace
+   position for the stable timestamp sort, generic.rs:78-107, and for seed perturbation). */
 k10s_engine* k10s_engine_create_bulk(const char* scenario_text, const void* pods_blob, uint64_t blob_len,
                                      const k10s_replica_params* params, uint32_t n_replicas,
                                      const k10s_capacities* caps, int32_t device);

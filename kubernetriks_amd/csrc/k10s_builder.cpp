@@ -126,53 +126,82 @@ BModel model(const std::string& s) {
 
 }  // namespace
 
-// Bulk create_pod events (k10s_engine_create_bulk): a little-endian SoA blob
+// Binary trace blocks (k10s_engine_create_bulk).  The blob is a sequence of self-delimiting
+// little-endian SoA blocks; nothing may follow the last one.
 //   "K10SPOD1" | u64 n | f64 ts[n] | u32 cpu[n] | u32 pad if n odd | u64 ram[n] | f64 dur[n] (NaN: none)
-//   | u32 name_off[n + 1] | name bytes[name_off[n]]
-// Each entry becomes the same BTrace a "workload <ts> create_pod <name> <cpu> <ram> <dur|none>" line
-// would, so the compiled scenario is identical to the all-text one.
+//              | u32 name_off[n + 1] | name bytes[name_off[n]]                -> workload create_pod
+//   "K10SNOD1" | u64 n | f64 ts[n] | u32 cpu[n] | u32 pad if n odd | u64 ram[n] | u32 op[n] (0 create,
+//              1 remove) | u32 pad if n odd | u32 name_off[n + 1] | name bytes  -> cluster create/remove_node
+// Each entry becomes the same BTrace a "workload <ts> create_pod ..." / "cluster <ts> create_node ..."
+// / "cluster <ts> remove_node ..." line would (appended after the text's lines of that trace, in
+// block order), so the compiled scenario is identical to the all-text one.
 // Bytes a name in a binary block may not contain (scenario-text separators; trace_soa.BLOB_NAME_FORBIDDEN).
 #define K10S_BLOB_NAME_FORBIDDEN " \t\n\v\f\r#="
-static void parse_bulk_pods(const uint8_t* b, uint64_t len, std::vector<BTrace>& workload) {
-    uint64_t at = 0;
+static uint64_t parse_bulk_block(const uint8_t* b, uint64_t len, std::vector<BTrace>& cluster,
+                                 std::vector<BTrace>& workload) {
     auto need = [&](uint64_t bytes) {
-        if (bytes > len || at > len - bytes) throw std::runtime_error("bulk pod blob truncated");
+        if (bytes > len) throw std::runtime_error("bulk blob truncated");
     };
     need(16);
-    if (std::memcmp(b, "K10SPOD1", 8) != 0) throw std::runtime_error("bulk pod blob: bad magic");
+    const bool pods = std::memcmp(b, "K10SPOD1", 8) == 0, nodes = std::memcmp(b, "K10SNOD1", 8) == 0;
+    if (!pods && !nodes) throw std::runtime_error("bulk blob: bad magic");
     uint64_t n;
     std::memcpy(&n, b + 8, 8);
-    at = 16;
-    if (n > (1ull << 32)) throw std::runtime_error("bulk pod blob: too many pods");
-    const uint64_t o_ts = at, o_cpu = o_ts + 8 * n, o_ram = o_cpu + 4 * n + 4 * (n & 1), o_dur = o_ram + 8 * n,
-                   o_off = o_dur + 8 * n, o_chr = o_off + 4 * (n + 1);
-    at = 0;
+    if (n > (1ull << 32)) throw std::runtime_error("bulk blob: too many entries");
+    const uint64_t pad = 4 * (n & 1);
+    const uint64_t o_ts = 16, o_cpu = o_ts + 8 * n, o_ram = o_cpu + 4 * n + pad, o_x = o_ram + 8 * n;
+    const uint64_t o_off = pods ? o_x + 8 * n : o_x + 4 * n + pad, o_chr = o_off + 4 * (n + 1);
     need(o_chr);
-    at = o_off;
     std::vector<uint32_t> off(n + 1);
     std::memcpy(off.data(), b + o_off, 4 * (n + 1));
-    at = o_chr;
-    need(off[n]);
-    // the same rules as trace_soa.read_pods_blob: offsets start at 0, never decrease, and the name
-    // bytes end exactly at the end of the block
-    if (off[0] != 0 || o_chr + off[n] != len) throw std::runtime_error("bulk pod blob: bad name offsets or trailing bytes");
+    // the same rules as trace_soa.read_*_blob: offsets start at 0 and never decrease
+    if (off[0] != 0) throw std::runtime_error("bulk blob: bad name offsets");
+    need(o_chr + off[n]);
     for (uint64_t i = 0; i < n; i++) {
-        if (off[i] > off[i + 1] || off[i + 1] > off[n]) throw std::runtime_error("bulk pod blob: bad name offsets");
+        if (off[i] > off[i + 1] || off[i + 1] > off[n]) throw std::runtime_error("bulk blob: bad name offsets");
         BTrace t;
         std::memcpy(&t.ts, b + o_ts + 8 * i, 8);
-        std::memcpy(&t.cpu, b + o_cpu + 4 * i, 4);
-        std::memcpy(&t.ram, b + o_ram + 8 * i, 8);
-        double d;
-        std::memcpy(&d, b + o_dur + 8 * i, 8);
-        t.has_dur = d == d;
-        if (t.has_dur) t.dur = d;
-        t.kind = K10S_EV_AS_CREATE_POD_REQ;
-        t.name.assign(reinterpret_cast<const char*>(b + o_chr + off[i]), off[i + 1] - off[i]);
-        if (t.name.empty() || t.name.find_first_of(K10S_BLOB_NAME_FORBIDDEN) != std::string::npos)
-            throw std::runtime_error("bulk pod blob: invalid pod name");
-        t.pos = (uint32_t)workload.size();
-        workload.push_back(t);
+        uint32_t cpu;
+        uint64_t ram;
+        std::memcpy(&cpu, b + o_cpu + 4 * i, 4);
+        std::memcpy(&ram, b + o_ram + 8 * i, 8);
+        std::string name(reinterpret_cast<const char*>(b + o_chr + off[i]), off[i + 1] - off[i]);
+        if (name.empty() || name.find_first_of(K10S_BLOB_NAME_FORBIDDEN) != std::string::npos)
+            throw std::runtime_error("bulk blob: invalid name");
+        if (pods) {
+            double d;
+            std::memcpy(&d, b + o_x + 8 * i, 8);
+            t.has_dur = d == d;
+            if (t.has_dur) t.dur = d;
+            t.kind = K10S_EV_AS_CREATE_POD_REQ;
+            t.name = name;
+            t.cpu = cpu;
+            t.ram = ram;
+            t.pos = (uint32_t)workload.size();
+            workload.push_back(t);
+        } else {
+            uint32_t op;
+            std::memcpy(&op, b + o_x + 4 * i, 4);
+            if (op == 0) {
+                t.kind = K10S_EV_AS_CREATE_NODE_REQ;
+                t.node.name = name;
+                t.node.cpu = cpu;
+                t.node.ram = ram;
+            } else if (op == 1) {
+                t.kind = K10S_EV_AS_REMOVE_NODE_REQ;
+                t.name = name;
+            } else {
+                throw std::runtime_error("bulk blob: bad cluster op");
+            }
+            t.pos = (uint32_t)cluster.size();
+            cluster.push_back(t);
+        }
     }
+    return o_chr + off[n];
+}
+static void parse_bulk(const uint8_t* b, uint64_t len, std::vector<BTrace>& cluster, std::vector<BTrace>& workload) {
+    uint64_t at = 0;
+    while (at < len) at += parse_bulk_block(b + at, len - at, cluster, workload);
 }
 
 bool build_scenario(const std::string& text, uint32_t group_bound_in, uint32_t ca_bound_in, HostScenario& hs,
@@ -331,7 +360,7 @@ bool build_scenario(const std::string& text, uint32_t group_bound_in, uint32_t c
             }
         }
         if (!header) throw std::runtime_error("empty scenario");
-        if (bulk) parse_bulk_pods(bulk, bulk_len, workload);
+        if (bulk) parse_bulk(bulk, bulk_len, cluster, workload);
         if (hs.ca_enabled && cagroups.empty()) throw std::runtime_error("node groups cannot be empty for CA");
 
         auto by_ts = [](const BTrace& a, const BTrace& b) { return a.ts < b.ts; };

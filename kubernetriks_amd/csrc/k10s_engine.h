@@ -30,13 +30,31 @@ namespace k10s {
 __constant__ DevConst k10s_dc;
 __shared__ RepHdr k10s_hdr;
 #endif
+// Every read of the launch constants goes through an opaque copy of the block's address (an empty
+// asm the compiler cannot see through): the scalar loads are then issued where a value is used
+// instead of being hoisted out of the event loop and kept live across it, which is what
+// exhausted the SGPRs (and spilled them into VGPR lanes) and raised the loop's VGPR count.
+#if K10S_DEVICE
+#ifndef K10S_DC_OPAQUE
+#define K10S_DC_OPAQUE 1
+#endif
+typedef const __attribute__((address_space(4))) DevConst* DevConstPtr;
+K10S_D DevConstPtr dc_ptr() {
+    DevConstPtr p = (DevConstPtr)&k10s_dc;
+#if K10S_DC_OPAQUE
+    asm volatile("" : "+s"(p));
+#endif
+    return p;
+}
+#define K10S_DC (*dc_ptr())
+#endif
 
 // Typed accessors over one replica's region; section bases are recomputed from the (constant)
 // layout at each use instead of being held live across the event loop.
 struct Rep {
 #if K10S_DEVICE
     K10S_GB(uint8_t) b;
-    K10S_D const Layout& L() const { return k10s_dc.L; }
+    K10S_D const Layout& L() const { return K10S_DC.L; }
 #else
     uint8_t* b;
     const Layout* Lp;
@@ -87,13 +105,13 @@ inline Rep make_rep(uint8_t* base, const Layout& L, uint32_t r) {
 // sizes, trace cursor, sticky error) are fields of the working header H().
 struct Ctx {
 #if K10S_DEVICE
-    K10S_D const Scenario& S() const { return k10s_dc.sc; }
-    K10S_D const Params& P() const { return *(const Params*)(k10s_dc.params + blockIdx.x); }
-    K10S_D const Layout& Ly() const { return k10s_dc.L; }
+    K10S_D const Scenario& S() const { return K10S_DC.sc; }
+    K10S_D const Params& P() const { return *(const Params*)(K10S_DC.params + blockIdx.x); }
+    K10S_D const Layout& Ly() const { return K10S_DC.L; }
     K10S_D RepHdr& H() const { return k10s_hdr; }
     K10S_D Rep V() const {
         Rep v;
-        v.b = k10s_dc.base + (uint64_t)blockIdx.x * k10s_dc.L.stride;
+        v.b = K10S_DC.base + (uint64_t)blockIdx.x * K10S_DC.L.stride;
         return v;
     }
 #else
@@ -185,7 +203,6 @@ K10S_HD bool ev_before(double ta, uint32_t sa, double tb, uint32_t sb) {
 // The dslab queue as an 8-ary min-heap of 32-B events.  Ids are unique, so every arity pops the
 // same (time, id) order; 8-ary cuts the dependent load chain of a pop to ~log8(n) levels, and the
 // 8 children of a level (256 contiguous bytes) are loaded and compared by 8 lanes at once.
-#define K10S_HEAP_D 8
 
 // Delay classes: every emission site with a constant network delay (or delay 0) names its class;
 // emissions of one class happen in nondecreasing clock order, so clock + delay is nondecreasing
@@ -208,15 +225,16 @@ enum : int {
 // Heap position i: the top K10S_HEAP_TOP positions (levels 0-2 of the 8-ary heap) are in the working
 // header, the rest in the replica's HBM heap array.  Level boundaries coincide with K10S_HEAP_TOP,
 // so the children of one node are either all in the header or all in HBM.
-static_assert(K10S_HEAP_TOP == 1 + K10S_HEAP_D + K10S_HEAP_D * K10S_HEAP_D, "heap top = levels 0..2");
+static_assert(K10S_HEAP_D != 8 || K10S_HEAP_TOP == 1 + K10S_HEAP_D + K10S_HEAP_D * K10S_HEAP_D, "heap top = levels 0..2");
+static_assert(K10S_HEAP_D == 8 || K10S_HEAP_TOP == 1 + K10S_HEAP_D, "heap top = levels 0..1");
 // Device: both arrays are reached through address-space-typed pointers (LDS symbol, global
 // pointer), so the compiler can never merge the two paths into one generic (FLAT) access.
 #if K10S_DEVICE
 // HBM part through a raw buffer descriptor (scalar base, 32-bit offsets): distinct instructions
 // from the LDS path, so the two are never merged into one generic (FLAT) access.
 K10S_D __amdgpu_buffer_rsrc_t heap_rsrc(Ctx& c) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(c.V().b + k10s_dc.L.heap), (short)0,
-                                             (int)(k10s_dc.L.cap_heap * (uint32_t)sizeof(HeapEv)), 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(c.V().b + K10S_DC.L.heap), (short)0,
+                                             (int)(K10S_DC.L.cap_heap * (uint32_t)sizeof(HeapEv)), 0x00020000);
 }
 K10S_D HeapEv heap_get(Ctx& c, uint32_t i) {
     if (i < K10S_HEAP_TOP) return k10s_hdr.heap_lds[i];
@@ -343,10 +361,12 @@ K10S_HD uint32_t heap_min_child(Ctx& c, uint32_t first, uint32_t n, int64_t& kmi
             sq = lo[2];
         }
     }
-    static_assert(K10S_HEAP_D == 8, "the DPP reduction below covers 8-lane groups");
     keymin_step<0>(k, sq, i);
     keymin_step<1>(k, sq, i);
     keymin_step<2>(k, sq, i);
+    if constexpr (K10S_HEAP_D >= 16) keymin_step<3>(k, sq, i);
+    if constexpr (K10S_HEAP_D >= 32) keymin_step<4>(k, sq, i);
+    if constexpr (K10S_HEAP_D >= 64) keymin_step<5>(k, sq, i);
     // lanes 0..D-1 now agree; broadcast lane 0's result to the whole wave
     const uint64_t klo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)k);
     const uint64_t khi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)k >> 32));
@@ -403,15 +423,42 @@ K10S_HELPER void heap_pop(Ctx& c) {
 // Ord: other.timestamp.total_cmp(&self.timestamp) => "a <= b" <=> b.ts <= a.ts (total order).
 K10S_HD bool q_le(const QInfo& a, const QInfo& b) { return total_key(b.timestamp) <= total_key(a.timestamp); }
 
-K10S_HD uint32_t aq_sift_up(QInfo* d, uint32_t start, uint32_t pos, const QInfo& elem) {
+// Action-queue slot i: the top K10S_AQ_TOP positions in the working header, the rest in HBM.
+// Loaded entries are wave-uniform by construction; saying so keeps the sift loops scalar.
+K10S_HD QInfo aq_get(Ctx& c, uint32_t i) {
+    QInfo q;
+#if K10S_AQ_TOP
+    if (i < K10S_AQ_TOP) q = c.H().aq_lds[i];
+    else
+#endif
+        q = c.V().aq()[i];
+#if K10S_DEVICE
+    q.timestamp = uniform_f64(q.timestamp);
+    q.initial = uniform_f64(q.initial);
+    q.attempts = uniform_u32(q.attempts);
+    q.pod = uniform_u32(q.pod);
+#endif
+    return q;
+}
+K10S_HD void aq_put(Ctx& c, uint32_t i, const QInfo& q) {
+#if K10S_AQ_TOP
+    if (i < K10S_AQ_TOP) {
+        c.H().aq_lds[i] = q;
+        return;
+    }
+#endif
+    c.V().aq()[i] = q;
+}
+
+K10S_HD uint32_t aq_sift_up(Ctx& c, uint32_t start, uint32_t pos, const QInfo& elem) {
     while (pos > start) {
         uint32_t parent = (pos - 1) / 2;
-        QInfo p = d[parent];
+        QInfo p = aq_get(c, parent);
         if (q_le(elem, p)) break;
-        d[pos] = p;
+        aq_put(c, pos, p);
         pos = parent;
     }
-    d[pos] = elem;
+    aq_put(c, pos, elem);
     return pos;
 }
 K10S_HELPER void aq_push(Ctx& c, const QInfo& q) {
@@ -420,32 +467,31 @@ K10S_HELPER void aq_push(Ctx& c, const QInfo& q) {
         return;
     }
     uint32_t old = c.H().aq_size++;
-    aq_sift_up(c.V().aq(), 0, old, q);
+    aq_sift_up(c, 0, old, q);
 }
 K10S_HELPER QInfo aq_pop(Ctx& c) {
-    QInfo* d = c.V().aq();
-    QInfo item = d[--c.H().aq_size];
-    uint32_t end = c.H().aq_size;
+    const uint32_t end = --c.H().aq_size;
+    QInfo item = aq_get(c, end);
     if (end == 0) return item;
-    QInfo top = d[0];
+    QInfo top = aq_get(c, 0);
     // sift_down_to_bottom(0) with `item` in the hole, then sift_up(0, pos)
     uint32_t pos = 0;
     uint32_t child = 1;
     while (end >= 2 && child <= end - 2) {
-        QInfo a = d[child], b = d[child + 1];
+        QInfo a = aq_get(c, child), b = aq_get(c, child + 1);
         if (q_le(a, b)) {
             child += 1;
             a = b;
         }
-        d[pos] = a;
+        aq_put(c, pos, a);
         pos = child;
         child = 2 * pos + 1;
     }
     if (child == end - 1) {
-        d[pos] = d[child];
+        aq_put(c, pos, aq_get(c, child));
         pos = child;
     }
-    aq_sift_up(d, 0, pos, item);
+    aq_sift_up(c, 0, pos, item);
     return top;
 }
 
@@ -906,7 +952,19 @@ K10S_HD int schedule_scan_pruned(Ctx& c, uint32_t rc, uint64_t rr, int32_t* chos
 }
 
 // ---- scheduling cycle (scheduler.rs:246-334) ----------------------------------------------------
-K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
+// K10S_CYCLE_INLINE=0 keeps the cycle out of line on the device (a cycle runs once per many
+// events; its register-hungry body, the node scan, then does not size the event loop's VGPR
+// allocation).  At the 64-VGPR budget of 8 waves/SIMD both forms fit; inline measured 0.6 %
+// faster (profiles/r02_v1_occupancy_ab.json), so it is the default.
+#ifndef K10S_CYCLE_INLINE
+#define K10S_CYCLE_INLINE 1
+#endif
+#if K10S_CYCLE_INLINE
+#define K10S_CYCLE_FN K10S_HD
+#else
+#define K10S_CYCLE_FN K10S_HD_NOINL
+#endif
+K10S_CYCLE_FN void run_scheduling_cycle(Ctx& c, double t) {
     double cycle_dur = 0.0;
     RepHdr* h = &c.H();
     h->g_pods_q = (uint64_t)h->aq_size + (uint64_t)h->uq_size;  // scheduler.rs:256-259

@@ -22,7 +22,7 @@ using namespace k10s;
 // Occupancy knob for the event-loop kernel (0 = compiler default).  amdgpu_waves_per_eu(n) caps
 // the register allocation so that n waves fit per SIMD.
 #ifndef K10S_WAVES_PER_EU
-#define K10S_WAVES_PER_EU 5
+#define K10S_WAVES_PER_EU 8
 #endif
 #if K10S_WAVES_PER_EU > 0
 #define K10S_RUN_BOUNDS __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(K10S_WAVES_PER_EU)))

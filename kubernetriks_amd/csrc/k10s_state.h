@@ -143,13 +143,34 @@ struct HeapEv {             // dslab Event {id, time, dst, data}, 32 B
 // positions [fq_head, fq_wend) are held in a K10S_FQW-entry window, the rest in the HBM ring, and a
 // drained window is refilled K10S_FQW entries at a time by one lane-parallel load.
 #ifndef K10S_FQW
-#define K10S_FQW 8
+#define K10S_FQW 4
 #endif
 static_assert((K10S_FQW & (K10S_FQW - 1)) == 0 && K10S_FQW <= 64, "K10S_FQW: power of two <= 64");
 // The top levels of the 8-ary event heap (1 + 8 + 64 entries) live in the working header too; the
 // HBM heap array holds positions >= K10S_HEAP_TOP only.
-#ifndef K10S_HEAP_TOP
+// Arity of the dslab event heap (k10s_engine.h): 8 (top 3 levels in LDS) or 16 / 32 / 64 (top 2
+// levels in LDS; a level's children are loaded by that many lanes at once).
+#ifndef K10S_HEAP_D
+#define K10S_HEAP_D 64
+#endif
+#if K10S_HEAP_D == 8
 #define K10S_HEAP_TOP 73
+#else
+#define K10S_HEAP_TOP (1 + K10S_HEAP_D)
+#endif
+static_assert(K10S_HEAP_D == 8 || K10S_HEAP_D == 16 || K10S_HEAP_D == 32 || K10S_HEAP_D == 64, "K10S_HEAP_D");
+
+struct QInfo {              // QueuedPodInfo (queue.rs:13-27), 24 B
+    double timestamp;
+    double initial;
+    uint32_t attempts;
+    uint32_t pod;
+};
+// The scheduler's action queue (Rust BinaryHeap restatement, k10s_engine.h aq_*): positions
+// [0, K10S_AQ_TOP) (the top levels of the binary heap) live in the working header (LDS on the
+// device), the rest in the replica's HBM array.  0 = all in HBM.
+#ifndef K10S_AQ_TOP
+#define K10S_AQ_TOP 0
 #endif
 
 #ifndef K10S_PROF
@@ -201,16 +222,12 @@ struct RepHdr {
     uint32_t tr_seq, tr_pad;      // trace_cursor < n_trace)
     HeapEv fq_win[K10S_NFQ * K10S_FQW];
     HeapEv heap_lds[K10S_HEAP_TOP];
+#if K10S_AQ_TOP
+    QInfo aq_lds[K10S_AQ_TOP];
+#endif
     // cycle attribution of the event loop (K10S_PROF builds only, zero otherwise): PROF_* phases,
     // then per event kind the dispatch cycles and the count (K10S_PROF builds only hold those)
     uint64_t prof[K10S_PROF_SLOTS];
-};
-
-struct QInfo {              // QueuedPodInfo (queue.rs:13-27), 24 B
-    double timestamp;
-    double initial;
-    uint32_t attempts;
-    uint32_t pod;
 };
 
 struct GroupState {         // HPA PodGroupInfo + metrics/usage-model state of one pod group

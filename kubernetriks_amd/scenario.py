@@ -570,12 +570,35 @@ def pods_blob(pods: Sequence[Tuple[float, "Pod"]]) -> bytes:
             ram.tobytes() + dur.tobytes() + off.tobytes() + b"".join(names))
 
 
+def nodes_blob(events: Sequence["ClusterEvent"]) -> bytes:
+    """Binary SoA block of cluster events (create_node / remove_node) for k10s_engine_create_bulk
+    (include/k10s.h "K10SNOD1"): ts f64, cpu u32, ram u64, op u32 (0 create, 1 remove), names as
+    one offset table + bytes.  Nodes with labels must go through the text format."""
+    import numpy as np
+    n = len(events)
+    ts = np.array([float(e.timestamp) for e in events], dtype="<f8")
+    cpu = np.array([int(e.node.cpu) if e.kind == "create_node" else 0 for e in events], dtype="<u4")
+    ram = np.array([int(e.node.ram) if e.kind == "create_node" else 0 for e in events], dtype="<u8")
+    op = np.array([0 if e.kind == "create_node" else 1 for e in events], dtype="<u4")
+    names = [_check_name(e.node.name if e.kind == "create_node" else e.node_name).encode() for e in events]
+    if any(e.kind == "create_node" and e.node.labels for e in events):
+        raise ValueError("nodes with labels are not supported in the bulk blob")
+    off = np.zeros(n + 1, dtype="<u4")
+    off[1:] = np.cumsum([len(b) for b in names], dtype=np.uint64)
+    pad = b"\0" * (4 * (n & 1))
+    return (b"K10SNOD1" + np.array([n], dtype="<u8").tobytes() + ts.tobytes() + cpu.tobytes() + pad +
+            ram.tobytes() + op.tobytes() + pad + off.tobytes() + b"".join(names))
+
+
 def scenario_bulk(config: SimulationConfig, cluster: GenericClusterTrace,
-                  workload: GenericWorkloadTrace) -> Tuple[str, bytes]:
-    """(scenario text, pods blob) for k10s_engine_create_bulk: the workload's create_pod events go
-    into the binary blob, everything else stays text.  The engine appends the blob after the text's
-    workload lines, so the result equals scenario_text(...) when the create_pod events come last in
-    the workload trace (e.g. a pure pod trace)."""
+                  workload: GenericWorkloadTrace, cluster_blob: bool = False) -> Tuple[str, bytes]:
+    """(scenario text, blob) for k10s_engine_create_bulk: the workload's create_pod events go into a
+    binary K10SPOD1 block, and with cluster_blob=True the cluster trace into a K10SNOD1 block;
+    everything else stays text.  The engine appends each block after the text's lines of its
+    trace, so the result equals scenario_text(...) when the blocked events come last in their
+    trace (e.g. a pure pod trace, a whole cluster trace)."""
     pods = [(e.timestamp, e.pod) for e in workload.events if e.kind == "create_pod"]
     rest = GenericWorkloadTrace([e for e in workload.events if e.kind != "create_pod"])
+    if cluster_blob:
+        return scenario_text(config, GenericClusterTrace(), rest), nodes_blob(cluster.events) + pods_blob(pods)
     return scenario_text(config, cluster, rest), pods_blob(pods)

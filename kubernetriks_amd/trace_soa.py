@@ -13,6 +13,13 @@ Semantics follow ``AlibabaWorkloadTraceV2017`` in the reference:
   * duplicated task ids are an error (workload.rs:160-161).
 The result is byte-identical to ``scenario.pods_blob`` over the stable-sorted events of
 ``scenario.alibaba_workload_trace_from_csv`` (tests/test_trace_soa.py).
+
+The cluster side (server_event.csv, ``AlibabaClusterTraceV2017``, cluster.rs:54-101) streams into
+the ``K10SNOD1`` block the same way: ``alibaba_node_{machine_id}``, cpus x 1000 as u32, memory
+x 2^37 as a saturating u64, a soft/hard error removes a node once and only one that was added,
+stable-sorted by timestamp; byte-identical to ``scenario.nodes_blob`` over
+``scenario.alibaba_cluster_trace_from_csv``.  A blob for k10s_engine_create_bulk is the
+concatenation of such blocks (``split_blocks`` takes one apart).
 """
 from __future__ import annotations
 
@@ -23,9 +30,10 @@ from typing import Dict, Iterable, Optional, Tuple, Union
 
 import numpy as np
 
-from .scenario import DENORMALIZATION_BASE, U32_MAX, _check_name, _f64_as_u64, _opt_float, _opt_int
+from .scenario import CPU_BASE, DENORMALIZATION_BASE, U32_MAX, _check_name, _f64_as_u64, _opt_float, _opt_int
 
 MAGIC = b"K10SPOD1"
+NODES_MAGIC = b"K10SNOD1"
 # bytes a block name may not contain (k10s_builder.cpp K10S_BLOB_NAME_FORBIDDEN)
 BLOB_NAME_FORBIDDEN = frozenset(b" \t\n\v\f\r#=")
 _HEADER = 16
@@ -161,6 +169,116 @@ def read_pods_blob(blob: bytes) -> dict:
             raise ValueError(f"invalid pod name {b!r} in K10SPOD1 block")
         names.append(b.decode())
     return {"ts": ts, "cpu": cpu, "ram": ram, "duration": dur, "names": names}
+
+
+def alibaba_nodes_blob(machine_events: Union[str, io.TextIOBase]) -> bytes:
+    """Stream server_event.csv (path or text stream) into a sorted K10SNOD1 block (cluster.rs:54-101)."""
+    ts, cpu, ram, op = array("d"), array("I"), array("Q"), array("I")
+    name_len = array("I")
+    names = bytearray()
+    created, removed = set(), set()
+    f = _open_text(machine_events)
+    try:
+        for row in csv.reader(f):
+            if not row:
+                continue
+            row = row + [""] * (7 - len(row))
+            t, mid, etype = int(row[0]), int(row[1]), row[2]
+            if etype == "add":
+                c, mem = _opt_int(row[4]), _opt_float(row[5])
+                if c is None or mem is None:
+                    raise ValueError("add event without cpus/memory (reference unwrap panics)")
+                created.add(mid)
+                ts.append(float(t))
+                cpu.append((c * CPU_BASE) & U32_MAX)
+                ram.append(_f64_as_u64(mem * float(DENORMALIZATION_BASE)))
+                op.append(0)
+            elif etype in ("softerror", "harderror"):
+                if mid in removed or mid not in created:
+                    continue
+                removed.add(mid)
+                ts.append(float(t))
+                cpu.append(0)
+                ram.append(0)
+                op.append(1)
+            else:
+                raise ValueError(f"Unsupported operation for a node in alibaba cluster trace: {etype}")
+            name = f"alibaba_node_{mid}".encode()
+            name_len.append(len(name))
+            names += name
+    finally:
+        if f is not machine_events:
+            f.close()
+    n = len(ts)
+    ts_a = np.frombuffer(ts, "<f8")
+    order = np.argsort(ts_a, kind="stable")                     # cluster.rs:99 (stable sort_by)
+    lens = np.frombuffer(name_len, "<u4")[order].astype(np.int64)
+    src_off = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.frombuffer(name_len, "<u4"), out=src_off[1:], dtype=np.int64)
+    off = np.zeros(n + 1, dtype="<u4")
+    off[1:] = np.cumsum(lens)
+    src = np.frombuffer(names, np.uint8)
+    out_names = bytearray(int(off[-1]))
+    dst = np.frombuffer(out_names, np.uint8)
+    for k, i in enumerate(order):
+        dst[int(off[k]):int(off[k + 1])] = src[src_off[i]:src_off[i + 1]]
+    pad = b"\0" * (4 * (n & 1))
+    return (NODES_MAGIC + np.array([n], dtype="<u8").tobytes() + ts_a[order].tobytes() +
+            np.frombuffer(cpu, "<u4")[order].tobytes() + pad + np.frombuffer(ram, "<u8")[order].tobytes() +
+            np.frombuffer(op, "<u4")[order].tobytes() + pad + off.tobytes() + bytes(out_names))
+
+
+def _block_len(blob: bytes, at: int) -> int:
+    if len(blob) - at < _HEADER or blob[at:at + 8] not in (MAGIC, NODES_MAGIC):
+        raise ValueError("not a K10SPOD1 / K10SNOD1 block")
+    n = int(np.frombuffer(blob, "<u8", 1, at + 8)[0])
+    pad = 4 * (n & 1)
+    fixed = n * (8 + 4 + 8) + pad + (8 * n if blob[at:at + 8] == MAGIC else 4 * n + pad) + 4 * (n + 1)
+    if len(blob) - at < _HEADER + fixed:
+        raise ValueError("truncated block")
+    off_end = int(np.frombuffer(blob, "<u4", 1, at + _HEADER + fixed - 4)[0])
+    return _HEADER + fixed + off_end
+
+
+def split_blocks(blob: bytes) -> list:
+    """The blocks of a k10s_engine_create_bulk blob, in order (ValueError when malformed)."""
+    out, at = [], 0
+    while at < len(blob):
+        ln = _block_len(blob, at)
+        if at + ln > len(blob):
+            raise ValueError("truncated block")
+        out.append(blob[at:at + ln])
+        at += ln
+    return out
+
+
+def read_nodes_blob(blob: bytes) -> dict:
+    """Decode a K10SNOD1 block: ts, cpu, ram, op (0 create_node, 1 remove_node) columns and names,
+    with the rules of k10s_builder.cpp (ValueError when malformed)."""
+    if len(blob) < _HEADER or blob[:8] != NODES_MAGIC:
+        raise ValueError("not a K10SNOD1 block")
+    n = int(np.frombuffer(blob, "<u8", 1, 8)[0])
+    pad = 4 * (n & 1)
+    p = _HEADER
+    if len(blob) < p + n * 24 + 2 * pad + 4 * (n + 1):
+        raise ValueError("truncated K10SNOD1 block")
+    ts = np.frombuffer(blob, "<f8", n, p); p += 8 * n
+    cpu = np.frombuffer(blob, "<u4", n, p); p += 4 * n + pad
+    ram = np.frombuffer(blob, "<u8", n, p); p += 8 * n
+    op = np.frombuffer(blob, "<u4", n, p); p += 4 * n + pad
+    off = np.frombuffer(blob, "<u4", n + 1, p); p += 4 * (n + 1)
+    if off[0] != 0 or np.any(np.diff(off.astype(np.int64)) < 0) or p + int(off[-1]) != len(blob):
+        raise ValueError("bad name offsets in K10SNOD1 block")
+    if np.any(op > 1):
+        raise ValueError("bad cluster op in K10SNOD1 block")
+    raw = blob[p:]
+    names = []
+    for i in range(n):
+        b = raw[off[i]:off[i + 1]]
+        if not b or any(ch in BLOB_NAME_FORBIDDEN for ch in b):
+            raise ValueError(f"invalid node name {b!r} in K10SNOD1 block")
+        names.append(b.decode())
+    return {"ts": ts, "cpu": cpu, "ram": ram, "op": op, "names": names}
 
 
 def write_pods_blob(path: str, blob: bytes) -> None:

@@ -170,9 +170,11 @@ extern "C" int hc_debug_queues(void* p, uint32_t r, double* aq, uint32_t* aq_pod
     Rep v = make_rep(h->state.data(), h->L, r);
     *naq = v.h()->aq_size;
     *nuq = v.h()->uq_size;
+    Ctx c = make_ctx(h, r, v.h());   // the replica's header in place (aq_get reads its LDS part)
     for (uint32_t i = 0; i < v.h()->aq_size && i < cap; i++) {
-        aq[i] = v.aq()[i].timestamp;
-        aq_pod[i] = v.aq()[i].pod;
+        const QInfo q = aq_get(c, i);
+        aq[i] = q.timestamp;
+        aq_pod[i] = q.pod;
     }
     for (uint32_t i = 0; i < v.h()->uq_size && i < cap; i++) {
         uq[i] = v.uq()[i].timestamp;

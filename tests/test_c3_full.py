@@ -6,7 +6,8 @@ oracle, replica by replica and bit for bit, in two load regimes:
   unschedulable map, are moved back to the action queue on every pod finish
   (scheduler.rs:235-244, 422-440) and flushed after 300 s (188-203).
 
-The engine is built from the binary create_pod block (k10s_engine_create_bulk, §8(f)2) and runs R
+The engine is built from the binary create_pod block (k10s_engine_create_bulk, §8(f)2; the light
+cases also take the 4,096 create_node events from the binary K10SNOD1 block) and runs R
 seed-perturbed replicas in one batch; each checked replica is replayed by the oracle on its
 materialized trace (workloads.replica_scenario).  Counters (incl. attempts, requeued, flushed),
 clock, estimator bits + histograms, queue lengths and every placement (pod, node, time bits) must
@@ -28,9 +29,9 @@ def _engine(backend):
     return Engine
 
 
-def _check(backend, cluster, workload, R, checked, base_seed, max_time=1e7, tweak=None):
+def _check(backend, cluster, workload, R, checked, base_seed, max_time=1e7, tweak=None, cluster_blob=False):
     cfg = SimulationConfig()
-    scn, blob = scenario_bulk(cfg, cluster, workload)
+    scn, blob = scenario_bulk(cfg, cluster, workload, cluster_blob=cluster_blob)
     E = _engine(backend)
     probe = E(scn, 1, pods_blob=blob)
     params = wl.replica_params(probe.default_params(), R, base_seed=base_seed, perturb=True)
@@ -50,15 +51,16 @@ def _check(backend, cluster, workload, R, checked, base_seed, max_time=1e7, twea
 # ---- light load ---------------------------------------------------------------------------------
 def test_c3_4096_nodes_host():
     c, w = wl.c3_traces(n_nodes=4096, n_pods=500, arrival_window=40.0, seed=11)
-    res = _check("host", c, w, R=2, checked=[0, 1], base_seed=400)
+    res = _check("host", c, w, R=2, checked=[0, 1], base_seed=400, cluster_blob=True)
     assert all(x["counters"]["placements"] == 500 for x in res)
 
 
 @pytest.mark.gpu
 def test_c3_4096_nodes_gpu():
-    """8 replicas x 4,096 nodes x 4,096 pods (the bench's arrival rate), 4 replayed by the oracle."""
+    """8 replicas x 4,096 nodes x 4,096 pods (the bench's arrival rate), 4 replayed by the oracle;
+    the scenario is built entirely from binary blocks (K10SNOD1 cluster + K10SPOD1 pods)."""
     c, w = wl.c3_traces(n_nodes=4096, n_pods=4096, arrival_window=300.0, seed=2017)
-    res = _check("gpu", c, w, R=8, checked=[0, 3, 5, 7], base_seed=123)
+    res = _check("gpu", c, w, R=8, checked=[0, 3, 5, 7], base_seed=123, cluster_blob=True)
     for x in res:
         k = x["counters"]
         assert k["placements"] == k["attempts"] == 4096 and k["nodes_scanned"] == 4096 * 4096

@@ -219,3 +219,82 @@ def test_perturb_blob_matches_perturb_pod():
             assert (int(d["cpu"][k]), int(d["ram"][k])) == (cpu, ram), k
             got = float(d["duration"][k])
             assert (dur is None and math.isnan(got)) or got == dur, k
+
+
+# ---- the cluster side: server_event.csv -> K10SNOD1 ------------------------------------------------
+REF_MACHINES = ("49380,618,softerror,machine_fail,0,0,0\n"            # cluster.rs:152 (never added: skipped)
+                "0,924,add,,64,0.6899697150104833,0.09572460286727773\n")   # cluster.rs:172
+
+
+def _synthetic_machines(n=300, seed=3):
+    rng = random.Random(seed)
+    rows = []
+    for m in range(n):
+        t = rng.choice([0, 0, rng.randint(1, 90000)])
+        rows.append(f"{t},{m},add,,{rng.choice([32, 64, 96])},{rng.random()!r},0.1")
+        for _ in range(rng.choice([0, 0, 1, 2])):
+            rows.append(f"{rng.randint(0, 90000)},{m},{rng.choice(['softerror', 'harderror'])},machine_fail,0,0,0")
+    rows.append("12,99999,softerror,,0,0,0")     # a machine that was never added
+    rng.shuffle(rows)
+    return "\n".join(rows) + "\n"
+
+
+@pytest.mark.parametrize("data", ["reference_rows", "synthetic", "empty"])
+def test_nodes_blob_equals_object_path(data):
+    from kubernetriks_amd.scenario import alibaba_cluster_trace_from_csv, nodes_blob
+    text = {"reference_rows": REF_MACHINES, "synthetic": _synthetic_machines(), "empty": ""}[data]
+    exp = nodes_blob(alibaba_cluster_trace_from_csv(text).events)
+    got = trace_soa.alibaba_nodes_blob(io.StringIO(text))
+    assert got == exp
+    d = trace_soa.read_nodes_blob(got)
+    assert list(d["ts"]) == sorted(d["ts"])
+    if data == "reference_rows":
+        assert d["names"] == ["alibaba_node_924"] and int(d["cpu"][0]) == 64000 and int(d["op"][0]) == 0
+    # a pods block after the nodes block: one create_bulk blob, taken apart again
+    pods = trace_soa.alibaba_pods_blob(io.StringIO(REF_INSTANCES), io.StringIO(REF_TASKS))
+    assert trace_soa.split_blocks(got + pods) == [got, pods]
+
+
+def test_malformed_nodes_blob():
+    good = trace_soa.alibaba_nodes_blob(io.StringIO(_synthetic_machines(20)))
+    bad_op = bytearray(good)
+    n = int.from_bytes(good[8:16], "little")
+    p_op = 16 + 8 * n + 4 * n + 4 * (n & 1) + 8 * n
+    bad_op[p_op:p_op + 4] = (7).to_bytes(4, "little")
+    for bad in (good[:-1], good + b"x", bytes(bad_op)):
+        with pytest.raises(ValueError):
+            trace_soa.read_nodes_blob(bad)
+        with pytest.raises(ValueError):
+            HostEngine("k10s_scenario 1\nend\n", 1, pods_blob=bad)
+
+
+@pytest.mark.parametrize("backend", ["host", pytest.param("gpu", marks=pytest.mark.gpu)])
+def test_cluster_blob_runs_like_text(backend):
+    """A cluster trace with node failures (softerror/harderror removals) as a K10SNOD1 block: the
+    engine equals its own text run and the oracle, bit for bit."""
+    import oracle_jobs
+    from kubernetriks_amd.scenario import alibaba_cluster_trace_from_csv
+    E = _engine(backend)
+    rows = []
+    for m in range(40):
+        rows.append(f"0,{m},add,,64,0.6899697150104833,0.1")
+    for m in range(0, 40, 7):
+        rows.append(f"{200 + m},{m},softerror,machine_fail,0,0,0")
+    for m in range(3, 40, 11):
+        rows.append(f"{700 + m},{m},harderror,,0,0,0")   # some already removed: skipped
+    text = "\n".join(rows) + "\n"
+    cluster = alibaba_cluster_trace_from_csv(text)
+    _, workload = wl.c3_traces(n_nodes=1, n_pods=400, arrival_window=600.0, seed=6)
+    cfg = SimulationConfig()
+    full = scenario_text(cfg, cluster, workload)
+    btext, blob = scenario_bulk(cfg, cluster, workload, cluster_blob=True)
+    assert trace_soa.split_blocks(blob)[0] == trace_soa.alibaba_nodes_blob(io.StringIO(text))
+    caps = parity.parity_caps(log=True)
+    a = E(full, 1, caps=caps)
+    b = E(btext, 1, caps=caps, pods_blob=blob)
+    for e in (a, b):
+        e.run_until_all_finished(1e6)
+    assert repr(a.results()[0]) == repr(b.results()[0]) and a.event_log(0) == b.event_log(0)
+    od = oracle_jobs.replay(full)
+    assert parity.compare(od, b, log=False) == []
+    assert b.results()[0]["counters"]["pods_succeeded"] == 400

@@ -68,3 +68,20 @@ P(K10S_EV_PS_POD_FINISHED)
 P(K10S_EV_S_POD_FINISHED)
 P(K10S_EV_S_RUN_CYCLE)
 P(K10S_EV_M_GAUGE_TICK)
+
+__global__ __launch_bounds__(64) void probe_scan(uint32_t rc, uint64_t rr, double w) {
+    Ctx c;
+    int32_t chosen = -1;
+    int st = schedule_scan(c.V().s_cpu(), c.V().s_ram(), c.V().s_present(), c.S().n_nodes, rc, rr, w, &chosen);
+    c.H().flags = (uint32_t)st + (uint32_t)chosen;
+}
+
+__global__ __launch_bounds__(64) void probe_cycle(double t) {
+    Ctx c;
+    run_scheduling_cycle(c, t);
+}
+
+__global__ __launch_bounds__(64) void probe_heap_pop() {
+    Ctx c;
+    heap_pop(c);
+}

@@ -7,7 +7,9 @@
   pN     -DK10S_SCAN_PIPE=N (scan loads N steps ahead)
   qN     -DK10S_FQW=N (delay-class FIFO window entries in LDS)
   bfN    -DK10S_SCAN_BF=N (branch-free node scan)
-Usage: tools/variants.py prof w8 s1 ..."""
+  hN     -DK10S_HEAP_D=N (event-heap arity: 8, 16, 32, 64)
+  NAME=v -DK10S_NAME=v (any knob), parts joined by '+'
+Usage: tools/variants.py prof w8 s1 WAVES_PER_EU=8+FQW=4 ..."""
 import os
 import sys
 
@@ -17,8 +19,10 @@ from kubernetriks_amd.build import REPO, build  # noqa: E402
 
 def flags(name):
     out = []
-    for part in name.split("_"):
-        if part == "prof":
+    for part in name.split("+"):
+        if "=" in part:                      # any engine knob: NAME=value -> -DK10S_NAME=value
+            out.append(f"-DK10S_{part}")
+        elif part == "prof":
             out.append("-DK10S_PROF=1")
         elif part.startswith("w"):
             out.append(f"-DK10S_WAVES_PER_EU={int(part[1:])}")
@@ -26,6 +30,8 @@ def flags(name):
             out.append(f"-DK10S_SCAN_PIPE={int(part[1:])}")
         elif part.startswith("q"):
             out.append(f"-DK10S_FQW={int(part[1:])}")
+        elif part.startswith("h") and part[1:].isdigit():
+            out.append(f"-DK10S_HEAP_D={int(part[1:])}")
         elif part.startswith("bf"):
             out.append(f"-DK10S_SCAN_BF={int(part[2:])}")
         elif part.startswith("s"):
@@ -37,4 +43,5 @@ def flags(name):
 
 if __name__ == "__main__":
     for v in sys.argv[1:]:
-        print(build(force=True, extra=flags(v), out=os.path.join(REPO, "build", f"libk10s_{v}.so")))
+        tag = v.replace("=", "").replace("+", "_")
+        print(build(force=True, extra=flags(v), out=os.path.join(REPO, "build", f"libk10s_{tag}.so")))
