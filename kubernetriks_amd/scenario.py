@@ -207,6 +207,9 @@ class SimulationConfig:
         ca = d.get("cluster_autoscaler")
         if ca:
             c.ca_enabled = bool(ca.get("enabled", False))
+            # resolve_cluster_autoscaler_impl (cluster_autoscaler.rs:219-233): only the kube algorithm
+            if c.ca_enabled and ca.get("autoscaler_type", "kube_cluster_autoscaler") != "kube_cluster_autoscaler":
+                raise ValueError("Unsupported cluster autoscaler implementation")
             c.ca_scan_interval = float(ca.get("scan_interval", 10.0))
             c.ca_max_node_count = int(ca.get("max_node_count", 0))
             kca = ca.get("kube_cluster_autoscaler") or {}
@@ -218,6 +221,10 @@ class SimulationConfig:
         hpa = d.get("horizontal_pod_autoscaler")
         if hpa:
             c.hpa_enabled = bool(hpa.get("enabled", False))
+            # resolve_horizontal_pod_autoscaler_impl (horizontal_pod_autoscaler.rs:171-185)
+            if c.hpa_enabled and hpa.get("autoscaler_type",
+                                         "kube_horizontal_pod_autoscaler") != "kube_horizontal_pod_autoscaler":
+                raise ValueError("Unsupported horizontal pod autoscaler implementation")
             c.hpa_scan_interval = float(hpa.get("scan_interval", 60.0))
             khpa = hpa.get("kube_horizontal_pod_autoscaler_config") or {}
             c.hpa_target_threshold_tolerance = float(khpa.get("target_threshold_tolerance", 0.1))

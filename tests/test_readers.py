@@ -180,3 +180,23 @@ def test_load_traces_alibaba_kind(tmp_path):
     # the object path equals the reader functions called directly
     assert workload == alibaba_workload_trace_from_csv((tmp_path / "inst.csv").read_text(),
                                                        (tmp_path / "task.csv").read_text())
+
+
+def test_only_the_reference_algorithms_resolve():
+    """the engine runs the reference's only CA / HPA / usage-model algorithms; an
+    enabled autoscaler of another type is refused like resolve_*_impl's panic
+    (cluster_autoscaler.rs:219-233, horizontal_pod_autoscaler.rs:171-185)."""
+    from kubernetriks_amd.scenario import UsageModel
+    d = _c1_config_dict()
+    d["cluster_autoscaler"] = {"enabled": True, "autoscaler_type": "kube_cluster_autoscaler", "max_node_count": 5}
+    assert SimulationConfig.from_dict(d).ca_enabled
+    d["cluster_autoscaler"]["autoscaler_type"] = "my_autoscaler"
+    with pytest.raises(ValueError):
+        SimulationConfig.from_dict(d)
+    d["cluster_autoscaler"]["enabled"] = False        # a disabled one is never resolved
+    SimulationConfig.from_dict(d)
+    d["horizontal_pod_autoscaler"] = {"enabled": True, "autoscaler_type": "other"}
+    with pytest.raises(ValueError):
+        SimulationConfig.from_dict(d)
+    with pytest.raises(ValueError):
+        UsageModel.from_dict({"model_name": "linear", "config": "{}"})
