@@ -305,6 +305,10 @@ K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uin
     e.b = b;
     e.x = x;
     const int64_t k = total_key(e.time);
+    if (k < H.emit_kmin) {  // run continuation bound (continue_source); ids grow, so the first
+        H.emit_kmin = k;    // emission at a time key is the smallest (key, id) there
+        H.emit_smin = seq;
+    }
     if (cls >= 0 && cap) {
         if (tl - hd < cap && (tl == hd || k >= total_key(last))) {
             if (we == tl && tl - hd < K10S_FQW) {  // the window holds the whole ring: append
@@ -2159,10 +2163,46 @@ K10S_HD void init_replica(Ctx& c) {
 enum : int { SRC_TRACE = K10S_NFQ, SRC_HEAP = K10S_NFQ + 1 };
 
 // Which source holds the minimum (time, id): a FIFO class 0..K10S_NFQ-1, SRC_TRACE, SRC_HEAP, or
-// -1 when all are empty.  Device: lanes 0..7 hold the FIFO heads, lane 8 the heap root, lane 9 the
-// trace head; a 4-step DPP min over the 16-lane row, broadcast from lane 0.
-K10S_HD int next_source(Ctx& c, uint32_t ntr) {
+// -1 when all are empty; also the minimum (k2, s2) over the OTHER sources (run continuation).
+// Device: lanes 0..7 hold the FIFO heads, lane 8 the trace head, lane 9 the heap root; a 4-step
+// DPP min of the 64-bit time keys over the 16-lane row, then the id minimum among the lanes at that
+// key (ids are unique, so it names one lane = the source), then the same two steps again with
+// that lane masked for the runner-up.
+#if K10S_DEVICE
+template <int S>
+K10S_D int64_t kmin_step(int64_t k) {
+    uint32_t la, lb, ha, hb;
+    xpair<S>((uint32_t)(uint64_t)k, la, lb);
+    xpair<S>((uint32_t)((uint64_t)k >> 32), ha, hb);
+    const int64_t ka = (int64_t)join64(la, ha), kb = (int64_t)join64(lb, hb);
+    return kb < ka ? kb : ka;
+}
+template <int S>
+K10S_D uint32_t umin_step(uint32_t v) {
+    uint32_t a, b;
+    xpair<S>(v, a, b);
+    return a < b ? a : b;
+}
+K10S_D int64_t row16_kmin(int64_t k) {
+    k = kmin_step<0>(k);
+    k = kmin_step<1>(k);
+    k = kmin_step<2>(k);
+    k = kmin_step<3>(k);
+    const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)k);
+    const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)k >> 32));
+    return (int64_t)(lo | (hi << 32));
+}
+K10S_D uint32_t row16_umin(uint32_t v) {
+    v = umin_step<0>(v);
+    v = umin_step<1>(v);
+    v = umin_step<2>(v);
+    v = umin_step<3>(v);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+#endif
+K10S_HD int next_source(Ctx& c, uint32_t ntr, int64_t& k2, uint32_t& s2) {
     const RepHdr& H = c.H();
+    const int64_t KMAX = 0x7FFFFFFFFFFFFFFFll;
 #if K10S_DEVICE
     // every lane reads its candidate's fields in one batch of LDS reads (no branch in between), then
     // masks invalid candidates: one LDS round trip per selection
@@ -2177,55 +2217,100 @@ K10S_HD int next_source(Ctx& c, uint32_t ntr) {
     bool valid = false;
     double t = 0.0;
     uint32_t sq = 0xFFFFFFFFu;
-    int src = -1;
     if (lane < K10S_NFQ) {
         valid = qh != qt;
         t = qtime;
         sq = qseq;
-        src = lane;
     } else if (lane == SRC_HEAP) {
         valid = hs > 0;
         t = htime;
         sq = hseq;
-        src = SRC_HEAP;
     } else if (lane == SRC_TRACE) {
         valid = cur < ntr;
         t = ttime;
         sq = tseq;
-        src = SRC_TRACE;
     }
-    int64_t k = valid ? total_key(t) : 0x7FFFFFFFFFFFFFFFll;
+    int64_t k = valid ? total_key(t) : KMAX;
     sq = valid ? sq : 0xFFFFFFFFu;
-    uint32_t us = valid ? (uint32_t)src : 0xFFFFFFFFu;
-    keymin_step<0>(k, sq, us);
-    keymin_step<1>(k, sq, us);
-    keymin_step<2>(k, sq, us);
-    keymin_step<3>(k, sq, us);
-    return (int)__builtin_amdgcn_readfirstlane((int)us);
+    const int64_t kmin = row16_kmin(k);
+    if (kmin == KMAX) {
+        k2 = KMAX;
+        s2 = 0xFFFFFFFFu;
+        return -1;
+    }
+    const uint32_t smin = row16_umin(k == kmin ? sq : 0xFFFFFFFFu);
+    const uint64_t win = __ballot(lane < 16 && k == kmin && sq == smin) & 0xFFFFull;
+    const int src = (int)__builtin_ctzll(win);
+    // the runner-up among the other sources
+    const bool other = lane != src;
+    const int64_t ko = other ? k : KMAX;
+    k2 = row16_kmin(ko);
+    s2 = k2 == KMAX ? 0xFFFFFFFFu : row16_umin(ko == k2 ? sq : 0xFFFFFFFFu);
+    return src;
 #else
-    const bool ht = H.trace_cursor < ntr;
-    int64_t k = ht ? total_key(H.tr_time) : 0x7FFFFFFFFFFFFFFFll;
-    uint32_t sq = ht ? H.tr_seq : 0xFFFFFFFFu;
-    int src = ht ? SRC_TRACE : -1;
+    int64_t kk[K10S_NFQ + 2];
+    uint32_t ss[K10S_NFQ + 2];
+    for (int q = 0; q < K10S_NFQ + 2; q++) {
+        kk[q] = KMAX;
+        ss[q] = 0xFFFFFFFFu;
+    }
+    for (int q = 0; q < K10S_NFQ; q++)
+        if (H.fq_head[q] != H.fq_tail[q]) {
+            kk[q] = total_key(H.fq_top[q].time);
+            ss[q] = H.fq_top[q].seq;
+        }
+    if (H.trace_cursor < ntr) {
+        kk[SRC_TRACE] = total_key(H.tr_time);
+        ss[SRC_TRACE] = H.tr_seq;
+    }
     if (H.heap_size > 0) {
-        int64_t hk = total_key(H.heap_top.time);
-        if (src < 0 || hk < k || (hk == k && H.heap_top.seq < sq)) {
-            k = hk;
-            sq = H.heap_top.seq;
-            src = SRC_HEAP;
-        }
+        kk[SRC_HEAP] = total_key(H.heap_top.time);
+        ss[SRC_HEAP] = H.heap_top.seq;
     }
-    for (int q = 0; q < K10S_NFQ; q++) {
-        if (H.fq_head[q] == H.fq_tail[q]) continue;
-        int64_t qk = total_key(H.fq_top[q].time);
-        if (src < 0 || qk < k || (qk == k && H.fq_top[q].seq < sq)) {
-            k = qk;
-            sq = H.fq_top[q].seq;
-            src = q;
+    int src = -1;
+    for (int q = 0; q < K10S_NFQ + 2; q++)
+        if (kk[q] != KMAX && (src < 0 || kk[q] < kk[src] || (kk[q] == kk[src] && ss[q] < ss[src]))) src = q;
+    k2 = KMAX;
+    s2 = 0xFFFFFFFFu;
+    for (int q = 0; q < K10S_NFQ + 2; q++)
+        if (q != src && kk[q] != KMAX && (kk[q] < k2 || (kk[q] == k2 && ss[q] < s2))) {
+            k2 = kk[q];
+            s2 = ss[q];
         }
-    }
     return src;
 #endif
+}
+
+// Run continuation: after an event of source `src`, its next event is the global minimum without a
+// full selection when it precedes (a) the runner-up of the last full selection — the other
+// sources' heads change only by emissions — and (b) every event emitted since (those carry larger
+// ids, so an equal time still comes after).  Returns the source or -1 (do a full selection).
+K10S_HD int continue_source(Ctx& c, uint32_t ntr) {
+    const RepHdr& H = c.H();
+    const uint32_t src = H.cont_src;
+    const int64_t k2 = H.cont_k2, ek = H.emit_kmin;
+    const uint32_t s2 = H.cont_s2, es = H.emit_smin;
+    double t;
+    uint32_t sq;
+    if (src < (uint32_t)K10S_NFQ) {
+        if (H.fq_head[src] == H.fq_tail[src]) return -1;
+        t = H.fq_top[src].time;
+        sq = H.fq_top[src].seq;
+    } else if (src == (uint32_t)SRC_TRACE) {
+        if (H.trace_cursor >= ntr) return -1;
+        t = H.tr_time;
+        sq = H.tr_seq;
+    } else if (src == (uint32_t)SRC_HEAP) {
+        if (H.heap_size == 0) return -1;
+        t = H.heap_top.time;
+        sq = H.heap_top.seq;
+    } else {
+        return -1;
+    }
+    const int64_t k = total_key(t);
+    if (k > ek || (k == ek && sq > es)) return -1;   // an emitted event comes first
+    if (k < k2 || (k == k2 && sq < s2)) return (int)src;
+    return -1;
 }
 
 // Refill a drained delay-class window from the HBM ring: positions [hd, hd + min(W, tail - hd)),
@@ -2280,6 +2365,9 @@ K10S_HD bool replica_stalled(Ctx& c) {
 }
 
 // ---- the event loop -----------------------------------------------------------------------------
+#ifndef K10S_CONTINUE
+#define K10S_CONTINUE 1   // run continuation (continue_source); 0 = a full selection per event
+#endif
 // Returns 1 if the replica still has work (event budget exhausted), else 0.  The working header
 // c.H() is LDS on the device (staged by the kernel) and the replica's header in place on the host.
 K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, uint64_t budget) {
@@ -2288,6 +2376,7 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
     const Scenario* sc = &c.S();
     h->cur_kind = 0xFFFF;
     h->cur_seq = 0;
+    h->cont_src = 0xFFFFFFFFu;  // the first event of a launch takes a full selection
     const uint64_t total_pods = sc->total_pods_in_trace;
     const uint32_t ntr = sc->n_trace;
     const uint32_t cap_log = c.Ly().cap_log;
@@ -2308,7 +2397,16 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
         bool have = false;
         const uint64_t t_sel = prof_now();
         for (;;) {
-            src = next_source(c, ntr);
+            src = K10S_CONTINUE ? continue_source(c, ntr) : -1;
+            if (src < 0) {
+                int64_t k2;
+                uint32_t s2;
+                src = next_source(c, ntr, k2, s2);
+                h->cont_k2 = k2;
+                h->cont_s2 = s2;
+                h->emit_kmin = 0x7FFFFFFFFFFFFFFFll;
+            }
+            h->cont_src = (uint32_t)src;
             if (src < 0) break;
             if (src == SRC_TRACE) {
                 const uint32_t cur = h->trace_cursor;
@@ -2407,6 +2505,18 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
                 h->flags |= 1u;
             }
         }
+#if K10S_DEVICE && defined(K10S_DBG_VALU)
+        // bottleneck probe (tooling builds only): K10S_DBG_VALU extra independent VALU ops per event
+        for (int i = 0; i < K10S_DBG_VALU; i++) asm volatile("v_mov_b32 v0, v0" ::: "v0");
+#endif
+#if K10S_DEVICE && defined(K10S_DBG_LAT)
+        // bottleneck probe: K10S_DBG_LAT extra dependent LDS round trips per event
+        {
+            uint32_t x = 0;
+            for (int i = 0; i < K10S_DBG_LAT; i++) x = uniform_u32(((volatile uint32_t*)&k10s_hdr.tr_pad)[x & 0]);
+            if (x == 0xDEADBEEFu) h->flags |= 0x100u;
+        }
+#endif
         const uint64_t t_dis = prof_now();
         dispatch(c, e);
         K10S_PROF_ADD(c, PROF_DISPATCH, t_dis);

@@ -220,6 +220,13 @@ struct RepHdr {
     HeapEv heap_top;
     double tr_time;               // cached head of the shared trace stream (valid while
     uint32_t tr_seq, tr_pad;      // trace_cursor < n_trace)
+    // run continuation (k10s_engine.h run_replica): the smallest (time key, id) among the sources
+    // other than the last selected one, as of the last full selection, and the smallest time key
+    // emitted since then
+    int64_t cont_k2;
+    uint32_t cont_s2, cont_src;
+    int64_t emit_kmin;            // (time key, id) of the smallest event emitted since
+    uint32_t emit_smin, cont_pad;
     HeapEv fq_win[K10S_NFQ * K10S_FQW];
     HeapEv heap_lds[K10S_HEAP_TOP];
 #if K10S_AQ_TOP

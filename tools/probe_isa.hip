@@ -28,8 +28,10 @@ __global__ __launch_bounds__(64) void probe_dispatch(uint32_t a, uint32_t b, dou
 
 __global__ __launch_bounds__(64) void probe_select(uint32_t ntr) {
     Ctx c;
-    int src = next_source(c, ntr);
-    c.H().flags = (uint32_t)src;
+    int64_t k2;
+    uint32_t s2;
+    int src = next_source(c, ntr, k2, s2);
+    c.H().flags = (uint32_t)src + s2;
 }
 
 __global__ __launch_bounds__(64) void probe_consume_fifo(int src) {
@@ -79,6 +81,11 @@ __global__ __launch_bounds__(64) void probe_scan(uint32_t rc, uint64_t rr, doubl
 __global__ __launch_bounds__(64) void probe_cycle(double t) {
     Ctx c;
     run_scheduling_cycle(c, t);
+}
+
+__global__ __launch_bounds__(64) void probe_continue(uint32_t ntr) {
+    Ctx c;
+    c.H().flags = (uint32_t)continue_source(c, ntr);
 }
 
 __global__ __launch_bounds__(64) void probe_heap_pop() {
