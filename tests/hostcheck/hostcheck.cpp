@@ -182,3 +182,6 @@ extern "C" int hc_debug_queues(void* p, uint32_t r, double* aq, uint32_t* aq_pod
     }
     return 0;
 }
+
+// The host score (bit-identical to the device's), for tests/test_scan_adversarial.py.
+extern "C" double hc_la_score(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr) { return la_score(ac, ar, rc, rr); }

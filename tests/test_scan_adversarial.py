@@ -1,0 +1,177 @@
+"""The node scan on adversarial node sets (kube_scheduler.rs:140-148: Fit, LeastAllocated, last
+maximum in name order): ascending free ram, all-identical nodes, near-ties one unit apart, nodes
+within a few 1e-5 of the best's rc/A + rr/R, huge ram, C3-like mixes, ragged sizes.
+
+* CPU: the Python score equals the host engine's (bit-identical to the device's); the oracle's
+  schedule_one equals a direct restatement of the argmax on these sets.
+* GPU: k10s_schedule_one_batch on the same sets at 4,096 nodes vs the oracle.
+"""
+import ctypes
+import random
+
+import pytest
+
+import oracle_bridge as ob
+from hostcheck_bridge import lib as hclib
+
+U64 = (1 << 64) - 1
+EPS = 1e-5   # near-tie spread of the u = rc/A + rr/R sets
+
+
+def _hc():
+    L = hclib()
+    L.hc_la_score.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64]
+    L.hc_la_score.restype = ctypes.c_double
+    return L
+
+
+def la(ac, ar, rc, rr):
+    """plugin.rs:52-63 in Python floats (IEEE double, correctly rounded like the engine's)."""
+    return (float(ac - rc) * 100.0 / float(ac) + float(ar - rr) * 100.0 / float(ar)) / 2.0
+
+
+def test_python_score_matches_host_score():
+    L = _hc()
+    rng = random.Random(5)
+    for _ in range(3000):
+        ac = rng.randint(1, (1 << 32) - 1)
+        ar = rng.choice([rng.randint(1, 1 << 40), rng.randint(1, U64)])
+        rc, rr = rng.randint(1, ac), rng.randint(1, ar)
+        assert la(ac, ar, rc, rr) == L.hc_la_score(ac, ar, rc, rr)
+
+
+def reference_argmax(cpu, ram, present, rc, rr):
+    bi, bs = -1, None
+    for n in range(len(cpu)):
+        if present[n] and rc <= cpu[n] and rr <= ram[n]:
+            s = la(cpu[n], ram[n], rc, rr)
+            if bs is None or s >= bs:
+                bs, bi = s, n
+    return bi
+
+
+def adversarial_problems(seed, N=4096, count=24):
+    """(cpu, ram, present, rc, rr) node sets built to stress the pruning: ascending free ram (every
+    node beats the best so far: many candidates and flushes), all-identical nodes, near-ties one
+    unit apart, nodes within a few EPS of the best's rc/A + rr/R, huge ram, and C3-like mixes."""
+    rng = random.Random(seed)
+    out = []
+    for i in range(count):
+        kind = i % 8
+        rc = rng.choice([500, 1000, 1, 64000])
+        rr = rng.choice([1 << 30, 1, 1 << 28, 123456789])
+        present = [rng.random() < 0.97 for _ in range(N)]
+        if kind == 0:                               # ascending ram
+            cpu = [64000] * N
+            ram = [(1 << 34) + 4096 * n for n in range(N)]
+        elif kind == 1:                             # identical
+            cpu = [64000] * N
+            ram = [137438953472] * N
+        elif kind == 2:                             # near ties around a few identical bests
+            B, S = 64000, 1 << 37
+            cpu, ram = [], []
+            for _ in range(N):
+                t = rng.random()
+                if t < 0.2:
+                    cpu.append(B), ram.append(S)
+                elif t < 0.4:
+                    cpu.append(B - 1), ram.append(S)
+                elif t < 0.6:
+                    cpu.append(B), ram.append(S - rng.randint(1, 3))
+                elif t < 0.7:
+                    cpu.append(B - 1), ram.append(S + rng.randint(1, 3))
+                else:
+                    cpu.append(rng.randint(rc, B)), ram.append(rng.randint(rr, S))
+        elif kind == 3:                             # within a few eps of the best's u
+            B, S = rng.randint(max(rc, 1000), 100000), rng.randint(max(rr, 1 << 30), 1 << 40)
+            uy = rc / B + rr / S
+            cpu, ram = [], []
+            for _ in range(N):
+                A = min(rng.randint(max(rc, B // 2), 2 * B), (1 << 32) - 1)
+                rest = uy + rng.uniform(-0.5, 3.0) * EPS - rc / A
+                R = int(rr / rest) if rest > 0 else S
+                cpu.append(A), ram.append(max(R, rr))
+        elif kind == 4:                             # huge ram (>= 2^53), tiny relative differences
+            cpu = [rng.choice([64000, 63999, 64000]) for _ in range(N)]
+            ram = [U64 - rng.randint(0, 1 << 12) for _ in range(N)]
+        elif kind == 5:                             # C3-like: modal nodes, big nodes, one-pod nodes
+            cpu, ram = [], []
+            for _ in range(N):
+                big = rng.random() < 0.03
+                r0 = int(rng.uniform(0.69, 1.0) * (1 << 37)) if big else int(0.6899697150104833 * (1 << 37))
+                k = rng.choice([0, 0, 1, 1, 2])
+                cpu.append(64000 - 500 * k), ram.append(r0 - k * rng.choice([1 << 30, 1 << 29]))
+        elif kind == 6:                             # best only in step 0 / only at the end
+            cpu = [rng.randint(1000, 32000) for _ in range(N)]
+            ram = [rng.randint(1 << 30, 1 << 33) for _ in range(N)]
+            cpu[rng.randint(0, 255)] = 64000
+            ram[N - 1 - rng.randint(0, 3)] = 1 << 36
+        else:                                       # random, with zero and small nodes
+            cpu = [rng.choice([0, 1, rng.randint(1, 70000)]) for _ in range(N)]
+            ram = [rng.choice([0, 1, rng.randint(1, 1 << 36), rng.randint(1, U64)]) for _ in range(N)]
+        if i % 3 == 2:                              # ragged sizes
+            n = rng.choice([257, 300, 511, 4000, 1, 255, 1000])
+            cpu, ram, present = cpu[:n], ram[:n], present[:n]
+        out.append((cpu, ram, present, rc, rr))
+    return out
+
+
+def test_oracle_matches_python_argmax_on_adversarial_sets():
+    """The oracle's schedule_one (the GPU test's checker) against a direct restatement of
+    kube_scheduler.rs:140-148 on the same adversarial sets."""
+    for cpu, ram, present, rc, rr in adversarial_problems(0, N=1024, count=16):
+        names = [(f"n{i:05d}", cpu[i], ram[i]) for i in range(len(cpu)) if present[i]]
+        st, name = ob.schedule_one(names, rc, rr)
+        want = reference_argmax(cpu, ram, present, rc, rr)
+        if want < 0:
+            assert st != 0
+        else:
+            assert st == 0 and name == f"n{want:05d}"
+
+
+@pytest.mark.gpu
+def test_scan_on_adversarial_sets_matches_oracle():
+    """k10s_schedule_one_batch on the adversarial sets at
+    4,096 nodes, against the oracle's schedule_one."""
+    import torch
+    from kubernetriks_amd.native import lib
+    probs = adversarial_problems(101, N=4096, count=48)
+    R, stride = len(probs), 4096
+    N = stride
+    cpu = torch.zeros(R * stride, dtype=torch.int64)
+    ram = torch.zeros(R * stride, dtype=torch.int64)
+    bits = torch.zeros(R * stride // 64, dtype=torch.int64)
+    rcs = torch.zeros(R, dtype=torch.int64)
+    rrs = torch.zeros(R, dtype=torch.int64)
+    nnodes = []
+    for r, (c_, m_, p_, rc, rr) in enumerate(probs):
+        n = len(c_)
+        nnodes.append(n)
+        cpu[r * stride:r * stride + n] = torch.tensor(c_, dtype=torch.int64)
+        ram[r * stride:r * stride + n] = torch.tensor([x - (1 << 64) if x >= 1 << 63 else x for x in m_],
+                                                      dtype=torch.int64)
+        for w in range(stride // 64):
+            v = 0
+            for b in range(64):
+                k = w * 64 + b
+                if k < n and p_[k]:
+                    v |= 1 << b
+            bits[r * stride // 64 + w] = v - (1 << 64) if v >= 1 << 63 else v
+        rcs[r], rrs[r] = rc, rr
+    dev = torch.device("cuda:0")
+    d_cpu, d_ram, d_bits = cpu.to(torch.int32).to(dev), ram.to(dev), bits.to(dev)
+    d_rc, d_rr = rcs.to(torch.int32).to(dev), rrs.to(dev)
+    out_node = torch.full((R,), -7, dtype=torch.int32, device=dev)
+    out_st = torch.full((R,), -7, dtype=torch.int32, device=dev)
+    # absent nodes (past a problem's length) are not present, so one N serves every problem
+    assert lib().k10s_schedule_one_batch(d_cpu.data_ptr(), d_ram.data_ptr(), d_bits.data_ptr(), N, stride,
+                                         d_rc.data_ptr(), d_rr.data_ptr(), 1.0, R, out_node.data_ptr(),
+                                         out_st.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    got_n, got_s = out_node.cpu().tolist(), out_st.cpu().tolist()
+    for r, (c_, m_, p_, rc, rr) in enumerate(probs):
+        present = [(f"n{i:05d}", c_[i], m_[i]) for i in range(len(c_)) if p_[i]]
+        st, name = ob.schedule_one(present, rc, rr)
+        assert got_s[r] == st, r
+        if st == 0:
+            assert f"n{got_n[r]:05d}" == name, (r, got_n[r], name)

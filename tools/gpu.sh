@@ -3,6 +3,7 @@
 #   gpurun --timeout 900 -- 'bash tools/gpu.sh <tag> <step> [<step> ...]'
 # Steps (each under its own time limit; the first failure ends the call):
 #   tests          pytest -m gpu (one process, per-test timeout)
+#   pytest:ARGS    pytest ARGS -m gpu (e.g. pytest:tests/test_scan_prune.py)
 #   smoke          __graft_entry__.smoke()
 #   bench[:ARGS]   python bench.py ARGS (default: --steps 5 --warmup 2); ARGS use ',' for spaces
 #   stats[:ARGS]   rocprofv3 --kernel-trace --stats over bench.py ARGS
@@ -30,6 +31,11 @@ for step in "$@"; do
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread \
         > "$O/pytest_gpu.log" 2>&1 || { echo "TESTS FAILED rc=$?"; tail -30 "$O/pytest_gpu.log"; exit 1; }
       tail -1 "$O/pytest_gpu.log" ;;
+    pytest)
+      n=$(ls "$O"/pytest_sel*.log 2>/dev/null | wc -l)
+      timeout -k 10 600 python -u -m pytest $(args_of "$rest") -m gpu -x -v --timeout 180 --timeout-method thread \
+        > "$O/pytest_sel$n.log" 2>&1 || { echo "PYTEST FAILED"; tail -30 "$O/pytest_sel$n.log"; exit 1; }
+      tail -1 "$O/pytest_sel$n.log" ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 \
         || { echo "SMOKE FAILED"; tail -20 "$O/smoke.log"; exit 1; }
