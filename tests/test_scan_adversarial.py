@@ -51,8 +51,8 @@ def reference_argmax(cpu, ram, present, rc, rr):
 
 
 def adversarial_problems(seed, N=4096, count=24):
-    """(cpu, ram, present, rc, rr) node sets built to stress the pruning: ascending free ram (every
-    node beats the best so far: many candidates and flushes), all-identical nodes, near-ties one
+    """(cpu, ram, present, rc, rr) node sets built to stress a scan's argmax: ascending free ram
+    (every node beats the best so far), all-identical nodes (ties: last index), near-ties one
     unit apart, nodes within a few EPS of the best's rc/A + rr/R, huge ram, and C3-like mixes."""
     rng = random.Random(seed)
     out = []
