@@ -155,7 +155,18 @@ typedef struct k10s_replica_params {
     uint32_t perturb;                    /* 0: trace as given; 1: seed-perturbed durations/requests */
     uint64_t seed;
     uint64_t ca_max_node_count;          /* read-only here (fixed by the scenario's node pool) */
+    /* Score plugins of the default profile (kube_scheduler.rs:44-61: a weighted sum over the enabled
+       score plugins, starting from 0.0): bit 0 LeastAllocatedResources (weight score_weight), bit 1
+       MostAllocatedResources (weight most_allocated_weight).  The reference registry
+       (plugin.rs:13-23) has only LeastAllocatedResources, so bit 1 is an extension (DESIGN.md §3,
+       parity against the oracle's restatement only).  0 is refused (no score plugin: every
+       filtered node scores 0.0).  Default K10S_SCORE_LEAST_ALLOCATED. */
+    double most_allocated_weight;
+    uint32_t score_plugins;
+    uint32_t reserved0;
 } k10s_replica_params;
+#define K10S_SCORE_LEAST_ALLOCATED 1u
+#define K10S_SCORE_MOST_ALLOCATED 2u
 
 /* Capacities of per-replica engine structures (0 = derive from the scenario). */
 typedef struct k10s_capacities {

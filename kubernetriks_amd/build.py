@@ -14,7 +14,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(REPO, "kubernetriks_amd", "csrc")
 OUT = os.path.join(REPO, "build", "libk10s.so")
-SOURCES = ["k10s_kernels.hip", "k10s_host.cpp", "k10s_builder.cpp"]
+SOURCES = ["k10s_kernels.hip", "k10s_kernels_plugins.hip", "k10s_host.cpp", "k10s_builder.cpp"]
 HEADERS = ["k10s_common.h", "k10s_state.h", "k10s_engine.h", "k10s_builder.h", "k10s_results.h"]
 ARCH = os.environ.get("K10S_OFFLOAD_ARCH", "gfx950")
 

@@ -221,6 +221,8 @@ bool build_scenario(const std::string& text, uint32_t group_bound_in, uint32_t c
         d.hpa_scan_interval = 60.0;
         d.hpa_target_threshold_tolerance = 0.1;
         d.score_weight = 1.0;
+        d.most_allocated_weight = 1.0;
+        d.score_plugins = K10S_SCORE_LEAST_ALLOCATED;
         d.seed = 123;
         std::vector<BCAGroup> cagroups;
         std::vector<BDefault> defaults;
@@ -256,6 +258,12 @@ bool build_scenario(const std::string& text, uint32_t group_bound_in, uint32_t c
                 else if (k == "as_to_ca_network_delay") d.as_to_ca_network_delay = f64(v);
                 else if (k == "as_to_hpa_network_delay") d.as_to_hpa_network_delay = f64(v);
                 else if (k == "score_weight") d.score_weight = f64(v);
+                else if (k == "most_allocated_weight") d.most_allocated_weight = f64(v);
+                else if (k == "score_plugins") {
+                    d.score_plugins = (uint32_t)u64(v);
+                    if (d.score_plugins == 0 || d.score_plugins > 3)
+                        throw std::runtime_error("score_plugins must be 1 (LeastAllocated), 2 (MostAllocated) or 3 (both)");
+                }
                 else if (k == "seed") d.seed = u64(v);
                 else if (k == "sim_name") {}
                 else throw std::runtime_error("unknown config key '" + k + "'");
@@ -716,6 +724,12 @@ Scenario rebase_scenario(const Scenario& o, const uint8_t* base) {
 }
 
 // ---- per-replica layout ----------------------------------------------------------------------
+std::string params_error(const Params& p) {
+    if (p.score_plugins == 0 || p.score_plugins > (K10S_SCORE_LEAST_ALLOCATED | K10S_SCORE_MOST_ALLOCATED))
+        return "score_plugins must be 1 (LeastAllocatedResources), 2 (MostAllocatedResources) or 3 (both)";
+    return "";
+}
+
 Layout make_layout(const HostScenario& hs, const k10s_capacities& caps) {
     Layout L;
     std::memset(&L, 0, sizeof L);
@@ -752,6 +766,8 @@ Layout make_layout(const HostScenario& hs, const k10s_capacities& caps) {
     L.s_cpu = take(4 * N);
     L.s_ram = take(8 * N);
     L.s_present = take(8 * (uint64_t)L.words_nodes);
+    L.s_ccpu = take(4 * N);
+    L.s_cram = take(8 * N);
     L.pruned = caps.pruned_scan ? 1u : 0u;
     L.stall = caps.stall_guard ? 1u : 0u;
     L.bshift = 6;

@@ -70,4 +70,7 @@ Scenario rebase_scenario(const Scenario& view_offsets, const uint8_t* base);
 
 Layout make_layout(const HostScenario& hs, const k10s_capacities& caps);
 
+// Caller-supplied replica parameters the engine cannot run: "" when valid, else the reason.
+std::string params_error(const Params& p);
+
 }  // namespace k10s

@@ -67,6 +67,8 @@ struct Rep {
     K10S_HD uint64_t* s_ram() const { return at<uint64_t>(L().s_ram); }
     K10S_HD uint64_t* s_present() const { return at<uint64_t>(L().s_present); }
     K10S_HD uint32_t* s_bcpu() const { return at<uint32_t>(L().s_bcpu); }
+    K10S_HD uint32_t* s_ccpu() const { return at<uint32_t>(L().s_ccpu); }
+    K10S_HD uint64_t* s_cram() const { return at<uint64_t>(L().s_cram); }
     K10S_HD uint64_t* s_bram() const { return at<uint64_t>(L().s_bram); }
     K10S_HD NodeState& node(uint32_t n) const { return at<NodeState>(L().node)[n]; }
     K10S_HD uint64_t* pend_rm() const { return at<uint64_t>(L().pend_rm); }
@@ -169,10 +171,13 @@ K10S_HD uint64_t prof_now() {
     return 0;
 #endif
 }
-#define K10S_PROF_ADD(c, slot, t0)                                        \
-    do {                                                                  \
-        if (K10S_PROF) (c).H().prof[(slot)] += prof_now() - (t0);         \
-    } while (0)
+#if K10S_PROF
+#define K10S_PROF_ADD(c, slot, t0) ((c).H().prof[(slot)] += prof_now() - (t0))
+#define K10S_PROF_COUNT(c, slot) ((c).H().prof[(slot)] += 1)
+#else
+#define K10S_PROF_ADD(c, slot, t0) ((void)(t0))
+#define K10S_PROF_COUNT(c, slot) ((void)0)
+#endif
 
 // ---- small helpers ---------------------------------------------------------------------------
 K10S_HD bool bit_test(const uint64_t* w, uint32_t i) { return (w[i >> 6] >> (i & 63)) & 1ull; }
@@ -818,6 +823,70 @@ K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const ui
     return K10S_SCHED_OK;
 }
 
+// ---- score plugins beyond LeastAllocated alone (k10s_replica_params.score_plugins) --------------
+// MostAllocatedResources is an extension: the reference registry (plugin.rs:13-23) has only Fit and
+// LeastAllocatedResources.  Defined as kube-scheduler's MostAllocated strategy in this model's terms
+// (requested = capacity − allocatable): per resource (capacity − allocatable + request)·100 /
+// capacity, the two averaged like plugin.rs:52-63 averages its terms; u32 / u64 wrapping arithmetic
+// (a fitting node has request <= allocatable <= capacity, so nothing wraps), 0/0 = NaN.
+K10S_HD double ma_score(uint32_t ac, uint64_t ar, uint32_t cc, uint64_t cr, uint32_t rc, uint64_t rr) {
+    double cpu_score = (double)(uint32_t)(cc - ac + rc) * 100.0 / (double)cc;
+    double ram_score = (double)(uint64_t)(cr - ar + rr) * 100.0 / (double)cr;
+    return (cpu_score + ram_score) / 2.0;
+}
+// The profile's weighted sum (kube_scheduler.rs:113-138): 0.0, then += score · weight per enabled
+// plugin in registry order (LeastAllocated, MostAllocated).
+K10S_HD double plugin_score(uint32_t ac, uint64_t ar, uint32_t cc, uint64_t cr, uint32_t rc, uint64_t rr,
+                            uint32_t plugins, double w_la, double w_ma) {
+    double s = 0.0;
+    if (plugins & K10S_SCORE_LEAST_ALLOCATED) s += la_score(ac, ar, rc, rr) * w_la;
+    if (plugins & K10S_SCORE_MOST_ALLOCATED) s += ma_score(ac, ar, cc, cr, rc, rr) * w_ma;
+    return s;
+}
+// schedule_one with the plugin set (any weights, NaN and filtered[0] rules of kube_scheduler.rs:
+// 140-148 as in schedule_scan): lanes stride the nodes (ascending per lane, "score >= best" keeps
+// the lane's last maximum), then the cross-lane (score_key, index) max.  Reads the capacity SoA
+// only for MostAllocated; IEEE divisions (the opt-in path is not the tuned one).
+#ifndef K10S_SCORE_PLUGINS
+#define K10S_SCORE_PLUGINS 1   // 0: the plugin path is not compiled (k10s_kernels.hip's default copy)
+#endif
+K10S_HD int schedule_scan_plugins(Ctx& c, uint32_t rc, uint64_t rr, int32_t* chosen) {
+    const uint32_t N = c.S().n_nodes;
+    const uint32_t* cpu = c.V().s_cpu();
+    const uint64_t* ram = c.V().s_ram();
+    const uint32_t* ccpu = c.V().s_ccpu();
+    const uint64_t* cram = c.V().s_cram();
+    const uint64_t* pres = c.V().s_present();
+    const uint32_t plugins = c.P().score_plugins;
+    const double w_la = c.P().score_weight, w_ma = c.P().most_allocated_weight;
+    uint64_t best_key = 0;
+    int32_t best_n = -1;
+    int32_t first = 0x7fffffff;
+    for (uint32_t n = (uint32_t)lane_id(); n < N; n += K10S_LANES) {
+        if (!bit_test(pres, n)) continue;
+        const uint32_t ac = cpu[n];
+        const uint64_t ar = ram[n];
+        if (rc <= ac && rr <= ar) {
+            if ((int32_t)n < first) first = (int32_t)n;
+            const double s = plugin_score(ac, ar, ccpu[n], cram[n], rc, rr, plugins, w_la, w_ma);
+            if (!is_nan(s)) {
+                const uint64_t k = score_key(s);
+                if (k >= best_key) {
+                    best_key = k;
+                    best_n = (int32_t)n;
+                }
+            }
+        }
+    }
+    first = wave_min_i32(first);
+    wave_argmax(best_key, best_n);
+    if (first == 0x7fffffff) return K10S_SCHED_NO_SUFFICIENT_RESOURCES;
+    const uint32_t f = (uint32_t)uniform_u32((uint32_t)first);
+    const double s0 = plugin_score(cpu[f], ram[f], ccpu[f], cram[f], rc, rr, plugins, w_la, w_ma);
+    *chosen = is_nan(s0) ? (int32_t)f : best_n;
+    return K10S_SCHED_OK;
+}
+
 // ---- block bounds of the scheduler cache and the exact pruned scan ------------------------------
 // The node cache is cut into blocks of 2^bshift consecutive indices (64 <= block, <= 64 blocks);
 // s_bcpu[b] / s_bram[b] hold the largest allocatable cpu / ram over the block's present nodes (0 if
@@ -968,7 +1037,8 @@ K10S_HD int schedule_scan_pruned(Ctx& c, uint32_t rc, uint64_t rr, int32_t* chos
 #else
 #define K10S_CYCLE_FN K10S_HD_NOINL
 #endif
-K10S_CYCLE_FN void run_scheduling_cycle(Ctx& c, double t) {
+template <bool PLUG>
+K10S_CYCLE_FN void run_scheduling_cycle_t(Ctx& c, double t) {
     double cycle_dur = 0.0;
     RepHdr* h = &c.H();
     h->g_pods_q = (uint64_t)h->aq_size + (uint64_t)h->uq_size;  // scheduler.rs:256-259
@@ -997,14 +1067,19 @@ K10S_CYCLE_FN void run_scheduling_cycle(Ctx& c, double t) {
             st = -1;
             uint32_t nread = 0;
             const uint64_t t_scan = prof_now();
-            if (c.Ly().pruned && w == 1.0 && rc > 0 && rr > 0) st = schedule_scan_pruned(c, rc, rr, &chosen, &nread);
+            if (PLUG) {
+                st = schedule_scan_plugins(c, rc, rr, &chosen);
+                nread = c.S().n_nodes;
+            } else if (c.Ly().pruned && w == 1.0 && rc > 0 && rr > 0) {
+                st = schedule_scan_pruned(c, rc, rr, &chosen, &nread);
+            }
             if (st < 0) {
                 st = schedule_scan(c.V().s_cpu(), c.V().s_ram(), c.V().s_present(), c.S().n_nodes, rc, rr, w, &chosen);
                 nread = c.S().n_nodes;
             }
             h->counters[K10S_C_NODES_READ] += nread;
             K10S_PROF_ADD(c, PROF_SCAN, t_scan);
-            if (K10S_PROF) h->prof[PROF_NSCAN] += 1;
+            K10S_PROF_COUNT(c, PROF_NSCAN);
         }
         if (st != K10S_SCHED_OK) {
             q.timestamp = t + cycle_dur;
@@ -1075,12 +1150,19 @@ K10S_HD void s_release(Ctx& c, uint32_t p) {  // release_node_resources (153-162
     node_bound_changed(c, (uint32_t)n);
 }
 
+K10S_HD void run_scheduling_cycle(Ctx& c, double t) { run_scheduling_cycle_t<false>(c, t); }
+// A replica whose profile is not LeastAllocated alone (K10S_SCORE_PLUGINS builds only: the host
+// engine and k10s_kernels_plugins.hip; compiled into the default kernel, the branch alone cost
+// 4.6 % at C3, profiles/r02_v4_score_plugins_ab.json).
+K10S_HD void run_scheduling_cycle_plugins(Ctx& c, double t) { run_scheduling_cycle_t<true>(c, t); }
+
 K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
     RepHdr* h = &c.H();
     switch (e.kind) {
     case K10S_EV_S_RUN_CYCLE: {
         const uint64_t t0 = prof_now();
-        run_scheduling_cycle(c, e.time);
+        if (K10S_SCORE_PLUGINS && c.P().score_plugins != K10S_SCORE_LEAST_ALLOCATED) run_scheduling_cycle_plugins(c, e.time);
+        else run_scheduling_cycle(c, e.time);
         K10S_PROF_ADD(c, PROF_CYCLE, t0);
         break;
     }
@@ -1094,6 +1176,10 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
         uint64_t ar = f2u(e.x);
         c.V().s_cpu()[n] = ac;
         c.V().s_ram()[n] = ar;
+        // the stored node's capacity: a node reaches the scheduler straight from its creation,
+        // allocatable = capacity (node.rs:60-66); only MostAllocated reads it
+        c.V().s_ccpu()[n] = ac;
+        c.V().s_cram()[n] = ar;
         if (!bit_test(c.V().s_present(), n)) {
             bit_set(c.V().s_present(), n);
             h->s_node_count += 1;
@@ -2138,6 +2224,8 @@ K10S_HD void init_replica(Ctx& c) {
         }
         s_cpu[n] = sc->def_cpu[def];
         s_ram[n] = sc->def_ram[def];
+        v.s_ccpu()[n] = sc->def_cpu[def];
+        v.s_cram()[n] = sc->def_ram[def];
         bit_set(v.s_present(), n);
     }
     h->s_node_count = sc->n_default;
@@ -2337,7 +2425,7 @@ K10S_HD void consume_source(Ctx& c, int src) {
         const uint64_t t_hp = prof_now();
         heap_pop(c);
         K10S_PROF_ADD(c, PROF_HEAPPOP, t_hp);
-        if (K10S_PROF) H.prof[PROF_NHEAPPOP] += 1;
+        K10S_PROF_COUNT(c, PROF_NHEAPPOP);
     } else {
         const uint32_t hd = H.fq_head[src] + 1;
         H.fq_head[src] = hd;

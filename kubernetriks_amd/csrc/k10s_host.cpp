@@ -18,6 +18,10 @@ using namespace k10s;
 hipError_t k10s_launch_init(const DevConst* h_dc, uint32_t n_replicas, hipStream_t s);
 hipError_t k10s_launch_run(const DevConst* h_dc, uint32_t n_replicas, int mode, double until_time, double max_time,
                            uint64_t budget, uint32_t* d_active, hipStream_t s);
+// the same two kernels with the score-plugin profile path compiled in (k10s_kernels_plugins.hip)
+hipError_t k10s_launch_init_plugins(const DevConst* h_dc, uint32_t n_replicas, hipStream_t s);
+hipError_t k10s_launch_run_plugins(const DevConst* h_dc, uint32_t n_replicas, int mode, double until_time,
+                                   double max_time, uint64_t budget, uint32_t* d_active, hipStream_t s);
 hipError_t k10s_launch_schedule(const uint32_t* alloc_cpu, const uint64_t* alloc_ram, const uint64_t* present,
                                 uint32_t n_nodes, uint32_t node_stride, const uint32_t* req_cpu, const uint64_t* req_ram,
                                 double weight, uint32_t n_problems, int32_t* out_node, int32_t* out_status,
@@ -54,6 +58,7 @@ struct k10s_engine {
     DevConst* h_dc = nullptr;      // pinned launch constants
     std::vector<Params> params;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool plugins = false;          // some replica's profile is not LeastAllocated alone
 };
 
 // All engines of a device launch on one stream: the launch constants are one __constant__ block per
@@ -84,7 +89,7 @@ static void engine_free(k10s_engine* e) {
 
 static int32_t engine_init(k10s_engine* e) {
     HIPCHK(hipSetDevice(e->device));
-    HIPCHK(k10s_launch_init(e->h_dc, e->R, e->stream));
+    HIPCHK((e->plugins ? k10s_launch_init_plugins : k10s_launch_init)(e->h_dc, e->R, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     return K10S_OK;
 }
@@ -270,6 +275,13 @@ k10s_engine* k10s_engine_create_bulk(const char* scenario_text, const void* pods
             e->params[r].seed = e->hs.defaults.seed + r;
         }
         e->params[r].ca_max_node_count = e->hs.defaults.ca_max_node_count;  // fixed by the node pool
+        if (e->params[r].score_plugins != K10S_SCORE_LEAST_ALLOCATED) e->plugins = true;
+        const std::string perr = params_error(e->params[r]);
+        if (!perr.empty()) {
+            set_err(K10S_E_INVALID, "params[" + std::to_string(r) + "]: " + perr);
+            delete e;
+            return nullptr;
+        }
     }
     auto fail = [&](const std::string& m) -> k10s_engine* {
         set_err(K10S_E_HIP, m);
@@ -333,8 +345,8 @@ int32_t k10s_engine_step_async(k10s_engine* e, int32_t mode, double until_time, 
     if (mode != K10S_RUN_UNTIL_ALL_FINISHED && mode != K10S_RUN_UNTIL_TIME) return set_err(K10S_E_INVALID, "bad mode");
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipMemsetAsync(e->d_active, 0, 4, e->stream));
-    HIPCHK(k10s_launch_run(e->h_dc, e->R, mode, until_time, max_time, max_events_per_launch, e->d_active,
-                           e->stream));
+    HIPCHK((e->plugins ? k10s_launch_run_plugins : k10s_launch_run)(e->h_dc, e->R, mode, until_time, max_time,
+                                                                     max_events_per_launch, e->d_active, e->stream));
     HIPCHK(hipMemcpyAsync(e->h_active, e->d_active, 4, hipMemcpyDeviceToHost, e->stream));
     return K10S_OK;
 }

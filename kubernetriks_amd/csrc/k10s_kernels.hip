@@ -15,6 +15,13 @@
 #include <mutex>
 
 #define K10S_KERNEL_TU 1
+// The score-plugin profile path (k10s_replica_params.score_plugins other than LeastAllocated
+// alone) is compiled only into the second copy of the event-loop kernels, k10s_kernels_plugins.hip
+// (same code, renamed symbols); an engine launches that copy only when one of its replicas needs
+// it, so the default kernel's register allocation never pays for the extension.
+#ifndef K10S_SCORE_PLUGINS
+#define K10S_SCORE_PLUGINS 0
+#endif
 #include "k10s_engine.h"
 
 using namespace k10s;
@@ -62,6 +69,7 @@ __global__ K10S_RUN_BOUNDS void k10s_run_kernel(uint32_t n_replicas, int mode, d
     if (more && threadIdx.x == 0) atomicAdd(active, 1u);
 }
 
+#ifndef K10S_PLUGINS_TU
 __global__ __launch_bounds__(64) void k10s_schedule_kernel(const uint32_t* __restrict__ alloc_cpu,
                                                              const uint64_t* __restrict__ alloc_ram,
                                                              const uint64_t* __restrict__ present, uint32_t n_nodes,
@@ -104,6 +112,8 @@ __global__ __launch_bounds__(256) void k10s_score_kernel(const uint32_t* __restr
 #endif
 }
 
+#endif  // !K10S_PLUGINS_TU
+
 // ---- launchers (called from k10s_host.cpp) -------------------------------------------------------
 // The launch constants live in the one __constant__ block k10s_dc, so every engine launch first
 // copies its block (from pinned host memory, stream-ordered) and then launches; engines of a device
@@ -132,6 +142,7 @@ hipError_t k10s_launch_run(const DevConst* h_dc, uint32_t n_replicas, int mode, 
     return hipGetLastError();
 }
 
+#ifndef K10S_PLUGINS_TU
 hipError_t k10s_launch_schedule(const uint32_t* alloc_cpu, const uint64_t* alloc_ram, const uint64_t* present,
                                 uint32_t n_nodes, uint32_t node_stride, const uint32_t* req_cpu, const uint64_t* req_ram,
                                 double weight, uint32_t n_problems, int32_t* out_node, int32_t* out_status,
@@ -148,3 +159,4 @@ hipError_t k10s_launch_score(const uint32_t* alloc_cpu, const uint64_t* alloc_ra
                        alloc_ram, req_cpu, req_ram, weight, n, out);
     return hipGetLastError();
 }
+#endif  // !K10S_PLUGINS_TU

@@ -1,0 +1,13 @@
+// k10s_kernels_plugins.hip — the event-loop kernels (init + run) compiled a second time with the
+// score-plugin profile path in (K10S_SCORE_PLUGINS=1: MostAllocatedResources and multi-plugin
+// profiles, k10s_engine.h run_scheduling_cycle_plugins).  Symbols are renamed so both copies live in
+// one library; k10s_host.cpp launches this copy only for engines with such a replica.
+#define K10S_SCORE_PLUGINS 1
+#define K10S_PLUGINS_TU 1
+#define k10s_dc k10s_dc_plugins
+#define k10s_hdr k10s_hdr_plugins
+#define k10s_init_kernel k10s_init_kernel_plugins
+#define k10s_run_kernel k10s_run_kernel_plugins
+#define k10s_launch_init k10s_launch_init_plugins
+#define k10s_launch_run k10s_launch_run_plugins
+#include "k10s_kernels.hip"

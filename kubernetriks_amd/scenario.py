@@ -191,6 +191,11 @@ class SimulationConfig:
     hpa_target_threshold_tolerance: float = 0.1
     default_cluster: List[DefaultNodeGroup] = field(default_factory=list)
     score_weight: float = 1.0  # LeastAllocatedResources weight (kube_scheduler.rs:55)
+    # The default profile's score plugins (kube_scheduler.rs:44-61) as bits: 1 LeastAllocatedResources,
+    # 2 MostAllocatedResources — an extension: the reference registry (plugin.rs:13-23) has only the
+    # first, and its config.yaml has no profile section; `scheduler_score_plugins` below adds one.
+    score_plugins: int = 1
+    most_allocated_weight: float = 1.0
     trace_config: Optional["TraceConfig"] = None   # config.rs:16, 53-71 (host-side only)
 
     @staticmethod
@@ -233,7 +238,34 @@ class SimulationConfig:
                                                       Node.from_dict(g["node_template"])))
         if d.get("trace_config") is not None:
             c.trace_config = TraceConfig.from_dict(d["trace_config"])
+        if d.get("scheduler_score_plugins") is not None:
+            c.set_score_plugins(d["scheduler_score_plugins"])
         return c
+
+    SCORE_PLUGIN_BITS = {"LeastAllocatedResources": 1, "MostAllocatedResources": 2}
+
+    def set_score_plugins(self, plugins) -> None:
+        """Extension key `scheduler_score_plugins`: a list of {name, weight} like the default profile's
+        Plugins.score (kube_scheduler.rs:29-41, 52-55).  Unknown names are refused like
+        PLUGIN_REGISTRY.get(..).unwrap() (kube_scheduler.rs:124); a plugin may appear once.  (With
+        two plugins the order does not matter: 0.0 + a + b == 0.0 + b + a.)"""
+        bits = 0
+        for p in plugins:
+            name = p["name"]
+            if name not in self.SCORE_PLUGIN_BITS:
+                raise ValueError(f"unknown score plugin {name!r}")
+            b = self.SCORE_PLUGIN_BITS[name]
+            if bits & b:
+                raise ValueError(f"score plugin {name!r} listed twice")
+            bits |= b
+            w = float(p["weight"])          # Plugin.weight.unwrap() (kube_scheduler.rs:131)
+            if b == 1:
+                self.score_weight = w
+            else:
+                self.most_allocated_weight = w
+        if bits == 0:
+            raise ValueError("scheduler_score_plugins is empty")
+        self.score_plugins = bits
 
     @staticmethod
     def from_yaml(text: str) -> "SimulationConfig":
@@ -248,6 +280,10 @@ class SimulationConfig:
             out.append(f"config {k}_network_delay {_f(getattr(self, k + '_network_delay'))}")
         if self.score_weight != 1.0:
             out.append(f"config score_weight {_f(self.score_weight)}")
+        if self.score_plugins != 1:
+            out.append(f"config score_plugins {int(self.score_plugins)}")
+        if self.most_allocated_weight != 1.0:
+            out.append(f"config most_allocated_weight {_f(self.most_allocated_weight)}")
         out.append(f"ca_config enabled {int(self.ca_enabled)} scan_interval {_f(self.ca_scan_interval)} "
                    f"max_node_count {int(self.ca_max_node_count)} scale_down_utilization_threshold "
                    f"{_f(self.ca_scale_down_utilization_threshold)}")

@@ -255,6 +255,8 @@ def config_for_params(cfg: SimulationConfig, p) -> SimulationConfig:
     c.hpa_scan_interval = p.hpa_scan_interval
     c.hpa_target_threshold_tolerance = p.hpa_target_threshold_tolerance
     c.score_weight = p.score_weight
+    c.score_plugins = p.score_plugins
+    c.most_allocated_weight = p.most_allocated_weight
     return c
 
 

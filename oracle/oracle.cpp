@@ -209,6 +209,10 @@ struct Config {
     double hpa_scan_interval = 60.0;
     double hpa_tolerance = 0.1;
     double score_weight = 1.0;      /* LeastAllocatedResources weight, kube_scheduler.rs:55 */
+    /* score plugins of the default profile: bit 0 LeastAllocatedResources, bit 1 MostAllocatedResources
+       (an extension: not in the reference registry, plugin.rs:13-23) */
+    uint32_t score_plugins = 1;
+    double most_allocated_weight = 1.0;
 };
 
 struct DefaultGroup {
@@ -315,7 +319,21 @@ static double least_allocated_score(const Pod& pod, const Node& node) {
     return (cpu_score + ram_score) / 2.0;
 }
 
-static int schedule_one(const Pod& pod, const std::map<std::string, Node>& nodes, double weight,
+/* MostAllocatedResources (extension, no reference counterpart): kube-scheduler's MostAllocated
+   strategy with requested = capacity - allocatable, per resource (cap - alloc + request) * 100 / cap,
+   the two averaged as plugin.rs:52-63 averages its terms; wrapping u32/u64 arithmetic. */
+static double most_allocated_score(const Pod& pod, const Node& node) {
+    double cpu_score = (double)(uint32_t)(node.cap_cpu - node.alloc_cpu + pod.cpu) * 100.0 / (double)node.cap_cpu;
+    double ram_score = (double)(uint64_t)(node.cap_ram - node.alloc_ram + pod.ram) * 100.0 / (double)node.cap_ram;
+    return (cpu_score + ram_score) / 2.0;
+}
+
+struct ScoreProfile {                 /* the default profile's score plugins (kube_scheduler.rs:44-61) */
+    uint32_t plugins = 1;             /* bit 0 LeastAllocatedResources, bit 1 MostAllocatedResources */
+    double w_la = 1.0, w_ma = 1.0;
+};
+
+static int schedule_one(const Pod& pod, const std::map<std::string, Node>& nodes, const ScoreProfile& prof,
                         std::string& out) {
     if (pod.cpu == 0 && pod.ram == 0) return SE_ZEROS;                /* 74-76 */
     if (nodes.empty()) return SE_NO_NODES;                             /* 78-80 */
@@ -333,12 +351,21 @@ static int schedule_one(const Pod& pod, const std::map<std::string, Node>& nodes
     }
     if (filtered.empty()) return SE_NO_SUFFICIENT;                     /* 109-111 */
     std::map<std::string, std::pair<const Node*, double>> node_scores; /* 113 */
-    for (const Node* n : filtered) {
-        auto it = node_scores.find(n->name);
-        if (it == node_scores.end()) it = node_scores.emplace(n->name, std::make_pair(n, 0.0)).first;
-        double s = least_allocated_score(pod, *n) * weight;
-        it->second.second += s;
-    }
+    /* 115-138: one pass per score plugin in profile order, node_scores[name] += score * weight */
+    if (prof.plugins & 1u)
+        for (const Node* n : filtered) {
+            auto it = node_scores.find(n->name);
+            if (it == node_scores.end()) it = node_scores.emplace(n->name, std::make_pair(n, 0.0)).first;
+            double s = least_allocated_score(pod, *n) * prof.w_la;
+            it->second.second += s;
+        }
+    if (prof.plugins & 2u)
+        for (const Node* n : filtered) {
+            auto it = node_scores.find(n->name);
+            if (it == node_scores.end()) it = node_scores.emplace(n->name, std::make_pair(n, 0.0)).first;
+            double s = most_allocated_score(pod, *n) * prof.w_ma;
+            it->second.second += s;
+        }
     const std::string* assigned = &filtered[0]->name;                   /* 140-148 */
     double max_score = node_scores.at(*assigned).second;
     for (auto& kv : node_scores) {
@@ -1176,7 +1203,11 @@ void Sim::run_scheduling_cycle(double t) {                                /* 246
         double sched_time = 0.000001 * (double)s_nodes.size();   /* model.rs:24-26 */
         cycle_dur += sched_time;
         std::string assigned;
-        int r = schedule_one(pod, s_nodes, cfg.score_weight, assigned);
+        ScoreProfile prof;
+        prof.plugins = cfg.score_plugins;
+        prof.w_la = cfg.score_weight;
+        prof.w_ma = cfg.most_allocated_weight;
+        int r = schedule_one(pod, s_nodes, prof, assigned);
         if (!(pod.cpu == 0 && pod.ram == 0) && !s_nodes.empty()) c.attempts++;
         if (r != SE_OK) {
             next.timestamp = t + cycle_dur;
@@ -1704,6 +1735,11 @@ static void parse_scenario(Sim& sim, const std::string& text) {
             else if (k == "as_to_ca_network_delay") c.as_to_ca = pf(tk[2]);
             else if (k == "as_to_hpa_network_delay") c.as_to_hpa = pf(tk[2]);
             else if (k == "score_weight") c.score_weight = pf(tk[2]);
+            else if (k == "most_allocated_weight") c.most_allocated_weight = pf(tk[2]);
+            else if (k == "score_plugins") {
+                c.score_plugins = (uint32_t)pu64(tk[2]);
+                if (c.score_plugins == 0 || c.score_plugins > 3) throw std::runtime_error("score_plugins must be 1, 2 or 3");
+            }
             else if (k == "seed" || k == "sim_name") {}
             else throw std::runtime_error("unknown config key " + k);
         } else if (h == "ca_config" || h == "hpa_config") {
@@ -2001,7 +2037,9 @@ int orc_schedule_one(int n, const char** names, const uint32_t* cpu, const uint6
     pod.cpu = pcpu;
     pod.ram = pram;
     std::string res;
-    int r = schedule_one(pod, nodes, weight, res);
+    ScoreProfile prof;
+    prof.w_la = weight;
+    int r = schedule_one(pod, nodes, prof, res);
     if (r == SE_OK && out && outlen > 0) std::snprintf(out, (size_t)outlen, "%s", res.c_str());
     return r;
 }

@@ -71,6 +71,12 @@ void* hc_create_bulk(const char* text, const void* blob, uint64_t blob_len, cons
             h->params[r].seed = h->hs.defaults.seed + r;
         }
         h->params[r].ca_max_node_count = h->hs.defaults.ca_max_node_count;
+        const std::string perr = params_error(h->params[r]);
+        if (!perr.empty()) {
+            if (err) std::snprintf(err, (size_t)errlen, "params[%u]: %s", r, perr.c_str());
+            delete h;
+            return nullptr;
+        }
     }
     h->state.assign((size_t)h->L.stride * R, 0);
     for (uint32_t r = 0; r < R; r++) {
