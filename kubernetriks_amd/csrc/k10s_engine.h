@@ -2547,8 +2547,7 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
         h->clock = e.time;
         h->cur_kind = e.kind;
         h->cur_seq = e.seq;
-        done++;
-        h->counters[K10S_C_EVENTS] += 1;
+        done++;  // counters[K10S_C_EVENTS] takes the launch's count once, at exit (no per-event LDS RMW)
         if (cap_log) {
             uint32_t k = h->log_n;
             if (k < cap_log) {
@@ -2619,6 +2618,7 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
         }
     }
     K10S_PROF_ADD(c, PROF_LOOP, t_loop);
+    h->counters[K10S_C_EVENTS] += done;
     if (h->error_code) status = K10S_REPLICA_ERROR;
     h->status = status;
     return more;

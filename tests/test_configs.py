@@ -96,3 +96,51 @@ def test_c5_parameter_sweep_over_autoscalers(backend):
         od = o.result(placements=True)
         od["status_name"] = parity.ORACLE_STATUS[4] if not od["panicked"] else "error"
         assert parity.compare(od, eng, r=k, log=False) == [], idx[k]
+
+
+# ---- the BASELINE sizes on the GPU ------------------------------------------------------------
+# Full replica counts per GPU (C2: 1,024; C4: 1,024; C5: 8,192 = 65,536 / 8 GPUs) in one batch,
+# with whole-batch properties (every replica terminates, the finish-hook identity
+# simulation_callbacks.rs:73-76 holds, the perturbation/sweep makes replicas differ) and bit-exact
+# oracle replays of replicas spread over the batch (first, last, both halves' edges).
+def _identity(res):
+    for r in res:
+        k = r["counters"]
+        assert k["terminated_pods"] == k["pods_succeeded"] + k["pods_unschedulable"] + k["pods_failed"] + \
+            k["pods_removed"], r
+
+
+@pytest.mark.gpu
+def test_c2_at_baseline_size_gpu():
+    R = 1024
+    eng = _batch_parity("gpu", wl.c2_parts(n_pods=300, seed=123),
+                        lambda d, n: wl.replica_params(d, n, base_seed=123, perturb=True), R,
+                        check=[0, 1, 511, 512, 1022, 1023])
+    res = eng.results()
+    assert all(r["status"] == "finished" for r in res)
+    _identity(res)
+    # perturbed durations: the pod-duration estimators differ (finish times are multiples of 1000 s)
+    assert len({tuple(r["estimators"]["pod_duration"][1:5]) for r in res}) > R // 4
+
+
+@pytest.mark.gpu
+def test_c4_at_baseline_size_gpu():
+    R = 1024
+    eng = _batch_parity("gpu", wl.c4_parts(n_batch_pods=80, seed=7),
+                        lambda d, n: wl.replica_params(d, n, base_seed=7, perturb=True), R,
+                        check=[0, 511, 1023], mode=RUN_UNTIL_TIME, until=1500.0)
+    res = eng.results()
+    assert sum(r["counters"]["total_scaled_up_nodes"] > 0 for r in res) == R
+
+
+@pytest.mark.gpu
+def test_c5_sweep_at_baseline_size_gpu():
+    """One GPU's share of the 65,536-replica sweep (8,192 replicas) on 4,096-node clusters."""
+    R = 8192
+    parts = (wl.SimulationConfig(),) + wl.c3_traces(n_nodes=4096, n_pods=600, arrival_window=200.0, seed=11)
+    eng = _batch_parity("gpu", parts, lambda d, n: wl.c5_params(d, n, base_seed=123), R,
+                        check=[0, 7, 4095, 8191])
+    res = eng.results()
+    assert all(r["status"] == "finished" for r in res)
+    _identity(res)
+    assert len({tuple(r["estimators"]["pod_queue_time"][1:5]) for r in res}) >= 8   # cycle interval x cond. move
