@@ -31,7 +31,8 @@ def main():
         "method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over one bench "
                   "step; values in KiB per dispatch; FETCH_SIZE doubled (gfx950 reports half of 16-B/lane streaming "
                   "reads, MI355X_MICROARCH.md HBM section); WRITE_SIZE as read",
-        "kernel": kernel, "config": json.loads(config), "launches": [nf, nw],
+        "kernel": kernel, "config": json.loads(config), "workload": cfg.get("workload_name", "c3"),
+        "launches": [nf, nw],
         "engine": b.get("engine"), "scan_mode": b.get("roofline", {}).get("scan_mode", "full"),
         "fetch_size_kib": fk, "write_size_kib": wk,
         "hbm_bytes_per_launch": (2.0 * fk + wk) * 1024.0 if fk is not None and wk is not None else None,
