@@ -17,17 +17,21 @@ def main():
     b = json.loads(open(bench_json).read().strip().splitlines()[-1])
     launches = max(1, b["steps"] + b["warmup"])
     events = b["totals"]["events"] / max(1, b["steps"]) if b.get("totals") else None
-    ctr, ns = {}, []
+    ctr, seen, ns = {}, {}, []
     for d in dirs:
+        mine = {}
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for row in csv.DictReader(open(f)):
                 if row["Kernel_Name"].startswith(kernel):
-                    ctr[row["Counter_Name"]] = ctr.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+                    mine[row["Counter_Name"]] = mine.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+        for k, v in mine.items():   # a counter taken in several passes: their mean
+            ctr[k] = ctr.get(k, 0.0) + v
+            seen[k] = seen.get(k, 0) + 1
         for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
             for row in csv.DictReader(open(f)):
                 if row["Kernel_Name"].startswith(kernel):
                     ns.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
-    per = {k: v / launches for k, v in ctr.items()}   # per launch
+    per = {k: v / seen[k] / launches for k, v in ctr.items()}   # per launch
     kns = sum(ns) / len(ns) if ns else None
     der = {}
     g = per.get("GRBM_GUI_ACTIVE")
