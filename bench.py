@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--cpu-workers", type=int, default=0, help="0 = the usable host cores (cgroup quota / affinity)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scan-kernel", action="store_true", help="skip the scheduling-kernel-alone measurement")
+    ap.add_argument("--no-backlog-line", action="store_true",
+                    help="skip the one-launch c3_backlog measurement reported beside a c3 run")
     ap.add_argument("--pruned-scan", action="store_true", help="exact block-bound pruned scan (DESIGN.md §3)")
     ap.add_argument("--profile", action="store_true", help="print the K10S_PROF cycle attribution (variant builds)")
     ap.add_argument("--selftest-host", action="store_true",
@@ -375,10 +377,55 @@ def main():
             out["profile"]["by_kind"] = {EVENT_KIND_NAMES.get(k, str(k)): {"count": kn[k], "share_of_loop": kc[k] / loop,
                                                                          "cycles_per_event": kc[k] / max(kn[k], 1)}
                                          for k in range(len(kc)) if kn[k]}
+    if rank == 0 and world == 1 and args.workload == "c3" and not args.no_backlog_line and not args.selftest_host:
+        # the same replicas under load (failed attempts, unschedulable map, move-all, flush): one launch
+        try:
+            del eng
+            out["backlog"] = backlog_line(args, cfg, make_engine, caps, ensemble, NUM_COUNTERS, version)
+        except Exception as ex:
+            log("backlog measurement failed:", ex)
+            out["backlog"] = None
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def backlog_line(args, cfg, make_engine, caps, ensemble, num_counters, version):
+    """One launch of the c3_backlog workload (same replica count, nodes and pods) beside a c3 run, so
+    the default bench line also shows the regime where attempts fail.  Not the headline value."""
+    import argparse
+    import numpy as np
+    import torch
+    from kubernetriks_amd.scenario import scenario_bulk
+    b = argparse.Namespace(**vars(args))
+    b.workload = "c3_backlog"
+    cluster, workload, desc = build_workload(b)
+    scn, blob = scenario_bulk(cfg, cluster, workload)
+    probe = make_engine(scn, 1, blob=blob)
+    defaults = probe.default_params()
+    del probe
+    params = ensemble.shard_params(defaults, args.replicas, 0, base_seed=123, perturb=True)
+    eng = make_engine(scn, args.replicas, params=params, caps=caps, blob=blob)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ms = eng.run_until_all_finished(max_time=1e7)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    c = np.zeros(num_counters, dtype=np.int64)
+    for r in eng.raw_results():
+        c += np.array([int(r.counters[k]) for k in range(num_counters)], dtype=np.int64)
+    placements, attempts, scanned = int(c[12]), int(c[13]), int(c[15])
+    per_launch = 12.0 * scanned + 12.0 * attempts + 12.0 * placements
+    achieved = per_launch / (ms * 1e-3) if ms > 0 else 0.0
+    log(f"backlog: {placements / elapsed / 1e6:.2f} M placements/s, run {ms:.1f} ms")
+    return {"workload": desc, "workload_name": "c3_backlog", "steps": 1, "warmup": 0,
+            "placements_per_s": placements / elapsed, "attempts_per_s": attempts / elapsed,
+            "ms_per_step": elapsed * 1e3, "kernel_ms_per_launch": ms,
+            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK, "algorithmic_bytes_per_launch": per_launch},
+            "totals": {"placements": placements, "attempts": attempts, "requeued": int(c[17]), "flushed": int(c[18])},
+            "engine": version()}
 
 
 if __name__ == "__main__":
