@@ -1025,12 +1025,13 @@ K10S_HD int schedule_scan_pruned(Ctx& c, uint32_t rc, uint64_t rr, int32_t* chos
 }
 
 // ---- scheduling cycle (scheduler.rs:246-334) ----------------------------------------------------
-// K10S_CYCLE_INLINE=0 keeps the cycle out of line on the device (a cycle runs once per many
-// events; its register-hungry body, the node scan, then does not size the event loop's VGPR
-// allocation).  At the 64-VGPR budget of 8 waves/SIMD both forms fit; inline measured 0.6 %
-// faster (profiles/r02_v1_occupancy_ab.json), so it is the default.
+// K10S_CYCLE_INLINE=0 (default) keeps the cycle out of line on the device: a cycle runs once per
+// many events, and out of line its attempt loop (the node scans, the queue pops) gets its own
+// register allocation instead of sharing the event loop's.  With the action queue's top levels in
+// LDS (K10S_AQ_TOP=15) it measured +1.2 % on C3 and +16.7 % on the backlog workload, where cycles
+// run many attempts (profiles/r02_v5_knobs_ab.json).
 #ifndef K10S_CYCLE_INLINE
-#define K10S_CYCLE_INLINE 1
+#define K10S_CYCLE_INLINE 0
 #endif
 #if K10S_CYCLE_INLINE
 #define K10S_CYCLE_FN K10S_HD

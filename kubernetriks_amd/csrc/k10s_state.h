@@ -168,9 +168,10 @@ struct QInfo {              // QueuedPodInfo (queue.rs:13-27), 24 B
 };
 // The scheduler's action queue (Rust BinaryHeap restatement, k10s_engine.h aq_*): positions
 // [0, K10S_AQ_TOP) (the top levels of the binary heap) live in the working header (LDS on the
-// device), the rest in the replica's HBM array.  0 = all in HBM.
+// device), the rest in the replica's HBM array.  0 = all in HBM.  Default 15 (levels 0-3, 360 B of
+// LDS): pops and pushes of the cycle's queue touch HBM only below level 3 (profiles/r02_v5_knobs_ab.json).
 #ifndef K10S_AQ_TOP
-#define K10S_AQ_TOP 0
+#define K10S_AQ_TOP 15
 #endif
 
 #ifndef K10S_PROF
