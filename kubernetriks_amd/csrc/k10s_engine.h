@@ -634,6 +634,12 @@ K10S_HD double la_score(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr) {
 // 3 KiB steps in flight instead of waiting one memory round trip per step.
 // Requires s_cpu / s_ram 16-B aligned and readable up to the next multiple of 4 nodes (engine
 // sections are 256-B padded; the unit surface's rows are node_stride (multiple of 64) long).
+// K10S_SCAN_PIPE: the unit-surface kernel (k10s_schedule_kernel, HBM-bound: 1 measured best);
+// K10S_LOOP_SCAN_PIPE: the scans inside the event loop (0 measured +1.2 % on C3 and +1.7 % on the
+// backlog workload over 1 with the cycle out of line, profiles/r02_v5_knobs_ab.json).
+#ifndef K10S_LOOP_SCAN_PIPE
+#define K10S_LOOP_SCAN_PIPE 0
+#endif
 #ifndef K10S_SCAN_PIPE
 #define K10S_SCAN_PIPE 1
 #endif
@@ -767,7 +773,7 @@ K10S_D void scan_grp(const ScanGrp& g, uint32_t n0, uint32_t n_nodes, uint32_t r
         scan_node_d<W1, TF>(n0 + 3, bits & 8u, g.cv.w, g.r23.y, rc, rr, frc, frr, weight, first, best_s, best_n);
     }
 }
-template <bool W1, bool TF>
+template <bool W1, bool TF, int PIPE>
 K10S_D void scan_lanes(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
                        uint32_t rc, uint64_t rr, double weight, int32_t& first, double& best_s, int32_t& best_n) {
     const uint32_t l4 = 4u * (uint32_t)lane_id();
@@ -776,19 +782,21 @@ K10S_D void scan_lanes(const uint32_t* s_cpu, const uint64_t* s_ram, const uint6
     rr = uniform_u64(rr);
     const double frc = uniform_f64((double)rc), frr = uniform_f64(u64_f64(rr));
     if (n_nodes == 0) return;
-    // Software pipeline: loads run K10S_SCAN_PIPE steps (of 256 nodes) ahead of the arithmetic.
-    ScanGrp g[K10S_SCAN_PIPE + 1];
+    // Software pipeline: loads run PIPE steps (of 256 nodes) ahead of the arithmetic.
+    ScanGrp g[PIPE + 1];
 #pragma unroll
-    for (int i = 0; i < K10S_SCAN_PIPE; i++) g[i] = scan_load(s_cpu, s_ram, present, n_nodes, 256u * i + l4);
+    for (int i = 0; i < PIPE; i++) g[i] = scan_load(s_cpu, s_ram, present, n_nodes, 256u * i + l4);
     for (uint32_t base = 0; base < n_nodes; base += 256) {
-        g[K10S_SCAN_PIPE] = scan_load(s_cpu, s_ram, present, n_nodes, base + 256u * K10S_SCAN_PIPE + l4);
+        g[PIPE] = scan_load(s_cpu, s_ram, present, n_nodes, base + 256u * PIPE + l4);
         scan_grp<W1, TF>(g[0], base + l4, n_nodes, rc, rr, frc, frr, weight, first, best_s, best_n);
 #pragma unroll
-        for (int i = 0; i < K10S_SCAN_PIPE; i++) g[i] = g[i + 1];
+        for (int i = 0; i < PIPE; i++) g[i] = g[i + 1];
     }
 }
 #endif
 
+// LOOP: the event loop's scans (K10S_LOOP_SCAN_PIPE) rather than the unit surface's (K10S_SCAN_PIPE).
+template <bool LOOP = false>
 K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
                           uint32_t rc, uint64_t rr, double weight, int32_t* chosen) {
     uint64_t best_key = 0;
@@ -800,15 +808,17 @@ K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const ui
         // A fitting node has alloc >= request > 0 in both resources, so neither term is 0/0 and every
         // score is a finite number >= 0: filtered[0] is never NaN, "some node fits" <=> best_n >= 0,
         // and neither filtered[0] nor its re-scored value is needed (kube_scheduler.rs:140-148).
-        scan_lanes<true, false>(s_cpu, s_ram, present, n_nodes, rc, rr, weight, first, best_s, best_n);
+        scan_lanes<true, false, LOOP ? K10S_LOOP_SCAN_PIPE : K10S_SCAN_PIPE>(s_cpu, s_ram, present, n_nodes, rc, rr,
+                                                                            weight, first, best_s, best_n);
         best_key = best_n >= 0 ? score_key(best_s) : 0;
         wave_argmax(best_key, best_n);
         if (best_n < 0) return K10S_SCHED_NO_SUFFICIENT_RESOURCES;
         *chosen = best_n;
         return K10S_SCHED_OK;
     }
-    if (weight == 1.0) scan_lanes<true, true>(s_cpu, s_ram, present, n_nodes, rc, rr, weight, first, best_s, best_n);
-    else scan_lanes<false, true>(s_cpu, s_ram, present, n_nodes, rc, rr, weight, first, best_s, best_n);
+    constexpr int P = LOOP ? K10S_LOOP_SCAN_PIPE : K10S_SCAN_PIPE;
+    if (weight == 1.0) scan_lanes<true, true, P>(s_cpu, s_ram, present, n_nodes, rc, rr, weight, first, best_s, best_n);
+    else scan_lanes<false, true, P>(s_cpu, s_ram, present, n_nodes, rc, rr, weight, first, best_s, best_n);
     best_key = best_n >= 0 ? score_key(best_s) : 0;
 #else
     for (uint32_t n = 0; n < n_nodes; n++)
@@ -1075,7 +1085,8 @@ K10S_CYCLE_FN void run_scheduling_cycle_t(Ctx& c, double t) {
                 st = schedule_scan_pruned(c, rc, rr, &chosen, &nread);
             }
             if (st < 0) {
-                st = schedule_scan(c.V().s_cpu(), c.V().s_ram(), c.V().s_present(), c.S().n_nodes, rc, rr, w, &chosen);
+                st = schedule_scan<true>(c.V().s_cpu(), c.V().s_ram(), c.V().s_present(), c.S().n_nodes, rc, rr, w,
+                                         &chosen);
                 nread = c.S().n_nodes;
             }
             h->counters[K10S_C_NODES_READ] += nread;
