@@ -266,8 +266,7 @@ def main():
     for i in range(args.steps):
         ms = one_step()
         kernel_ms.append(ms)
-        for r in eng.raw_results():
-            counters += np.array([int(r.counters[k]) for k in range(NUM_COUNTERS)], dtype=np.int64)
+        counters += eng.counter_matrix().sum(axis=0, dtype=np.uint64).astype(np.int64)
         log(f"[rank {rank}] step {i}: run {ms:.1f} ms")
     if backend == "nccl":
         torch.cuda.synchronize()
@@ -412,9 +411,7 @@ def backlog_line(args, cfg, make_engine, caps, ensemble, num_counters, version):
     ms = eng.run_until_all_finished(max_time=1e7)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    c = np.zeros(num_counters, dtype=np.int64)
-    for r in eng.raw_results():
-        c += np.array([int(r.counters[k]) for k in range(num_counters)], dtype=np.int64)
+    c = eng.counter_matrix().sum(axis=0, dtype=np.uint64).astype(np.int64)
     placements, attempts, scanned = int(c[12]), int(c[13]), int(c[15])
     per_launch = 12.0 * scanned + 12.0 * attempts + 12.0 * placements
     achieved = per_launch / (ms * 1e-3) if ms > 0 else 0.0

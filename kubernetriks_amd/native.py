@@ -186,6 +186,15 @@ class EngineBase:
         self._check(self._fn["results"](self._h, arr))
         return arr
 
+    def counter_matrix(self, arr=None):
+        """The replicas' counters as one (R, NUM_COUNTERS) uint64 numpy view of a results array
+        (no per-replica Python loop)."""
+        import numpy as np
+        if arr is None:
+            arr = self.raw_results()
+        return np.ndarray((len(arr), NUM_COUNTERS), dtype="<u8", buffer=arr, offset=ReplicaResult.counters.offset,
+                          strides=(ctypes.sizeof(ReplicaResult), 8))
+
     def results(self) -> List[dict]:
         return [result_to_dict(r) for r in self.raw_results()]
 

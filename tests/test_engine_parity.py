@@ -402,3 +402,15 @@ def test_bulk_pod_blob_rejects_malformed():
 def test_bulk_pod_blob_equals_text_gpu():
     from kubernetriks_amd.native import Engine
     _bulk_pair(Engine)
+
+
+def test_counter_matrix_view_equals_results():
+    """bench.py sums counters through EngineBase.counter_matrix (a numpy view of the results array)."""
+    from kubernetriks_amd.native import COUNTER_NAMES
+    scn = gen.random_scenario(5, n_pods=40)
+    e = HostEngine(scn, 3)
+    e.run_until_all_finished(20000.0)
+    m = e.counter_matrix()
+    assert m.shape == (3, len(COUNTER_NAMES))
+    for r, res in enumerate(e.results()):
+        assert [int(x) for x in m[r]] == [res["counters"][k] for k in COUNTER_NAMES]
