@@ -205,9 +205,10 @@ K10S_HD bool ev_before(double ta, uint32_t sa, double tb, uint32_t sb) {
     return ka < kb || (ka == kb && sa < sb);
 }
 
-// The dslab queue as an 8-ary min-heap of 32-B events.  Ids are unique, so every arity pops the
-// same (time, id) order; 8-ary cuts the dependent load chain of a pop to ~log8(n) levels, and the
-// 8 children of a level (256 contiguous bytes) are loaded and compared by 8 lanes at once.
+// The dslab queue as a K10S_HEAP_D-ary (default 64) min-heap of 32-B events.  Ids are unique, so
+// every arity pops the same (time, id) order; a wide heap cuts the dependent load chain of a pop to
+// ~log_D(n) levels, and the D children of a level (contiguous) are loaded and compared by D lanes
+// at once.
 
 // Delay classes: every emission site with a constant network delay (or delay 0) names its class;
 // emissions of one class happen in nondecreasing clock order, so clock + delay is nondecreasing
@@ -227,7 +228,7 @@ enum : int {
     FQ_NOW = 7,          // emit_now (delay 0)
 };
 
-// Heap position i: the top K10S_HEAP_TOP positions (levels 0-2 of the 8-ary heap) are in the working
+// Heap position i: the top K10S_HEAP_TOP positions (levels 0-1; 0-2 for arity 8) are in the working
 // header, the rest in the replica's HBM heap array.  Level boundaries coincide with K10S_HEAP_TOP,
 // so the children of one node are either all in the header or all in HBM.
 static_assert(K10S_HEAP_D != 8 || K10S_HEAP_TOP == 1 + K10S_HEAP_D + K10S_HEAP_D * K10S_HEAP_D, "heap top = levels 0..2");
@@ -352,7 +353,7 @@ K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uin
 K10S_HD uint32_t emit0(Ctx& c, uint32_t kind, double delay) { return emit(c, kind, delay, -1, 0, 0, 0.0); }
 
 // Smallest (time, id) among children [first, min(first + D, n)); returns its index.  Device: lanes
-// 0..7 load one child each (one 256-B read) and reduce with 3 DPP steps.
+// 0..D-1 load one child's key each (one contiguous read) and reduce with log2(D) DPP/permlane steps.
 K10S_HD uint32_t heap_min_child(Ctx& c, uint32_t first, uint32_t n, int64_t& kmin, uint32_t& smin) {
 #if K10S_DEVICE
     const int lane = lane_id();

@@ -146,8 +146,8 @@ struct HeapEv {             // dslab Event {id, time, dst, data}, 32 B
 #define K10S_FQW 4
 #endif
 static_assert((K10S_FQW & (K10S_FQW - 1)) == 0 && K10S_FQW <= 64, "K10S_FQW: power of two <= 64");
-// The top levels of the 8-ary event heap (1 + 8 + 64 entries) live in the working header too; the
-// HBM heap array holds positions >= K10S_HEAP_TOP only.
+// The top levels of the event heap (K10S_HEAP_TOP entries: 1 + 64 at the default arity 64) live in
+// the working header too; the HBM heap array holds positions >= K10S_HEAP_TOP only.
 // Arity of the dslab event heap (k10s_engine.h): 8 (top 3 levels in LDS) or 16 / 32 / 64 (top 2
 // levels in LDS; a level's children are loaded by that many lanes at once).
 #ifndef K10S_HEAP_D
