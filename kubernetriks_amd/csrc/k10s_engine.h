@@ -796,6 +796,108 @@ K10S_D void scan_lanes(const uint32_t* s_cpu, const uint64_t* s_ram, const uint6
 }
 #endif
 
+// ---- screened scan (event loop, weight 1.0, rc > 0, rr > 0; K10S_SCAN_SCREEN) -----------------
+// With u = rc/A + rr/R, a fitting node's LeastAllocated score is 100 − 50·u (plugin.rs:52-63), so
+// the argmax is the u minimum.  Each lane keeps lu, the smallest u among the nodes it scored, and
+// after every 256-node step the wave takes thr = min lu: some scored node y has u(y) <= thr
+// (within f32 rounding).  A later node x whose single-precision, division-free test
+//     rc·R + rr·A  >  A·R·(thr + eps)            (scan_screen, eps = 1e-5)
+// holds has, in exact arithmetic, u(x) > u(y) + 9.9e-6 − 36·2^-24 > u(y) + 7e-6, so its exact
+// score is more than 3e-4 below y's and its computed f64 score is strictly below y's computed
+// score (each within 3.4e-14 of exact): x can never be the (score, last index) argmax, and is
+// not scored.  Every other fitting node is scored exactly as in scan_node_d — except a node with
+// exactly the lane's best allocatables, which has exactly its score and just takes the index.
+// f32 ranges: A·R < 2^96, no overflow; all operands >= 1, no denormals.  The bound is checked at
+// and around the threshold by tests/test_scan_screen.py through the host form of this test.
+#define K10S_SCREEN_EPS 1e-5f
+K10S_HD bool scan_screen(uint32_t ac, uint64_t ar, float fa, float fr, float T) {
+    const float fA = (float)ac;
+    const float fR = __builtin_fmaf((float)(uint32_t)(ar >> 32), 4294967296.0f, (float)(uint32_t)ar);
+    return __builtin_fmaf(fa, fR, fr * fA) > fA * fR * T;
+}
+// u of a scored node from its exact score: (100 − s)/50, rounded to f32.
+K10S_HD float screen_u(double s) { return (float)((100.0 - s) * 0.02); }
+
+#if K10S_DEVICE
+// 1 (default): the event loop's fast-path scans screen (+2.0 % at C3 once the scheduling cycle runs
+// out of line with its own registers, profiles/r02_v6_scan_screen_ab.json; inlined into the event
+// loop its state spilled inside the scan, r02_v3_scan_experiments_ab.json).  The unit-surface
+// kernel keeps the plain scan (it is HBM-bound).
+#ifndef K10S_SCAN_SCREEN
+#define K10S_SCAN_SCREEN 1
+#endif
+K10S_D void scan_node_screen(uint32_t n, bool present, uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr, double frc,
+                             double frr, float fa, float fr, float T, double& best_s, int32_t& best_n, uint32_t& la,
+                             uint64_t& lr, float& lu) {
+    if (rc <= ac && rr <= ar && present) {
+        if (ac == la && ar == lr) {
+            best_n = (int32_t)n;
+        } else if (!scan_screen(ac, ar, fa, fr, T)) {
+            const double fac = (double)ac;
+            const double cs = div_rn((fac - frc) * 100.0, fac);
+            const uint2 w = __builtin_bit_cast(uint2, ar);
+            const double far = u64_f64(ar);
+            double dr = far - frr;
+            if (__builtin_expect(w.y >= (1u << 21), 0)) dr = u64_f64(ar - rr);
+            const double s = (cs + div_rn(dr * 100.0, far)) * 0.5;
+            if (s >= best_s) {
+                best_s = s;
+                best_n = (int32_t)n;
+                la = ac;
+                lr = ar;
+            }
+            const float u = screen_u(s);
+            lu = u < lu ? u : lu;
+        }
+    }
+}
+template <int S>
+K10S_D float minf_step(float v) {
+    uint32_t a, b;
+    xpair<S>(__builtin_bit_cast(uint32_t, v), a, b);
+    const float fa = __builtin_bit_cast(float, a), fb = __builtin_bit_cast(float, b);
+    return fa < fb ? fa : fb;
+}
+K10S_D float wave_min_f32(float v) {
+    v = minf_step<0>(v); v = minf_step<1>(v); v = minf_step<2>(v);
+    v = minf_step<3>(v); v = minf_step<4>(v); v = minf_step<5>(v);
+    return v;
+}
+template <int PIPE>
+K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
+                              uint32_t rc, uint64_t rr, double& best_s, int32_t& best_n) {
+    const uint32_t l4 = 4u * (uint32_t)lane_id();
+    rc = uniform_u32(rc);
+    rr = uniform_u64(rr);
+    const double frc = uniform_f64((double)rc), frr = uniform_f64(u64_f64(rr));
+    const float fa = (float)rc;
+    const float fr = __builtin_fmaf((float)(uint32_t)(rr >> 32), 4294967296.0f, (float)(uint32_t)rr);
+    if (n_nodes == 0) return;
+    uint32_t la = 0;   // the lane best's allocatables (0: none; a fitting node has both >= 1)
+    uint64_t lr = 0;
+    float lu = __builtin_inff();
+    float T = __builtin_inff();  // thr + eps: +inf screens nothing out (the first step)
+    ScanGrp g[PIPE + 1];
+#pragma unroll
+    for (int i = 0; i < PIPE; i++) g[i] = scan_load(s_cpu, s_ram, present, n_nodes, 256u * i + l4);
+    for (uint32_t base = 0; base < n_nodes; base += 256) {
+        g[PIPE] = scan_load(s_cpu, s_ram, present, n_nodes, base + 256u * PIPE + l4);
+        const uint32_t n0 = base + l4;
+        const uint32_t bits = grp_bits(g[0], n0, n_nodes);
+        if (bits) {
+            scan_node_screen(n0, bits & 1u, g[0].cv.x, g[0].r01.x, rc, rr, frc, frr, fa, fr, T, best_s, best_n, la, lr, lu);
+            scan_node_screen(n0 + 1, bits & 2u, g[0].cv.y, g[0].r01.y, rc, rr, frc, frr, fa, fr, T, best_s, best_n, la, lr, lu);
+            scan_node_screen(n0 + 2, bits & 4u, g[0].cv.z, g[0].r23.x, rc, rr, frc, frr, fa, fr, T, best_s, best_n, la, lr, lu);
+            scan_node_screen(n0 + 3, bits & 8u, g[0].cv.w, g[0].r23.y, rc, rr, frc, frr, fa, fr, T, best_s, best_n, la, lr, lu);
+        }
+        const float thr = __builtin_bit_cast(float, uniform_u32(__builtin_bit_cast(uint32_t, wave_min_f32(lu))));
+        T = thr + K10S_SCREEN_EPS;
+#pragma unroll
+        for (int i = 0; i < PIPE; i++) g[i] = g[i + 1];
+    }
+}
+#endif
+
 // LOOP: the event loop's scans (K10S_LOOP_SCAN_PIPE) rather than the unit surface's (K10S_SCAN_PIPE).
 template <bool LOOP = false>
 K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
@@ -809,8 +911,11 @@ K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const ui
         // A fitting node has alloc >= request > 0 in both resources, so neither term is 0/0 and every
         // score is a finite number >= 0: filtered[0] is never NaN, "some node fits" <=> best_n >= 0,
         // and neither filtered[0] nor its re-scored value is needed (kube_scheduler.rs:140-148).
-        scan_lanes<true, false, LOOP ? K10S_LOOP_SCAN_PIPE : K10S_SCAN_PIPE>(s_cpu, s_ram, present, n_nodes, rc, rr,
-                                                                            weight, first, best_s, best_n);
+        if (LOOP && K10S_SCAN_SCREEN)
+            scan_lanes_screen<K10S_LOOP_SCAN_PIPE>(s_cpu, s_ram, present, n_nodes, rc, rr, best_s, best_n);
+        else
+            scan_lanes<true, false, LOOP ? K10S_LOOP_SCAN_PIPE : K10S_SCAN_PIPE>(s_cpu, s_ram, present, n_nodes, rc,
+                                                                                rr, weight, first, best_s, best_n);
         best_key = best_n >= 0 ? score_key(best_s) : 0;
         wave_argmax(best_key, best_n);
         if (best_n < 0) return K10S_SCHED_NO_SUFFICIENT_RESOURCES;

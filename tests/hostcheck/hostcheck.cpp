@@ -191,3 +191,11 @@ extern "C" int hc_debug_queues(void* p, uint32_t r, double* aq, uint32_t* aq_pod
 
 // The host score (bit-identical to the device's), for tests/test_scan_adversarial.py.
 extern "C" double hc_la_score(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr) { return la_score(ac, ar, rc, rr); }
+// The event loop's screened scan test (k10s_engine.h scan_screen, operands formed as
+// scan_lanes_screen forms them), for tests/test_scan_screen.py.
+extern "C" int hc_scan_screen(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr, float thr) {
+    const float fa = (float)rc;
+    const float fr = __builtin_fmaf((float)(uint32_t)(rr >> 32), 4294967296.0f, (float)(uint32_t)rr);
+    return scan_screen(ac, ar, fa, fr, thr + K10S_SCREEN_EPS) ? 1 : 0;
+}
+extern "C" float hc_screen_u(double s) { return screen_u(s); }
