@@ -2574,6 +2574,78 @@ K10S_HD bool replica_stalled(Ctx& c) {
 #ifndef K10S_CONTINUE
 #define K10S_CONTINUE 1   // run continuation (continue_source); 0 = a full selection per event
 #endif
+// Fair share of a SIMD's issue slots between its resident replicas.  The instruction arbiter prefers
+// the oldest wave among equal priorities, so with 8 identical replicas per SIMD the oldest finishes
+// in ~63 % of the time of the youngest (tools/wall_spread.py) and the SIMD runs the rest of the launch
+// with fewer and fewer waves.  Every 2^K10S_FAIR_SHIFT events a wave draws a new priority 0..3 from
+// a hash of (replica, epoch), so every wave spends the same share of the launch at each priority and
+// the resident round drains together.  Scheduling hints only: no effect on any result.
+#ifndef K10S_FAIR
+#define K10S_FAIR 0
+#endif
+#ifndef K10S_FAIR_SHIFT
+#define K10S_FAIR_SHIFT 10
+#endif
+#ifndef K10S_FAIR_BAND
+#define K10S_FAIR_BAND 4096
+#endif
+#define K10S_FAIR_KEYS 4096   // XCC x SE x SH x CU x SIMD
+#if defined(__HIP__) && (K10S_FAIR == 4 || K10S_FAIR == 5)
+__device__ uint32_t k10s_fair_board[2 * K10S_FAIR_KEYS];   // zeroed before every run launch
+#endif
+K10S_HD void fair_priority(uint64_t done) {
+#if K10S_DEVICE && K10S_FAIR
+    if ((done & ((1ull << K10S_FAIR_SHIFT) - 1)) != 0) return;
+#if K10S_FAIR == 2
+    // rotation by the wave's slot on its SIMD (HW_ID.WAVE_ID): over every 8 epochs each slot holds
+    // each priority for exactly 2 epochs, and the pairs that tie alternate
+    const uint32_t slot = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 4);
+    const uint32_t pr = ((slot + (uint32_t)(done >> K10S_FAIR_SHIFT)) & 7u) >> 1;
+#elif K10S_FAIR == 3
+    // rotation with a single wave on top: ranks 0..7 -> priorities 0,0,0,1,1,2,2,3
+    const uint32_t slot = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 4);
+    const uint32_t rk = (slot + (uint32_t)(done >> K10S_FAIR_SHIFT)) & 7u;
+    const uint32_t pr = (0xE940u >> (2u * rk)) & 3u;
+#elif K10S_FAIR == 4 || K10S_FAIR == 5
+    // least progress first: the waves of one SIMD (HW_ID + XCC_ID key) add their event counts to a
+    // per-SIMD board; a wave behind its SIMD's mean by more than one epoch runs at priority 3, one
+    // ahead by more than one epoch at 0 (vector atomics by lanes 0/1 on distinct words)
+    const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) & 7u;
+    const uint32_t key = (((xcc * 4u + ((hw >> 13) & 3u)) * 2u + ((hw >> 12) & 1u)) * 16u + ((hw >> 8) & 15u)) * 4u +
+                         ((hw >> 4) & 3u);
+    const int lane = lane_id();
+    const uint32_t inc = 1u << K10S_FAIR_SHIFT;
+    uint32_t got = 0;
+    if (lane < 2) {
+        uint32_t* w = lane == 0 ? &k10s_fair_board[key] : &k10s_fair_board[K10S_FAIR_KEYS + key];
+        got = atomicAdd(w, lane == 0 ? inc : (done == 0 ? 1u : 0u));
+    }
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)got, 0) + inc;
+    uint32_t nw = (uint32_t)__builtin_amdgcn_readlane((int)got, 1) + (done == 0 ? 1u : 0u);
+    nw = nw ? nw : 1u;
+    const int64_t lag = (int64_t)(tot / nw) - (int64_t)(done + inc);
+#if K10S_FAIR == 4
+    const uint32_t pr = lag > (int64_t)inc ? 3u : lag >= 0 ? 2u : lag >= -(int64_t)inc ? 1u : 0u;
+#else
+    // 5: random priority (as 1) while within K10S_FAIR_BAND events of the SIMD's mean; outside it the
+    // lagging wave is raised above every random draw and the leading one lowered below them
+    const uint32_t rnd = 1u + (uint32_t)(splitmix64(((uint64_t)blockIdx.x << 32) ^ (done >> K10S_FAIR_SHIFT)) >> 63);
+    const uint32_t pr = lag > (int64_t)K10S_FAIR_BAND ? 3u : lag < -(int64_t)K10S_FAIR_BAND ? 0u : rnd;
+#endif
+#else
+    const uint32_t pr = (uint32_t)(splitmix64(((uint64_t)blockIdx.x << 32) ^ (done >> K10S_FAIR_SHIFT)) >> 62);
+#endif
+    switch (pr) {
+    case 0: __builtin_amdgcn_s_setprio(0); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    default: __builtin_amdgcn_s_setprio(3); break;
+    }
+#else
+    (void)done;
+#endif
+}
 // Returns 1 if the replica still has work (event budget exhausted), else 0.  The working header
 // c.H() is LDS on the device (staged by the kernel) and the replica's header in place on the host.
 K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, uint64_t budget) {
@@ -2665,6 +2737,7 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
         h->clock = e.time;
         h->cur_kind = e.kind;
         h->cur_seq = e.seq;
+        fair_priority(done);
         done++;  // counters[K10S_C_EVENTS] takes the launch's count once, at exit (no per-event LDS RMW)
         if (cap_log) {
             uint32_t k = h->log_n;

@@ -61,9 +61,22 @@ __global__ K10S_RUN_BOUNDS void k10s_run_kernel(uint32_t n_replicas, int mode, d
                                                 uint64_t budget, uint32_t* active) {
     uint32_t r = blockIdx.x;
     if (r >= n_replicas) return;
+#if K10S_WALL
+    // tooling builds only: launch wall-time placement of each replica (100 MHz realtime counter,
+    // hardware ids) in the profile slots, for the finish-time spread of one resident round
+    const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
+#endif
     hdr_copy((uint32_t*)&k10s_hdr, hdr_global(r));
     Ctx c;
     int more = run_replica(c, mode, until_time, max_time, budget);
+#if K10S_WALL
+    if (threadIdx.x == 0) {
+        k10s_hdr.prof[0] = w0;
+        k10s_hdr.prof[1] = __builtin_amdgcn_s_memrealtime();
+        k10s_hdr.prof[2] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+        k10s_hdr.prof[3] = (uint32_t)__builtin_amdgcn_s_getreg((15 << 11) | 20);   // XCC_ID
+    }
+#endif
     __syncthreads();
     hdr_copy(hdr_global(r), (const uint32_t*)&k10s_hdr);
     if (more && threadIdx.x == 0) atomicAdd(active, 1u);
@@ -137,6 +150,12 @@ hipError_t k10s_launch_run(const DevConst* h_dc, uint32_t n_replicas, int mode, 
     std::lock_guard<std::mutex> g(g_launch_mu);
     hipError_t e = upload(h_dc, s);
     if (e != hipSuccess) return e;
+#if K10S_FAIR == 4 || K10S_FAIR == 5
+    void* board = nullptr;
+    e = hipGetSymbolAddress(&board, HIP_SYMBOL(k10s_fair_board));
+    if (e == hipSuccess) e = hipMemsetAsync(board, 0, sizeof(k10s_fair_board), s);
+    if (e != hipSuccess) return e;
+#endif
     hipLaunchKernelGGL(k10s_run_kernel, dim3(n_replicas), dim3(64), 0, s, n_replicas, mode, until_time, max_time,
                        budget, d_active);
     return hipGetLastError();

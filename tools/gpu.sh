@@ -8,6 +8,7 @@
 #   bench[:ARGS]   python bench.py ARGS (default: --steps 5 --warmup 2); ARGS use ',' for spaces
 #   stats[:ARGS]   rocprofv3 --kernel-trace --stats over bench.py ARGS
 #   pmc:NAME:C1,C2,...[:ARGS]   one rocprofv3 --pmc pass (kernel trace only) over bench.py ARGS
+#   py:SCRIPT,ARGS python SCRIPT ARGS (output to py<n>.json / py<n>.err)
 #   env:K=V        export K=V for the following steps (e.g. env:K10S_LIB=build/libk10s_prof.so)
 
 # Outputs go to gpurun_out/<tag>/.
@@ -56,6 +57,11 @@ for step in "$@"; do
         --pmc $(echo "$ctrs" | tr ',' ' ') -- python3 "$R/bench.py" $(args_of "$bargs") \
         > "$O/pmc_$name.json" 2> "$O/pmc_$name.err") || { echo "PMC $name FAILED"; tail -20 "$O/pmc_$name.err"; exit 1; }
       echo "PMC $name ok" ;;
+    py)
+      n=$(ls "$O"/py*.json 2>/dev/null | wc -l)
+      timeout -k 10 600 python -u $(args_of "$rest") > "$O/py$n.json" 2> "$O/py$n.err" \
+        || { echo "PY FAILED"; tail -20 "$O/py$n.err"; exit 1; }
+      tail -c 1500 "$O/py$n.json"; echo ;;
     env)
       export "$rest"; echo "exported $rest" ;;
     *)
