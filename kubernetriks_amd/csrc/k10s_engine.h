@@ -2574,20 +2574,28 @@ K10S_HD bool replica_stalled(Ctx& c) {
 #ifndef K10S_CONTINUE
 #define K10S_CONTINUE 1   // run continuation (continue_source); 0 = a full selection per event
 #endif
-// Fair share of a SIMD's issue slots between its resident replicas.  The instruction arbiter prefers
-// the oldest wave among equal priorities, so with 8 identical replicas per SIMD the oldest finishes
-// in ~63 % of the time of the youngest (tools/wall_spread.py) and the SIMD runs the rest of the launch
-// with fewer and fewer waves.  Every 2^K10S_FAIR_SHIFT events a wave draws a new priority 0..3 from
-// a hash of (replica, epoch), so every wave spends the same share of the launch at each priority and
-// the resident round drains together.  Scheduling hints only: no effect on any result.
+// Wave priorities (s_setprio) so that the replicas of one SIMD drain together.  The instruction
+// arbiter prefers the oldest wave among equal priorities, so with 8 identical replicas per SIMD the
+// oldest finished at 63 % of the launch and the youngest at 100 % (tools/wall_spread.py,
+// profiles/r02_v7_wall_spread_*.json): the SIMD ran the last third with fewer and fewer waves.
+// Every 2^K10S_FAIR_SHIFT events a wave picks a priority:
+//   1  random 0..3 from a hash of (replica, epoch)                       C3 2,089 -> 1,836 ms
+//   2  rotation by the wave's SIMD slot (2 waves per level)              1,871 ms
+//   3  rotation, one wave on top                                         1,913 ms
+//   4  least progress first (per-SIMD event board, 4 levels)             1,873 ms (all end together)
+//   5  (default) random 1..2 while within K10S_FAIR_BAND events of the SIMD's mean, 3 when behind
+//      by more, 0 when ahead by more                                     1,734 ms
+// Strict fairness (4) drains the SIMD together but lowers its throughput while all 8 waves run;
+// letting random waves lead inside a band keeps that throughput and still bounds the drift
+// (profiles/r02_v7_fair_ab.json).  Scheduling hints only: no effect on any result.
 #ifndef K10S_FAIR
-#define K10S_FAIR 0
+#define K10S_FAIR 5
 #endif
 #ifndef K10S_FAIR_SHIFT
-#define K10S_FAIR_SHIFT 10
+#define K10S_FAIR_SHIFT 6
 #endif
 #ifndef K10S_FAIR_BAND
-#define K10S_FAIR_BAND 4096
+#define K10S_FAIR_BAND 512
 #endif
 #define K10S_FAIR_KEYS 4096   // XCC x SE x SH x CU x SIMD
 #if defined(__HIP__) && (K10S_FAIR == 4 || K10S_FAIR == 5)
