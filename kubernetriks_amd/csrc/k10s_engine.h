@@ -851,6 +851,63 @@ K10S_D void scan_node_screen(uint32_t n, bool present, uint32_t ac, uint64_t ar,
         }
     }
 }
+// K10S_SCREEN_PACKED (default 1): scan_lanes_screen evaluates the screen of a lane's 4 nodes first
+// (screen_grp), then scores the remaining ones in order (score_node_exact); the same decisions and
+// the same f32 operations as scan_node_screen, so the same nodes are scored and the result is
+// identical, with fewer instructions: the conversions are single v_cvt_f32_u32 each, the products
+// run 2 nodes per v_pk_mul_f32 / v_pk_fma_f32, and no exec-mask branch separates the 4 nodes.
+#ifndef K10S_SCREEN_PACKED
+#define K10S_SCREEN_PACKED 1
+#endif
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+K10S_D float cvt_f32_u32(uint32_t v) {   // (float)v, correctly rounded, as the one instruction
+    float f;
+    asm("v_cvt_f32_u32 %0, %1" : "=v"(f) : "v"(v));
+    return f;
+}
+// Bit k set: node k of the group is present, fits, and is not ruled out by the screen (scan_screen).
+K10S_D uint32_t screen_grp(const ScanGrp& g, uint32_t bits, uint32_t rc, uint64_t rr, float fa, float fr, float T) {
+    const uint32_t fit = bits & ((uint32_t)(rc <= g.cv.x && rr <= g.r01.x) | ((uint32_t)(rc <= g.cv.y && rr <= g.r01.y) << 1) |
+                                 ((uint32_t)(rc <= g.cv.z && rr <= g.r23.x) << 2) | ((uint32_t)(rc <= g.cv.w && rr <= g.r23.y) << 3));
+    const f32x2 A01 = {cvt_f32_u32(g.cv.x), cvt_f32_u32(g.cv.y)};
+    const f32x2 A23 = {cvt_f32_u32(g.cv.z), cvt_f32_u32(g.cv.w)};
+    const f32x2 H01 = {cvt_f32_u32((uint32_t)(g.r01.x >> 32)), cvt_f32_u32((uint32_t)(g.r01.y >> 32))};
+    const f32x2 H23 = {cvt_f32_u32((uint32_t)(g.r23.x >> 32)), cvt_f32_u32((uint32_t)(g.r23.y >> 32))};
+    const f32x2 L01 = {cvt_f32_u32((uint32_t)g.r01.x), cvt_f32_u32((uint32_t)g.r01.y)};
+    const f32x2 L23 = {cvt_f32_u32((uint32_t)g.r23.x), cvt_f32_u32((uint32_t)g.r23.y)};
+    const f32x2 two32 = {4294967296.0f, 4294967296.0f};
+    const f32x2 R01 = __builtin_elementwise_fma(H01, two32, L01), R23 = __builtin_elementwise_fma(H23, two32, L23);
+    const f32x2 va = {fa, fa}, vr = {fr, fr}, vT = {T, T};
+    const f32x2 l01 = __builtin_elementwise_fma(va, R01, vr * A01), l23 = __builtin_elementwise_fma(va, R23, vr * A23);
+    const f32x2 r01 = (A01 * R01) * vT, r23 = (A23 * R23) * vT;
+    const uint32_t out = (uint32_t)(l01.x > r01.x) | ((uint32_t)(l01.y > r01.y) << 1) | ((uint32_t)(l23.x > r23.x) << 2) |
+                         ((uint32_t)(l23.y > r23.y) << 3);
+    return fit & ~out;
+}
+// A fitting node the screen did not rule out: the lane best's allocatables take the index (same
+// score), anything else is scored exactly (scan_node_screen's exact branch).
+K10S_D void score_node_exact(uint32_t n, uint32_t ac, uint64_t ar, uint64_t rr, double frc, double frr, double& best_s,
+                             int32_t& best_n, uint32_t& la, uint64_t& lr, float& lu) {
+    if (ac == la && ar == lr) {
+        best_n = (int32_t)n;
+        return;
+    }
+    const double fac = (double)ac;
+    const double cs = div_rn((fac - frc) * 100.0, fac);
+    const uint2 w = __builtin_bit_cast(uint2, ar);
+    const double far = u64_f64(ar);
+    double dr = far - frr;
+    if (__builtin_expect(w.y >= (1u << 21), 0)) dr = u64_f64(ar - rr);
+    const double s = (cs + div_rn(dr * 100.0, far)) * 0.5;
+    if (s >= best_s) {
+        best_s = s;
+        best_n = (int32_t)n;
+        la = ac;
+        lr = ar;
+    }
+    const float u = screen_u(s);
+    lu = u < lu ? u : lu;
+}
 template <int S>
 K10S_D float minf_step(float v) {
     uint32_t a, b;
@@ -884,6 +941,23 @@ K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, cons
         g[PIPE] = scan_load(s_cpu, s_ram, present, n_nodes, base + 256u * PIPE + l4);
         const uint32_t n0 = base + l4;
         const uint32_t bits = grp_bits(g[0], n0, n_nodes);
+#if K10S_SCREEN_PACKED
+        // the screen of the lane's 4 nodes first, branch-free and 2 nodes per packed f32 op; only
+        // the nodes it cannot rule out take the sequential exact path below
+        const uint32_t need = screen_grp(g[0], bits, rc, rr, fa, fr, T);
+        if (need) {
+            if (need & 1u) score_node_exact(n0, g[0].cv.x, g[0].r01.x, rr, frc, frr, best_s, best_n, la, lr, lu);
+            if (need & 2u) score_node_exact(n0 + 1, g[0].cv.y, g[0].r01.y, rr, frc, frr, best_s, best_n, la, lr, lu);
+            if (need & 4u) score_node_exact(n0 + 2, g[0].cv.z, g[0].r23.x, rr, frc, frr, best_s, best_n, la, lr, lu);
+            if (need & 8u) score_node_exact(n0 + 3, g[0].cv.w, g[0].r23.y, rr, frc, frr, best_s, best_n, la, lr, lu);
+        }
+        // thr only moves when some lane scored a node exactly this step (lu changed): skip the
+        // 6-step wave reduction otherwise (T is then exactly what the reduction would give)
+        if (__ballot(need != 0)) {
+            const float thr = __builtin_bit_cast(float, uniform_u32(__builtin_bit_cast(uint32_t, wave_min_f32(lu))));
+            T = thr + K10S_SCREEN_EPS;
+        }
+#else
         if (bits) {
             scan_node_screen(n0, bits & 1u, g[0].cv.x, g[0].r01.x, rc, rr, frc, frr, fa, fr, T, best_s, best_n, la, lr, lu);
             scan_node_screen(n0 + 1, bits & 2u, g[0].cv.y, g[0].r01.y, rc, rr, frc, frr, fa, fr, T, best_s, best_n, la, lr, lu);
@@ -892,6 +966,7 @@ K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, cons
         }
         const float thr = __builtin_bit_cast(float, uniform_u32(__builtin_bit_cast(uint32_t, wave_min_f32(lu))));
         T = thr + K10S_SCREEN_EPS;
+#endif
 #pragma unroll
         for (int i = 0; i < PIPE; i++) g[i] = g[i + 1];
     }
