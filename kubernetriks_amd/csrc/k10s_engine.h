@@ -682,6 +682,17 @@ K10S_D ScanGrp scan_load(const uint32_t* s_cpu, const uint64_t* s_ram, const uin
     g.r23 = *reinterpret_cast<const ulonglong2*>(s_ram + a + 2);
     return g;
 }
+// The event loop's screened scan (rc > 0): absent nodes hold (0, 0) in the cache (S_REMOVE_NODE,
+// init_replica), so Fit alone excludes them and the presence word is not read.
+K10S_D ScanGrp scan_load_np(const uint32_t* s_cpu, const uint64_t* s_ram, uint32_t n_nodes, uint32_t n0) {
+    const uint32_t a = n0 < n_nodes ? n0 : 0u;
+    ScanGrp g;
+    g.pw = ~0ull;
+    g.cv = *reinterpret_cast<const uint4*>(s_cpu + a);
+    g.r01 = *reinterpret_cast<const ulonglong2*>(s_ram + a);
+    g.r23 = *reinterpret_cast<const ulonglong2*>(s_ram + a + 2);
+    return g;
+}
 K10S_D uint32_t grp_bits(const ScanGrp& g, uint32_t n0, uint32_t n_nodes) {
     if (n0 >= n_nodes) return 0;
     const uint32_t valid = n_nodes - n0;
@@ -920,6 +931,14 @@ K10S_D float wave_min_f32(float v) {
     v = minf_step<3>(v); v = minf_step<4>(v); v = minf_step<5>(v);
     return v;
 }
+#ifndef K10S_SCREEN_NO_PRESENCE
+#define K10S_SCREEN_NO_PRESENCE 1
+#endif
+#if K10S_SCREEN_NO_PRESENCE
+#define SCREEN_LOAD(c, r, p, n, n0) scan_load_np(c, r, n, n0)
+#else
+#define SCREEN_LOAD(c, r, p, n, n0) scan_load(c, r, p, n, n0)
+#endif
 template <int PIPE>
 K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
                               uint32_t rc, uint64_t rr, double& best_s, int32_t& best_n) {
@@ -936,9 +955,9 @@ K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, cons
     float T = __builtin_inff();  // thr + eps: +inf screens nothing out (the first step)
     ScanGrp g[PIPE + 1];
 #pragma unroll
-    for (int i = 0; i < PIPE; i++) g[i] = scan_load(s_cpu, s_ram, present, n_nodes, 256u * i + l4);
+    for (int i = 0; i < PIPE; i++) g[i] = SCREEN_LOAD(s_cpu, s_ram, present, n_nodes, 256u * i + l4);
     for (uint32_t base = 0; base < n_nodes; base += 256) {
-        g[PIPE] = scan_load(s_cpu, s_ram, present, n_nodes, base + 256u * PIPE + l4);
+        g[PIPE] = SCREEN_LOAD(s_cpu, s_ram, present, n_nodes, base + 256u * PIPE + l4);
         const uint32_t n0 = base + l4;
         const uint32_t bits = grp_bits(g[0], n0, n_nodes);
 #if K10S_SCREEN_PACKED
@@ -1440,6 +1459,10 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
             return;
         }
         bit_clear(c.V().s_present(), n);
+        // invariant: an absent node's cache entry is (0, 0), as after initialize, so no request with
+        // cpu > 0 fits it and the event loop's screened scan needs no presence words
+        c.V().s_cpu()[n] = 0;
+        c.V().s_ram()[n] = 0;
         h->s_node_count -= 1;
         node_bound_changed(c, n);
         if (c.V().node(n).flags & NF_S_ASSIGN) {  // reschedule_unfinished_pods (352-364), name order
