@@ -2504,6 +2504,9 @@ K10S_D uint32_t row16_umin(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 #endif
+#ifndef K10S_SELECT_SPLIT
+#define K10S_SELECT_SPLIT 0   // 1: 32-bit row minima for the source selection (0.3-0.6 % slower, r02_v11)
+#endif
 K10S_HD int next_source(Ctx& c, uint32_t ntr, int64_t& k2, uint32_t& s2) {
     const RepHdr& H = c.H();
     const int64_t KMAX = 0x7FFFFFFFFFFFFFFFll;
@@ -2536,6 +2539,32 @@ K10S_HD int next_source(Ctx& c, uint32_t ntr, int64_t& k2, uint32_t& s2) {
     }
     int64_t k = valid ? total_key(t) : KMAX;
     sq = valid ? sq : 0xFFFFFFFFu;
+#if K10S_SELECT_SPLIT
+    // The (key, id) minimum as three 32-bit row minima (fused v_min_u32 DPP steps): the biased key's
+    // high word, its low word among the lanes at that high word, the id among the lanes at that key;
+    // then the same three with the winning lane masked for the runner-up.  Biasing the int64 key by
+    // 2^63 makes its unsigned order the signed order, so the result is the 64-bit one bit for bit.
+    const uint64_t uk = (uint64_t)k ^ 0x8000000000000000ull;
+    const uint32_t kh = (uint32_t)(uk >> 32), kl = (uint32_t)uk;
+    const uint32_t mh = row16_umin(kh);
+    const uint32_t ml = row16_umin(kh == mh ? kl : 0xFFFFFFFFu);
+    if (mh == 0xFFFFFFFFu && ml == 0xFFFFFFFFu) {   // every key is KMAX: nothing pending
+        k2 = KMAX;
+        s2 = 0xFFFFFFFFu;
+        return -1;
+    }
+    const bool at_min = kh == mh && kl == ml;
+    const uint32_t smin = row16_umin(at_min ? sq : 0xFFFFFFFFu);
+    const uint64_t win = __ballot(lane_id() < 16 && at_min && sq == smin) & 0xFFFFull;
+    const int src = (int)__builtin_ctzll(win);
+    const bool other = lane != src;
+    const uint32_t oh = other ? kh : 0xFFFFFFFFu, ol = other ? kl : 0xFFFFFFFFu;
+    const uint32_t mh2 = row16_umin(oh);
+    const uint32_t ml2 = row16_umin(oh == mh2 ? ol : 0xFFFFFFFFu);
+    k2 = (int64_t)((((uint64_t)mh2 << 32) | ml2) ^ 0x8000000000000000ull);
+    s2 = k2 == KMAX ? 0xFFFFFFFFu : row16_umin(oh == mh2 && ol == ml2 ? sq : 0xFFFFFFFFu);
+    return src;
+#else
     const int64_t kmin = row16_kmin(k);
     if (kmin == KMAX) {
         k2 = KMAX;
@@ -2551,6 +2580,7 @@ K10S_HD int next_source(Ctx& c, uint32_t ntr, int64_t& k2, uint32_t& s2) {
     k2 = row16_kmin(ko);
     s2 = k2 == KMAX ? 0xFFFFFFFFu : row16_umin(ko == k2 ? sq : 0xFFFFFFFFu);
     return src;
+#endif
 #else
     int64_t kk[K10S_NFQ + 2];
     uint32_t ss[K10S_NFQ + 2];
