@@ -118,9 +118,21 @@ K10S_HD double fmax_rs(double a, double b) {
 }
 
 // ---- lanes -----------------------------------------------------------------------------------
+// K10S_LANE_OPAQUE: the lane index is re-read at each use (an empty asm the compiler cannot hoist),
+// so lane-dependent masks are recomputed where needed instead of being held in SGPR pairs across
+// the event loop (where they are spilled around every out-of-line handler call).  Tuning knob.
+#ifndef K10S_LANE_OPAQUE
+#define K10S_LANE_OPAQUE 1   // C3 +1.7 % (profiles/r02_v13_sgpr_live_ab.json)
+#endif
 K10S_HD int lane_id() {
 #if K10S_DEVICE
+#if K10S_LANE_OPAQUE
+    uint32_t t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return (int)(t & 63);
+#else
     return (int)(threadIdx.x & 63);
+#endif
 #else
     return 0;
 #endif

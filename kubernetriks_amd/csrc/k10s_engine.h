@@ -2316,8 +2316,37 @@ K10S_COLD void on_metrics(Ctx& c, HeapEv e) {
     emit0(c, K10S_EV_M_POD_METRICS_TICK, 60.0);
 }
 
+// K10S_FAST_DISPATCH: the api server's pure forwarding cases for the per-pod message chain (the
+// same statements as in on_api_server) run inline in the event loop instead of through the
+// out-of-line handler call and its register save/restore.  Tuning knob, semantics-neutral.
+#ifndef K10S_FAST_DISPATCH
+#define K10S_FAST_DISPATCH 0
+#endif
 K10S_HD void dispatch(Ctx& c, const HeapEv& e) {
     uint32_t k = e.kind;
+#if K10S_FAST_DISPATCH
+    switch (k) {
+    case K10S_EV_AS_CREATE_POD_REQ:   // api_server.rs:151-155
+        c.H().g_cur_pods += 1;
+        emit(c, K10S_EV_PS_CREATE_POD_REQ, c.P().as_to_ps_network_delay, -1, e.a, 0, 0.0, FQ_AS_TO_PS);
+        return;
+    case K10S_EV_AS_POD_STARTED:
+        emit(c, K10S_EV_PS_POD_STARTED, c.P().as_to_ps_network_delay, -1, e.a, 0, e.x, FQ_AS_TO_PS);
+        return;
+#if K10S_FAST_DISPATCH >= 2
+    case K10S_EV_AS_POD_FINISHED: {   // api_server.rs:262-265
+        RepHdr& H = c.H();
+        H.counters[K10S_C_TERMINATED_PODS] += 1;
+        H.counters[K10S_C_PODS_SUCCEEDED] += 1;
+        H.g_cur_pods -= 1;
+        emit(c, K10S_EV_PS_POD_FINISHED, c.P().as_to_ps_network_delay, -1, e.a, e.b, e.x, FQ_AS_TO_PS);
+        return;
+    }
+#endif
+    default:
+        break;
+    }
+#endif
     if (k <= K10S_EV_M_GAUGE_TICK) on_metrics(c, e);
     else if (k <= K10S_EV_AS_CREATE_GROUP_REQ) on_api_server(c, e);
     else if (k <= K10S_EV_PS_POD_REMOVED) on_ps(c, e);
@@ -2794,12 +2823,18 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
     const uint64_t total_pods = sc->total_pods_in_trace;
     const uint32_t ntr = sc->n_trace;
     const uint32_t cap_log = c.Ly().cap_log;
+    // one time limit per mode (until_time / max_time)
+    const uint32_t until_mode0 = mode == K10S_RUN_UNTIL_TIME ? 1u : 0u;
+    const double limit = until_mode0 ? until_time : max_time;
+    auto until_mode = [&]() -> bool {
+        return until_mode0 != 0;
+    };
     uint64_t done = 0;
     int more = 0;
     uint32_t status = K10S_REPLICA_RUNNING;
     const uint64_t t_loop = prof_now();
     while (!h->error_code) {
-        if (mode == K10S_RUN_UNTIL_ALL_FINISHED && h->counters[K10S_C_TERMINATED_PODS] >= total_pods &&
+        if (!until_mode() && h->counters[K10S_C_TERMINATED_PODS] >= total_pods &&
             is_multiple_of_1000(h->clock)) {
             status = K10S_REPLICA_FINISHED;
             break;
@@ -2851,16 +2886,13 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
         }
         K10S_PROF_ADD(c, PROF_SELECT, t_sel);
         if (!have) {
-            if (mode == K10S_RUN_UNTIL_TIME) h->clock = until_time;
-            status = mode == K10S_RUN_UNTIL_TIME ? K10S_REPLICA_RUNNING : K10S_REPLICA_FINISHED;
+            if (until_mode()) h->clock = limit;
+            status = until_mode() ? K10S_REPLICA_RUNNING : K10S_REPLICA_FINISHED;
             break;
         }
-        if (mode == K10S_RUN_UNTIL_TIME && e.time > until_time) {
-            h->clock = until_time;
-            break;
-        }
-        if (mode == K10S_RUN_UNTIL_ALL_FINISHED && e.time > max_time) {
-            status = K10S_REPLICA_TIME_LIMIT;
+        if (e.time > limit) {
+            if (until_mode()) h->clock = limit;                // step_until_time: stop at the time
+            else status = K10S_REPLICA_TIME_LIMIT;             // run until finished: max_time reached
             break;
         }
         if (budget && done >= budget) {
@@ -2938,7 +2970,7 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
         h->prof[K10S_PROF_KIND0 + e.kind] += prof_now() - t_dis;
         h->prof[K10S_PROF_KIND0 + K10S_EV_NUM_KINDS + e.kind] += 1;
 #endif
-        if (e.kind == K10S_EV_M_GAUGE_TICK && c.Ly().stall && mode == K10S_RUN_UNTIL_ALL_FINISHED &&
+        if (e.kind == K10S_EV_M_GAUGE_TICK && c.Ly().stall && !until_mode() &&
             replica_stalled(c)) {
             status = K10S_REPLICA_STALLED;
             break;
