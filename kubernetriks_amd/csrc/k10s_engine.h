@@ -2816,13 +2816,14 @@ K10S_HD void fair_priority(uint64_t done) {
 K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, uint64_t budget) {
     RepHdr* h = &c.H();
     if (h->status != K10S_REPLICA_RUNNING) return 0;
-    const Scenario* sc = &c.S();
-    h->cur_kind = 0xFFFF;
+        h->cur_kind = 0xFFFF;
     h->cur_seq = 0;
     h->cont_src = 0xFFFFFFFFu;  // the first event of a launch takes a full selection
-    const uint64_t total_pods = sc->total_pods_in_trace;
-    const uint32_t ntr = sc->n_trace;
-    const uint32_t cap_log = c.Ly().cap_log;
+    // launch constants are re-read at each use (scalar loads through the opaque constant pointer)
+    // rather than held in SGPRs across the loop, where they are spilled around the handler calls
+#define total_pods (c.S().total_pods_in_trace)
+#define ntr (c.S().n_trace)
+#define cap_log (c.Ly().cap_log)
     // one time limit per mode (until_time / max_time)
     const uint32_t until_mode0 = mode == K10S_RUN_UNTIL_TIME ? 1u : 0u;
     const double limit = until_mode0 ? until_time : max_time;
@@ -2859,16 +2860,16 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
             if (src < 0) break;
             if (src == SRC_TRACE) {
                 const uint32_t cur = h->trace_cursor;
-                const uint32_t tk = sc->trace[cur].kind, ta = sc->trace[cur].arg;
-                e.time = sc->trace[cur].time;
-                e.seq = sc->trace[cur].seq;
+                const uint32_t tk = c.S().trace[cur].kind, ta = c.S().trace[cur].arg;
+                e.time = c.S().trace[cur].time;
+                e.seq = c.S().trace[cur].seq;
                 e.kind = (uint16_t)tk;
                 e.slot = -1;
                 e.x = 0.0;
                 e.a = ta;
                 e.b = 0;
                 if (tk == K10S_EV_AS_CREATE_NODE_REQ) {
-                    e.a = sc->def_node[ta];
+                    e.a = c.S().def_node[ta];
                     e.b = ta;
                 }
             } else if (src == SRC_HEAP) {
@@ -2981,6 +2982,9 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
     if (h->error_code) status = K10S_REPLICA_ERROR;
     h->status = status;
     return more;
+#undef total_pods
+#undef ntr
+#undef cap_log
 }
 
 }  // namespace k10s

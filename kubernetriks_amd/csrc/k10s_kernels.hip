@@ -44,8 +44,15 @@ __device__ __forceinline__ void hdr_copy(uint32_t* dst, const uint32_t* src) {
     for (uint32_t i = threadIdx.x; i < W; i += 64) dst[i] = src[i];
     __syncthreads();
 }
+// Through the opaque constant pointer (K10S_DC): the copy-out after the event loop recomputes the
+// address instead of keeping the copy-in's 4 SGPRs live (and spilled around every handler call)
+// across the whole loop.
 __device__ __forceinline__ uint32_t* hdr_global(uint32_t r) {
+#if K10S_DEVICE
+    return (uint32_t*)(K10S_DC.base + (uint64_t)r * K10S_DC.L.stride + K10S_DC.L.hdr);
+#else
     return (uint32_t*)(k10s_dc.base + (uint64_t)r * k10s_dc.L.stride + k10s_dc.L.hdr);
+#endif
 }
 
 __global__ __launch_bounds__(64) void k10s_init_kernel(uint32_t n_replicas) {
