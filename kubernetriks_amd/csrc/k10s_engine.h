@@ -29,6 +29,19 @@ namespace k10s {
 #if defined(__HIP__)
 __constant__ DevConst k10s_dc;
 __shared__ RepHdr k10s_hdr;
+// The launch's run arguments, staged in LDS by the run kernel (K10S_RUN_ARGS_LDS): read where the
+// loop tests them instead of held in SGPRs across the loop, where they are spilled around every
+// out-of-line handler call.
+struct RunArgs {
+    double limit;       // until_time (K10S_RUN_UNTIL_TIME) or max_time
+    uint64_t budget;    // events per launch, 0 = unbounded
+    uint32_t until_mode;
+    uint32_t pad;
+};
+__shared__ RunArgs k10s_run;
+#endif
+#ifndef K10S_RUN_ARGS_LDS
+#define K10S_RUN_ARGS_LDS 0   // 1: 8.6 % slower at C3 (LDS reads on every event's path), r02_v16
 #endif
 // Every read of the launch constants goes through an opaque copy of the block's address (an empty
 // asm the compiler cannot see through): the scalar loads are then issued where a value is used
@@ -2825,11 +2838,18 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
 #define ntr (c.S().n_trace)
 #define cap_log (c.Ly().cap_log)
     // one time limit per mode (until_time / max_time)
+#if K10S_DEVICE && K10S_RUN_ARGS_LDS
+    (void)mode; (void)until_time; (void)max_time; (void)budget;
+#define limit (k10s_run.limit)
+#define budget (k10s_run.budget)
+    auto until_mode = [&]() -> bool { return uniform_u32(k10s_run.until_mode) != 0; };
+#else
     const uint32_t until_mode0 = mode == K10S_RUN_UNTIL_TIME ? 1u : 0u;
     const double limit = until_mode0 ? until_time : max_time;
     auto until_mode = [&]() -> bool {
         return until_mode0 != 0;
     };
+#endif
     uint64_t done = 0;
     int more = 0;
     uint32_t status = K10S_REPLICA_RUNNING;
@@ -2985,6 +3005,10 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
 #undef total_pods
 #undef ntr
 #undef cap_log
+#if K10S_DEVICE && K10S_RUN_ARGS_LDS
+#undef limit
+#undef budget
+#endif
 }
 
 }  // namespace k10s

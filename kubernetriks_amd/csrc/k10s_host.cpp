@@ -317,6 +317,7 @@ k10s_engine* k10s_engine_create_bulk(const char* scenario_text, const void* pods
     e->h_dc->L = e->L;
     e->h_dc->params = e->d_params;
     e->h_dc->base = e->d_state;
+    e->h_dc->active = e->d_active;
     if (engine_init(e) != K10S_OK) {
         std::string m = g_err;
         engine_free(e);

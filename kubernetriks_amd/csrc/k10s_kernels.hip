@@ -73,6 +73,13 @@ __global__ K10S_RUN_BOUNDS void k10s_run_kernel(uint32_t n_replicas, int mode, d
     // hardware ids) in the profile slots, for the finish-time spread of one resident round
     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
 #endif
+#if K10S_RUN_ARGS_LDS
+    if (threadIdx.x == 0) {   // staged before hdr_copy's barrier
+        k10s_run.limit = mode == K10S_RUN_UNTIL_TIME ? until_time : max_time;
+        k10s_run.budget = budget;
+        k10s_run.until_mode = mode == K10S_RUN_UNTIL_TIME ? 1u : 0u;
+    }
+#endif
     hdr_copy((uint32_t*)&k10s_hdr, hdr_global(r));
     Ctx c;
     int more = run_replica(c, mode, until_time, max_time, budget);
@@ -86,7 +93,10 @@ __global__ K10S_RUN_BOUNDS void k10s_run_kernel(uint32_t n_replicas, int mode, d
 #endif
     __syncthreads();
     hdr_copy(hdr_global(r), (const uint32_t*)&k10s_hdr);
-    if (more && threadIdx.x == 0) atomicAdd(active, 1u);
+    (void)active;   // the same pointer, read after the loop through the constant block
+#if K10S_DEVICE
+    if (more && threadIdx.x == 0) atomicAdd(K10S_DC.active, 1u);
+#endif
 }
 
 #ifndef K10S_PLUGINS_TU

@@ -331,6 +331,7 @@ struct DevConst {
     Layout L;
     K10S_RO(Params) params;   // [n_replicas]
     K10S_GB(uint8_t) base;    // replica regions, stride L.stride
+    uint32_t* active;         // count of replicas with work left after a budgeted launch
 };
 
 }  // namespace k10s
