@@ -116,3 +116,35 @@ def test_c3_backlog_full_size_gpu():
         else:
             assert k["flushed"] > 0, k
             assert x["estimators"]["pod_queue_time"][2] > 300.0  # waited past the flush age
+
+
+# ---- node churn ---------------------------------------------------------------------------------
+def _churn(n_pods, window, removed_frac=0.5, seed=31):
+    """C3 cluster where a random half of the nodes is removed while pods run and a quarter of those
+    is created again under the same names later, so
+    the screened scan meets removed nodes (their cache entries are (0, 0), k10s_engine.h
+    S_REMOVE_NODE), pods rescheduled from removed nodes (scheduler.rs:352-364) and re-added nodes."""
+    import random
+    c, w = wl.c3_traces(n_nodes=4096, n_pods=n_pods, arrival_window=window, seed=seed)
+    rng = random.Random(seed)
+    nodes = [e.node for e in c.events if e.kind == "create_node"]
+    gone = rng.sample(nodes, int(removed_frac * len(nodes)))
+    for i, nd in enumerate(gone):
+        c.remove_node(window * (0.2 + 0.5 * i / len(gone)), nd.name)
+    for nd in gone[: len(gone) // 4]:
+        c.create_node(window * 0.8, nd)
+    return c, w
+
+
+def test_c3_node_churn_host():
+    c, w = _churn(n_pods=600, window=40.0)
+    res = _check("host", c, w, R=1, checked=[0], base_seed=600)
+    assert res[0]["counters"]["placements"] >= 600
+
+
+@pytest.mark.gpu
+def test_c3_node_churn_gpu():
+    c, w = _churn(n_pods=4096, window=300.0)
+    res = _check("gpu", c, w, R=8, checked=[0, 3, 6], base_seed=600, cluster_blob=True)
+    for x in res:
+        assert x["status"] == "finished" and x["counters"]["placements"] >= 4096, x["counters"]
