@@ -5,6 +5,7 @@ Each test body runs against two backends:
   * "gpu"  — the product: build/libk10s.so on a MI355X (pytest -m gpu);
   * "host" — the TEST-ONLY host build of the same engine source (tests/hostcheck), on CPU.
 """
+import os
 import math
 import random
 
@@ -61,7 +62,9 @@ def test_hpa_checkpoints(backend):
 
 
 FUZZ_SEEDS_HOST = list(range(0, 120))
-FUZZ_SEEDS_GPU = list(range(0, 60))
+# K10S_FUZZ_GPU_SEEDS=N widens the GPU sweep to seeds 0..N-1 (an extended run, e.g. after kernel
+# changes; the default keeps the round-end suite short)
+FUZZ_SEEDS_GPU = list(range(0, int(os.environ.get("K10S_FUZZ_GPU_SEEDS", "60"))))
 
 
 def _fuzz(backend, seed):
