@@ -947,12 +947,15 @@ K10S_D float wave_min_f32(float v) {
 #ifndef K10S_SCREEN_NO_PRESENCE
 #define K10S_SCREEN_NO_PRESENCE 1
 #endif
-#if K10S_SCREEN_NO_PRESENCE
-#define SCREEN_LOAD(c, r, p, n, n0) scan_load_np(c, r, n, n0)
-#else
-#define SCREEN_LOAD(c, r, p, n, n0) scan_load(c, r, p, n, n0)
+// NP: the event loop's own node cache (absent nodes hold (0, 0): no presence words read); the unit
+// surface's caller-owned buffers keep their presence bitmap.
+#define SCREEN_LOAD(c, r, p, n, n0) ((NP && K10S_SCREEN_NO_PRESENCE) ? scan_load_np(c, r, n, n0) : scan_load(c, r, p, n, n0))
+// K10S_UNIT_SCREEN (default 1): the unit surface (k10s_schedule_kernel) screens too.  Scoring every
+// node exactly (two f64 divisions) made it VALU-bound below the HBM roofline.
+#ifndef K10S_UNIT_SCREEN
+#define K10S_UNIT_SCREEN 1
 #endif
-template <int PIPE>
+template <int PIPE, bool NP = true>
 K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
                               uint32_t rc, uint64_t rr, double& best_s, int32_t& best_n) {
     const uint32_t l4 = 4u * (uint32_t)lane_id();
@@ -1019,7 +1022,9 @@ K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const ui
         // score is a finite number >= 0: filtered[0] is never NaN, "some node fits" <=> best_n >= 0,
         // and neither filtered[0] nor its re-scored value is needed (kube_scheduler.rs:140-148).
         if (LOOP && K10S_SCAN_SCREEN)
-            scan_lanes_screen<K10S_LOOP_SCAN_PIPE>(s_cpu, s_ram, present, n_nodes, rc, rr, best_s, best_n);
+            scan_lanes_screen<K10S_LOOP_SCAN_PIPE, true>(s_cpu, s_ram, present, n_nodes, rc, rr, best_s, best_n);
+        else if (!LOOP && K10S_UNIT_SCREEN)
+            scan_lanes_screen<K10S_SCAN_PIPE, false>(s_cpu, s_ram, present, n_nodes, rc, rr, best_s, best_n);
         else
             scan_lanes<true, false, LOOP ? K10S_LOOP_SCAN_PIPE : K10S_SCAN_PIPE>(s_cpu, s_ram, present, n_nodes, rc,
                                                                                 rr, weight, first, best_s, best_n);
