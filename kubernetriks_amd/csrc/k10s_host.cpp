@@ -55,6 +55,7 @@ struct k10s_engine {
     Params* d_params = nullptr;
     uint32_t* d_active = nullptr;
     uint32_t* h_active = nullptr;  // pinned
+    RepHdr* h_hdr = nullptr;       // pinned staging for the replica headers (results / profile readback)
     DevConst* h_dc = nullptr;      // pinned launch constants
     std::vector<Params> params;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -81,6 +82,7 @@ static void engine_free(k10s_engine* e) {
     if (e->d_params) (void)hipFree(e->d_params);
     if (e->d_active) (void)hipFree(e->d_active);
     if (e->h_active) (void)hipHostFree(e->h_active);
+    if (e->h_hdr) (void)hipHostFree(e->h_hdr);
     if (e->h_dc) (void)hipHostFree(e->h_dc);
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
@@ -379,24 +381,32 @@ int32_t k10s_engine_run(k10s_engine* e, int32_t mode, double until_time, double 
     return K10S_OK;
 }
 
+// All replica headers into the engine's pinned staging buffer (one strided DMA; a pageable
+// destination would be copied through a bounce buffer).
+static int32_t read_all_hdrs(const k10s_engine* ce) {
+    k10s_engine* e = const_cast<k10s_engine*>(ce);
+    HIPCHK(hipSetDevice(e->device));
+    if (!e->h_hdr) HIPCHK(hipHostMalloc(&e->h_hdr, sizeof(RepHdr) * (size_t)e->R));
+    HIPCHK(hipMemcpy2DAsync(e->h_hdr, sizeof(RepHdr), e->d_state + e->L.hdr, e->L.stride, sizeof(RepHdr), e->R,
+                            hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return K10S_OK;
+}
+
 int32_t k10s_engine_results(const k10s_engine* e, k10s_replica_result* out) {
     if (!e || !out) return set_err(K10S_E_INVALID, "null");
-    std::vector<RepHdr> hdr(e->R);
-    HIPCHK(hipSetDevice(e->device));
-    HIPCHK(hipMemcpy2D(hdr.data(), sizeof(RepHdr), e->d_state + e->L.hdr, e->L.stride, sizeof(RepHdr), e->R,
-                       hipMemcpyDeviceToHost));
-    for (uint32_t r = 0; r < e->R; r++) hdr_to_result(hdr[r], out[r]);
+    int32_t rc = read_all_hdrs(e);
+    if (rc != K10S_OK) return rc;
+    for (uint32_t r = 0; r < e->R; r++) hdr_to_result(e->h_hdr[r], out[r]);
     return K10S_OK;
 }
 
 int32_t k10s_engine_profile(const k10s_engine* e, uint64_t* out) {
     if (!e || !out) return set_err(K10S_E_INVALID, "null");
-    std::vector<RepHdr> hdr(e->R);
-    HIPCHK(hipSetDevice(e->device));
-    HIPCHK(hipMemcpy2D(hdr.data(), sizeof(RepHdr), e->d_state + e->L.hdr, e->L.stride, sizeof(RepHdr), e->R,
-                       hipMemcpyDeviceToHost));
+    int32_t rc = read_all_hdrs(e);
+    if (rc != K10S_OK) return rc;
     for (uint32_t r = 0; r < e->R; r++)
-        for (int i = 0; i < K10S_PROF_SLOTS; i++) out[(size_t)r * K10S_PROF_SLOTS + i] = hdr[r].prof[i];
+        for (int i = 0; i < K10S_PROF_SLOTS; i++) out[(size_t)r * K10S_PROF_SLOTS + i] = e->h_hdr[r].prof[i];
     return K10S_OK;
 }
 
