@@ -84,7 +84,12 @@ def _free_port() -> int:
 
 def launch_ranks(n: int) -> int:
     """Start n rank processes of this script (one per GPU) and return the worst exit status.  The
-    parent never initialises the GPU (an exec/fork after GPU init is unsafe), it only waits."""
+    parent never initialises the GPU (an exec/fork after GPU init is unsafe), it only waits.  It
+    brings the engine library up to date first (hipcc only, no GPU), so the ranks never compile,
+    let alone concurrently; build() also serializes on a file lock for launchers other than this one
+    (torch.distributed.run)."""
+    from kubernetriks_amd.build import build
+    build()
     port = str(_free_port())
     procs = []
     for r in range(n):

@@ -24,7 +24,8 @@
  * Errors: every function returns K10S_OK (0) or a negative K10S_E_* code; a reference
  * `panic!` inside one replica is not an ABI error — it stops that replica and is reported in
  * k10s_replica_result.error_code (K10S_PANIC_*), like the reference process would abort.
- * Threading: one handle per device; a handle is not thread-safe.
+ * Threading: one handle per device; a handle is not thread-safe (the read-back calls
+ * k10s_engine_results / k10s_engine_profile serialize among themselves on one handle).
  */
 #ifndef K10S_H
 #define K10S_H

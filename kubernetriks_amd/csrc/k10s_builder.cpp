@@ -738,6 +738,7 @@ Layout make_layout(const HostScenario& hs, const k10s_capacities& caps) {
     L.words_nodes = (uint32_t)((N + 63) / 64);
     L.words_uids = (uint32_t)((hs.n_uids + 63) / 64);
     L.words_group = (uint32_t)((hs.group_bound + 63) / 64);
+    L.words_pods = (uint32_t)((P + 63) / 64);
     L.cap_heap = caps.event_heap ? caps.event_heap : (uint32_t)std::min<uint64_t>(3 * P + 4 * N + 4 * S + 64, 0x7FFFFFFF);
     L.cap_aq = caps.active_queue ? caps.active_queue : (uint32_t)(P + 16);
     L.cap_uq = caps.unschedulable ? caps.unschedulable : (uint32_t)(P + 16);
@@ -789,6 +790,12 @@ Layout make_layout(const HostScenario& hs, const k10s_capacities& caps) {
     L.ca_cpu = take(4 * ca_n);
     L.ca_ram = take(8 * ca_n);
     L.ca_undo = take(8 * (uint64_t)L.cap_undo);
+    const uint64_t ca_on = hs.ca_enabled ? 1 : 0;
+    L.ca_ubits = take(ca_on * 8 * (uint64_t)L.words_pods);
+    L.ca_live = take(ca_on * 8 * (uint64_t)L.words_nodes);
+    L.ps_head = take(ca_on * 4 * N);
+    L.ps_link = take(ca_on * 8 * P);
+    L.ca_list = take(ca_on * 8 * P);
     L.heap = take(sizeof(HeapEv) * (uint64_t)L.cap_heap);
     L.aq = take(sizeof(QInfo) * (uint64_t)L.cap_aq);
     L.uq = take(sizeof(QInfo) * (uint64_t)L.cap_uq);

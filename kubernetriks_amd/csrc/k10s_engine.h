@@ -96,6 +96,11 @@ struct Rep {
     K10S_HD uint32_t* ca_cpu() const { return at<uint32_t>(L().ca_cpu); }
     K10S_HD uint64_t* ca_ram() const { return at<uint64_t>(L().ca_ram); }
     K10S_HD uint32_t* ca_undo() const { return at<uint32_t>(L().ca_undo); }
+    K10S_HD uint64_t* ca_ubits() const { return at<uint64_t>(L().ca_ubits); }
+    K10S_HD uint64_t* ca_live() const { return at<uint64_t>(L().ca_live); }
+    K10S_HD int32_t* ps_head() const { return at<int32_t>(L().ps_head); }
+    K10S_HD int32_t* ps_link() const { return at<int32_t>(L().ps_link); }   // [2p] prev, [2p + 1] next
+    K10S_HD uint32_t* ca_list() const { return at<uint32_t>(L().ca_list); }
     K10S_HD HeapEv* heap() const { return at<HeapEv>(L().heap); }
     K10S_HD HeapEv* fq() const { return at<HeapEv>(L().fq); }
     K10S_HD QInfo* aq() const { return at<QInfo>(L().aq); }
@@ -1526,6 +1531,110 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
 // info is a snapshot of PS state at that instant, and the CA's node-group state is only touched
 // by autoscale() while exactly one request is in flight, so deciding at snapshot time and
 // emitting the actions at delivery time (cluster_autoscaler.rs:309-331) is equivalent.
+//
+// Lane-parallel where the reference loops over collections: the unscheduled-pod cache and the
+// CA-origin nodes are bitmaps read 64 words per step (set bits visited in ascending index = name
+// order), a node's assigned pods come from its PS assignment list (O(pods on the node), then sorted
+// by name), and every first-fit over nodes is a wave "lowest fitting index" over 4-node lane groups.
+// The serial parts are the reference's own sequential dependences (each placement changes the
+// allocatable the next pod sees).
+
+// Calls f(i) for every set bit i of words[0, W) in ascending order; stops early on an error.
+template <typename F>
+K10S_HD void for_each_bit(Ctx& c, const uint64_t* words, uint32_t W, F f) {
+    for (uint32_t wb = 0; wb < W; wb += K10S_LANES) {
+        const uint32_t w = wb + (uint32_t)lane_id();
+        const uint64_t word = w < W ? words[w] : 0ull;
+#if K10S_DEVICE
+        uint64_t nz = __ballot(word != 0);
+        while (nz) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(nz);
+            nz &= nz - 1;
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)word, (int)l);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(word >> 32), (int)l);
+            uint64_t bits = (uint64_t)lo | ((uint64_t)hi << 32);
+            while (bits) {
+                const uint32_t b = (uint32_t)__builtin_ctzll(bits);
+                bits &= bits - 1;
+                f((wb + l) * 64u + b);
+                if (c.H().error_code) return;
+            }
+        }
+#else
+        uint64_t bits = word;
+        while (bits) {
+            const uint32_t b = (uint32_t)__builtin_ctzll(bits);
+            bits &= bits - 1;
+            f(w * 64u + b);
+            if (c.H().error_code) return;
+        }
+#endif
+    }
+}
+
+// Lowest index m in [0, n), m != skip, with rc <= ca_cpu[m] && rr <= ca_ram[m]; -1 if none.
+// (node_fits_pod, kube_cluster_autoscaler.rs:82-85, as the first-fit loops 114-123 / 159-178 use it.)
+K10S_HD int32_t ca_first_fit(Ctx& c, uint32_t n, uint32_t skip, uint32_t rc, uint64_t rr) {
+    const uint32_t* cc = c.V().ca_cpu();
+    const uint64_t* cr = c.V().ca_ram();
+#if K10S_DEVICE
+    // each lane tests 4 consecutive entries per 256-entry step (one 16-B cpu load, two 16-B ram
+    // loads: the sections are 256-B aligned and padded, entries >= n are masked out)
+    const uint32_t l4 = 4u * (uint32_t)lane_id();
+    for (uint32_t base = 0; base < n; base += 256) {
+        const uint32_t m0 = base + l4;
+        uint32_t bits = 0;
+        if (m0 < n) {
+            const uint4 cv = *reinterpret_cast<const uint4*>(cc + m0);
+            const ulonglong2 r01 = *reinterpret_cast<const ulonglong2*>(cr + m0);
+            const ulonglong2 r23 = *reinterpret_cast<const ulonglong2*>(cr + m0 + 2);
+            bits = (uint32_t)(rc <= cv.x && rr <= r01.x) | ((uint32_t)(rc <= cv.y && rr <= r01.y) << 1) |
+                   ((uint32_t)(rc <= cv.z && rr <= r23.x) << 2) | ((uint32_t)(rc <= cv.w && rr <= r23.y) << 3);
+            const uint32_t valid = n - m0;
+            bits &= valid >= 4 ? 0xFu : ((1u << valid) - 1u);
+            if (skip - m0 < 4u) bits &= ~(1u << (skip - m0));
+        }
+        const uint64_t any = __ballot(bits != 0);
+        if (any) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(any);
+            const uint32_t lb = (uint32_t)__builtin_amdgcn_readlane((int)bits, (int)l);
+            return (int32_t)(base + 4u * l + (uint32_t)__builtin_ctz(lb));
+        }
+    }
+    return -1;
+#else
+    for (uint32_t m = 0; m < n; m++)
+        if (m != skip && rc <= cc[m] && rr <= cr[m]) return (int32_t)m;
+    return -1;
+#endif
+}
+
+// Sort the k distinct pod indices src[0, k) ascending into dst[0, k) (BTreeSet<String> order of a
+// node's assignment set).  Device: rank sort, 64 elements per pass against all k.
+K10S_HD void ca_sort(const uint32_t* src, uint32_t* dst, uint32_t k) {
+#if K10S_DEVICE
+    const uint32_t lane = (uint32_t)lane_id();
+    for (uint32_t cb = 0; cb < k; cb += 64) {
+        const uint32_t mine = cb + lane < k ? src[cb + lane] : 0xFFFFFFFFu;
+        uint32_t rank = 0;
+        for (uint32_t ob = 0; ob < k; ob += 64) {
+            const uint32_t other = ob + lane < k ? src[ob + lane] : 0xFFFFFFFFu;
+            const uint32_t m = k - ob < 64u ? k - ob : 64u;
+            for (uint32_t j = 0; j < m; j++)
+                rank += (uint32_t)__builtin_amdgcn_readlane((int)other, (int)j) < mine ? 1u : 0u;
+        }
+        if (cb + lane < k) dst[rank] = mine;
+    }
+    wave_sync();
+#else
+    for (uint32_t i = 0; i < k; i++) {
+        uint32_t x = src[i], j = i;
+        for (; j > 0 && dst[j - 1] > x; j--) dst[j] = dst[j - 1];
+        dst[j] = x;
+    }
+#endif
+}
+
 K10S_COLD void ca_decide(Ctx& c) {
     RepHdr* h = &c.H();
     const Scenario* sc = &c.S();
@@ -1535,11 +1644,9 @@ K10S_COLD void ca_decide(Ctx& c) {
     if (h->unsched_cache_count > 0) {
         // scale_up_info (persistent_storage.rs:137-145) looks every cached unscheduled pod up in
         // storage before the algorithm runs: a removed one panics (the cache is never cleaned, A.5)
-        for (uint32_t p = 0; p < sc->n_pods; p++) {
-            if ((c.V().pod(p).flags & PF_UNSCHED) && !(c.V().pod(p).flags & PF_IN_PS)) {
-                fail(c, K10S_PANIC_MISSING_POD);
-                return;
-            }
+        if (h->unsched_missing > 0) {
+            fail(c, K10S_PANIC_MISSING_POD);
+            return;
         }
         // scale_up (191-245)
         uint64_t cur = 0;
@@ -1555,27 +1662,23 @@ K10S_COLD void ca_decide(Ctx& c) {
         }
         if (over) return;
         uint32_t nalloc = 0;
-        for (uint32_t p = 0; p < sc->n_pods && !c.H().error_code; p++) {
-            if (!(c.V().pod(p).flags & PF_UNSCHED)) continue;
-            uint32_t rc = c.V().pod(p).req_cpu;
-            uint64_t rr = c.V().pod(p).req_ram;
-            bool fit = false;
-            for (uint32_t i = 0; i < nalloc; i++) {  // try_fit_in_allocated_nodes (114-123)
-                if (rc <= c.V().ca_cpu()[i] && rr <= c.V().ca_ram()[i]) {
-                    c.V().ca_cpu()[i] -= rc;
-                    c.V().ca_ram()[i] -= rr;
-                    fit = true;
-                    break;
-                }
+        // the unscheduled-pod cache in name order (BTreeSet, persistent_storage.rs:41)
+        for_each_bit(c, c.V().ca_ubits(), c.Ly().words_pods, [&](uint32_t p) {
+            const uint32_t rc = uniform_u32(c.V().pod(p).req_cpu);
+            const uint64_t rr = uniform_u64(c.V().pod(p).req_ram);
+            const int32_t i = ca_first_fit(c, nalloc, 0xFFFFFFFFu, rc, rr);   // try_fit_in_allocated_nodes (114-123)
+            if (i >= 0) {
+                c.V().ca_cpu()[i] -= rc;
+                c.V().ca_ram()[i] -= rr;
+                return;
             }
-            if (fit) continue;
-            if (cur >= max_nodes) continue;
+            if (cur >= max_nodes) return;
             for (uint32_t g = 0; g < sc->n_ca_groups; g++) {  // try_find_fitting_template (88-112)
                 if (sc->ca_has_max[g] && cag[2 * g] >= sc->ca_max[g]) continue;
                 if (rc <= sc->ca_cpu[g] && rr <= sc->ca_ram[g]) {
                     cag[2 * g] += 1;
                     cag[2 * g + 1] += 1;
-                    uint32_t k = cag[2 * g + 1];
+                    const uint32_t k = cag[2 * g + 1];
                     if (k > sc->ca_bound) {
                         fail(c, K10S_ERR_NAME_BOUND);
                         return;
@@ -1588,66 +1691,98 @@ K10S_COLD void ca_decide(Ctx& c) {
                     c.V().ca_act()[nalloc].arg = sc->ca_def[g * sc->ca_bound + (k - 1)];
                     c.V().ca_cpu()[nalloc] = sc->ca_cpu[g];
                     c.V().ca_ram()[nalloc] = sc->ca_ram[g];
+                    wave_sync();
                     nalloc++;
                     cur++;
-                    break;
+                    return;
                 }
             }
-        }
+        });
         h->ca_n_act = nalloc;
         return;
     }
-    // scale_down (247-306) over PS nodes in name order with a mutable copy of their allocatable
+    // scale_down (247-306) over the PS-present CA-origin nodes in name order.  `info.nodes` is
+    // materialized lazily: until some candidate has pods to move, every node's allocatable is its
+    // PS value; the first such candidate copies all of them (absent nodes as (0, 0), so they fit
+    // no pod with a nonzero request) and the moves then mutate the copy (all_pods_can_be_moved_to_
+    // other_nodes, 148-181).
     const uint32_t N = sc->n_nodes;
-    for (uint32_t n = 0; n < N; n++) {
-        c.V().ca_cpu()[n] = c.V().node(n).ps_cpu;
-        c.V().ca_ram()[n] = c.V().node(n).ps_ram;
-    }
+    bool copied = false;
     uint32_t nrem = 0;
-    for (uint32_t n = 0; n < N && !c.H().error_code; n++) {
-        if (!(c.V().node(n).flags & NF_PS_PRESENT)) continue;
-        uint32_t def = c.V().node(n).ps_def;
-        if (!sc->def_ca_origin[def]) continue;
-        uint32_t cap_c = sc->def_cpu[def];
-        uint64_t cap_r = sc->def_ram[def];
-        double cu = (double)(uint32_t)(cap_c - c.V().ca_cpu()[n]) / (double)cap_c;
-        double ru = (double)(uint64_t)(cap_r - c.V().ca_ram()[n]) / (double)cap_r;
-        double util = cu > ru ? cu : ru;
-        if (!(util < c.P().ca_scale_down_utilization_threshold)) continue;
-        // all_pods_can_be_moved_to_other_nodes (148-181): pods in PS assignments[n], name order
-        uint32_t nundo = 0;
-        bool ok = true;
-        uint32_t ep = c.V().node(n).ps_epoch;
-        for (uint32_t p = 0; p < sc->n_pods && ok; p++) {
-            if (c.V().pod(p).ps_assigned != (int32_t)n || c.V().pod(p).ps_aepoch != ep || ep == 0) continue;
-            uint32_t rc = c.V().pod(p).req_cpu;
-            uint64_t rr = c.V().pod(p).req_ram;
-            bool placed = false;
-            for (uint32_t m = 0; m < N; m++) {
-                if (m == n || !(c.V().node(m).flags & NF_PS_PRESENT)) continue;
-                if (rc <= c.V().ca_cpu()[m] && rr <= c.V().ca_ram()[m]) {
-                    c.V().ca_cpu()[m] -= rc;
-                    c.V().ca_ram()[m] -= rr;
-                    if (nundo >= c.Ly().cap_undo) {
-                        fail(c, K10S_ERR_CA_BUFFER);
-                        return;
+    for_each_bit(c, c.V().ca_live(), c.Ly().words_nodes, [&](uint32_t n) {
+        const NodeState& ND = c.V().node(n);
+        const uint32_t def = uniform_u32(ND.ps_def);
+        const uint32_t cap_c = sc->def_cpu[def];
+        const uint64_t cap_r = sc->def_ram[def];
+        const uint32_t ac = uniform_u32(copied ? c.V().ca_cpu()[n] : ND.ps_cpu);
+        const uint64_t ar = uniform_u64(copied ? c.V().ca_ram()[n] : ND.ps_ram);
+        const double cu = (double)(uint32_t)(cap_c - ac) / (double)cap_c;   // is_under_threshold_utilization (128-142)
+        const double ru = (double)(uint64_t)(cap_r - ar) / (double)cap_r;
+        const double util = cu > ru ? cu : ru;
+        if (!(util < c.P().ca_scale_down_utilization_threshold)) return;
+        // the node's assigned pods in name order (info.assignments[node], 271-276)
+        uint32_t* gath = c.V().ca_list();
+        uint32_t* sorted = gath + sc->n_pods;
+        uint32_t k = 0;
+        for (int32_t p = uniform_u32((uint32_t)c.V().ps_head()[n]); p >= 0;
+             p = (int32_t)uniform_u32((uint32_t)c.V().ps_link()[2 * p + 1])) {
+            if (k >= sc->n_pods) {   // a corrupt list would never end: impossible by construction
+                fail(c, K10S_ERR_CA_BUFFER);
+                return;
+            }
+            gath[k++] = (uint32_t)p;
+        }
+        wave_sync();
+        if (k > 0) {
+            ca_sort(gath, sorted, k);
+            if (!copied) {
+                for (uint32_t m = (uint32_t)lane_id(); m < N; m += K10S_LANES) {
+                    const NodeState& M = c.V().node(m);
+                    const bool pres = (M.flags & NF_PS_PRESENT) != 0;
+                    c.V().ca_cpu()[m] = pres ? M.ps_cpu : 0u;
+                    c.V().ca_ram()[m] = pres ? M.ps_ram : 0ull;
+                }
+                wave_sync();
+                copied = true;
+            }
+            uint32_t nundo = 0;
+            bool ok = true;
+            for (uint32_t i = 0; i < k; i++) {
+                const uint32_t p = uniform_u32(sorted[i]);
+                const uint32_t rc = uniform_u32(c.V().pod(p).req_cpu);
+                const uint64_t rr = uniform_u64(c.V().pod(p).req_ram);
+                if (rc == 0 && rr == 0) {   // fits any other PS node; (0, 0) absent entries must not count
+                    if (c.H().ps_node_count < 2) {
+                        ok = false;
+                        break;
                     }
-                    c.V().ca_undo()[2 * nundo] = m;
-                    c.V().ca_undo()[2 * nundo + 1] = p;
-                    nundo++;
-                    placed = true;
+                    continue;
+                }
+                const int32_t m = ca_first_fit(c, N, n, rc, rr);
+                if (m < 0) {
+                    ok = false;
                     break;
                 }
+                c.V().ca_cpu()[m] -= rc;
+                c.V().ca_ram()[m] -= rr;
+                if (nundo >= c.Ly().cap_undo) {
+                    fail(c, K10S_ERR_CA_BUFFER);
+                    return;
+                }
+                c.V().ca_undo()[2 * nundo] = (uint32_t)m;
+                c.V().ca_undo()[2 * nundo + 1] = p;
+                nundo++;
+                wave_sync();
             }
-            if (!placed) ok = false;
-        }
-        if (!ok) {
-            for (uint32_t i = 0; i < nundo; i++) {  // *nodes = original
-                uint32_t m = c.V().ca_undo()[2 * i], p = c.V().ca_undo()[2 * i + 1];
-                c.V().ca_cpu()[m] += c.V().pod(p).req_cpu;
-                c.V().ca_ram()[m] += c.V().pod(p).req_ram;
+            if (!ok) {
+                for (uint32_t i = 0; i < nundo; i++) {  // *nodes = original
+                    const uint32_t m = uniform_u32(c.V().ca_undo()[2 * i]), p = uniform_u32(c.V().ca_undo()[2 * i + 1]);
+                    c.V().ca_cpu()[m] += c.V().pod(p).req_cpu;
+                    c.V().ca_ram()[m] += c.V().pod(p).req_ram;
+                    wave_sync();
+                }
+                return;
             }
-            continue;
         }
         if (nrem >= c.Ly().cap_act) {
             fail(c, K10S_ERR_CA_BUFFER);
@@ -1656,9 +1791,10 @@ K10S_COLD void ca_decide(Ctx& c) {
         c.V().ca_act()[nrem].up = 0;
         c.V().ca_act()[nrem].arg = n;
         nrem++;
-    }
+    });
+    if (c.H().error_code) return;
     for (uint32_t i = 0; i < nrem; i++) {
-        uint32_t n = c.V().ca_act()[i].arg;
+        uint32_t n = uniform_u32(c.V().ca_act()[i].arg);
         int32_t g = sc->def_ca_group[c.V().node(n).ps_def];
         if (g < 0) {
             fail(c, K10S_PANIC_CA_GROUP);
@@ -1670,6 +1806,24 @@ K10S_COLD void ca_decide(Ctx& c) {
 }
 
 // ---- persistent storage (persistent_storage.rs:185-490) --------------------------------------
+// The PS assignment set of a CA-origin node as an intrusive doubly-linked list (insertion order;
+// the CA sorts a node's members by name when it needs them, kube_cluster_autoscaler.rs:271-277).
+K10S_HD void ps_list_insert(Ctx& c, uint32_t n, uint32_t p) {
+    int32_t* link = c.V().ps_link();
+    const int32_t h = c.V().ps_head()[n];
+    link[2 * p] = -1;
+    link[2 * p + 1] = h;
+    if (h >= 0) link[2 * h] = (int32_t)p;
+    c.V().ps_head()[n] = (int32_t)p;
+}
+K10S_HD void ps_list_remove(Ctx& c, uint32_t n, uint32_t p) {
+    int32_t* link = c.V().ps_link();
+    const int32_t pr = link[2 * p], nx = link[2 * p + 1];
+    if (pr >= 0) link[2 * pr + 1] = nx;
+    else c.V().ps_head()[n] = nx;
+    if (nx >= 0) link[2 * nx] = pr;
+}
+
 K10S_HD void ps_clean_up(Ctx& c, uint32_t p) {  // 173-182
     PodState& P = c.V().pod(p);
     const int32_t n = P.ps_assigned;
@@ -1683,7 +1837,10 @@ K10S_HD void ps_clean_up(Ctx& c, uint32_t p) {  // 173-182
     if (nf & NF_PS_PRESENT) {
         N.ps_cpu = ncpu + rc;
         N.ps_ram = nram + rr;
-        if (pae == nep) P.ps_aepoch = 0;
+        if (pae == nep) {
+            P.ps_aepoch = 0;
+            if (nf & NF_CA_ORIGIN) ps_list_remove(c, (uint32_t)n, p);
+        }
     }
 }
 
@@ -1698,12 +1855,18 @@ K10S_WARM void on_ps(Ctx& c, HeapEv e) {
             fail(c, K10S_PANIC_DUPLICATE_NODE);
             return;
         }
-        c.V().node(n).flags |= NF_PS_PRESENT;
+        // NF_CA_ORIGIN (and the assignment list behind it) only when the CA runs: its only reader
+        const bool ca_origin = c.S().ca_enabled && c.S().def_ca_origin[def] != 0;
+        c.V().node(n).flags = (uint8_t)((c.V().node(n).flags & ~NF_CA_ORIGIN) | NF_PS_PRESENT | (ca_origin ? NF_CA_ORIGIN : 0));
         c.V().node(n).ps_def = def;
         c.V().node(n).ps_cpu = c.S().def_cpu[def];
         c.V().node(n).ps_ram = c.S().def_ram[def];
         c.V().node(n).ps_epoch += 1;
         h->ps_node_count += 1;
+        if (ca_origin) {  // a new, empty assignment set (persistent_storage.rs:70-84)
+            c.V().ps_head()[n] = -1;
+            bit_set(c.V().ca_live(), n);
+        }
         emit(c, K10S_EV_AS_CREATE_NODE_RESP, pr->as_to_ps_network_delay, -1, n, 0, 0.0, FQ_AS_TO_PS);
         break;
     }
@@ -1719,11 +1882,13 @@ K10S_WARM void on_ps(Ctx& c, HeapEv e) {
     }
     case K10S_EV_PS_CREATE_POD_REQ: {
         uint32_t p = e.a;
-        if (c.V().pod(p).flags & PF_IN_PS) {
+        const uint8_t pf = c.V().pod(p).flags;
+        if (pf & PF_IN_PS) {
             fail(c, K10S_PANIC_DUPLICATE_POD);
             return;
         }
-        c.V().pod(p).flags |= PF_IN_PS;
+        c.V().pod(p).flags = (uint8_t)(pf | PF_IN_PS);
+        if (pf & PF_UNSCHED) h->unsched_missing -= 1;  // a re-created pod of the unscheduled cache
         c.V().pod(p).ps_assigned = -1;
         if (c.V().prec()) c.V().prec()[p].state = 1;
         emit(c, K10S_EV_S_POD_SCHEDULE_REQ, pr->ps_to_sched_network_delay, -1, p, 0, 0.0, FQ_PS_TO_SCHED);
@@ -1744,6 +1909,7 @@ K10S_WARM void on_ps(Ctx& c, HeapEv e) {
         if (pf & PF_UNSCHED) {
             P.flags = (uint8_t)(pf & ~PF_UNSCHED);
             h->unsched_cache_count -= 1;
+            if (c.S().ca_enabled) bit_clear(c.V().ca_ubits(), p);
         }
         if (!(nf & NF_PS_PRESENT)) {
             fail(c, K10S_PANIC_MISSING_NODE);
@@ -1752,6 +1918,7 @@ K10S_WARM void on_ps(Ctx& c, HeapEv e) {
         N.ps_cpu = ncpu - rc;
         N.ps_ram = nram - rr;
         P.ps_aepoch = nep;
+        if (nf & NF_CA_ORIGIN) ps_list_insert(c, n, p);
         emit(c, K10S_EV_AS_ASSIGN_RESP, pr->as_to_ps_network_delay, -1, p, n, 0.0, FQ_AS_TO_PS);
         break;
     }
@@ -1764,6 +1931,7 @@ K10S_WARM void on_ps(Ctx& c, HeapEv e) {
         if (!(c.V().pod(p).flags & PF_UNSCHED)) {
             c.V().pod(p).flags |= PF_UNSCHED;
             h->unsched_cache_count += 1;
+            if (c.S().ca_enabled) bit_set(c.V().ca_ubits(), p);
         }
         break;
     }
@@ -1783,6 +1951,7 @@ K10S_WARM void on_ps(Ctx& c, HeapEv e) {
         const double dur = P.dur;
         if (pf & PF_IN_PS) {
             P.flags = (uint8_t)(pf & ~PF_IN_PS);
+            if (pf & PF_UNSCHED) h->unsched_missing += 1;
             ps_clean_up(c, p);
             if (!(sflags & POD_HAS_DUR)) {
                 fail(c, K10S_PANIC_MISSING_POD);
@@ -1803,7 +1972,8 @@ K10S_WARM void on_ps(Ctx& c, HeapEv e) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
         }
-        c.V().node(n).flags &= (uint8_t)~NF_PS_PRESENT;
+        if (c.V().node(n).flags & NF_CA_ORIGIN) bit_clear(c.V().ca_live(), n);
+        c.V().node(n).flags &= (uint8_t)~(NF_PS_PRESENT | NF_CA_ORIGIN);
         h->ps_node_count -= 1;
         emit(c, K10S_EV_AS_REMOVE_NODE_RESP, pr->as_to_ps_network_delay, -1, n, 0, 0.0, FQ_AS_TO_PS);
         break;
@@ -1821,6 +1991,7 @@ K10S_WARM void on_ps(Ctx& c, HeapEv e) {
             emit(c, K10S_EV_AS_REMOVE_POD_RESP, pr->as_to_ps_network_delay, -1, p, 0, 0.0, FQ_AS_TO_PS);
             return;
         }
+        if (c.V().pod(p).flags & PF_UNSCHED) h->unsched_missing += 1;
         c.V().pod(p).flags &= (uint8_t)~PF_IN_PS;
         if (c.V().prec()) {
             c.V().prec()[p].t_removed = e.time;
@@ -2455,6 +2626,11 @@ K10S_HD void init_replica(Ctx& c) {
     }
     for (uint32_t i = lane; i < G * L->words_group; i += K10S_LANES) v.grp_bits()[i] = 0;
     for (uint32_t i = lane; i < 2 * sc->n_ca_groups; i += K10S_LANES) v.cag()[i] = 0;
+    if (sc->ca_enabled) {
+        for (uint32_t i = lane; i < L->words_pods; i += K10S_LANES) v.ca_ubits()[i] = 0;
+        for (uint32_t i = lane; i < L->words_nodes; i += K10S_LANES) v.ca_live()[i] = 0;
+        for (uint32_t i = lane; i < N; i += K10S_LANES) v.ps_head()[i] = -1;
+    }
     wave_sync();
 
     // serial part (wave-uniform) on the working header
@@ -2474,6 +2650,10 @@ K10S_HD void init_replica(Ctx& c) {
         uint32_t slot = sc->n_pool + j;
         NodeState& nd = v.node(n);
         nd.flags |= NF_PS_PRESENT;
+        if (sc->ca_enabled && sc->def_ca_origin[def]) {
+            nd.flags |= NF_CA_ORIGIN;
+            bit_set(v.ca_live(), n);
+        }
         nd.ps_def = def;
         nd.ps_cpu = sc->def_cpu[def];
         nd.ps_ram = sc->def_ram[def];
@@ -2729,12 +2909,33 @@ K10S_HD void consume_source(Ctx& c, int src) {
     }
 }
 
+// Does some node of the scheduler cache fit a (cpu, ram) request (Fit::filter, plugin.rs:34-45)?
+// Lane-parallel over node indices with an early exit; a zero request never schedules
+// (RequestedResourcesAreZeros, kube_scheduler.rs:74-76).
+K10S_HD bool cache_fits(Ctx& c, uint32_t rc, uint64_t rr) {
+    if (rc == 0 && rr == 0) return false;
+    const uint32_t N = c.S().n_nodes;
+    const uint32_t* cpu = c.V().s_cpu();
+    const uint64_t* ram = c.V().s_ram();
+    const uint64_t* pres = c.V().s_present();
+    for (uint32_t base = 0; base < N; base += K10S_LANES) {
+        const uint32_t n = base + (uint32_t)lane_id();
+        const bool f = n < N && bit_test(pres, n) && rc <= cpu[n] && rr <= ram[n];
+        if (wave_any(f)) return true;
+    }
+    return false;
+}
+
 // Stall guard (opt-in, k10s_capacities.stall_guard), evaluated after a gauge tick: the trace is
 // exhausted, the heap holds only the four periodic ticks (pod metrics, gauge, scheduling cycle,
 // flush; a pending pod finish, even a lazily canceled one, counts as progress), every delay-class
 // ring is empty, the action queue is empty and neither autoscaler runs.  Then no node's
-// allocatable can change again, every retry of an unschedulable pod fails as before, and the
-// replica would cycle until max_time (TIME_LIMIT) without terminating another pod.
+// allocatable can change again.  The replica is stalled only if, in addition, no live entry of the
+// unschedulable map fits any node of that frozen cache: then every retry fails as before and the
+// replica would cycle until max_time (TIME_LIMIT) without terminating another pod.  (With the
+// conditional move, scheduler.rs:210-233, a pod that fits only the resources freed by several
+// finishes together is not moved by any of them and waits for the 300-s flush, 188-203: such an
+// entry fits the cache now and keeps the replica running.)
 K10S_HD bool replica_stalled(Ctx& c) {
     const RepHdr& H = c.H();
     if (H.counters[K10S_C_TERMINATED_PODS] >= c.S().total_pods_in_trace) return false;
@@ -2742,6 +2943,13 @@ K10S_HD bool replica_stalled(Ctx& c) {
     if (c.S().ca_enabled || c.S().hpa_enabled) return false;
     for (int q = 0; q < K10S_NFQ; q++)
         if (H.fq_head[q] != H.fq_tail[q]) return false;
+    const QInfo* d = c.V().uq();
+    const uint32_t n = uniform_u32(H.uq_size);
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t p = uniform_u32(d[i].pod);
+        if (!pod_in_s(c, p)) continue;  // stale entry of a deleted pod: never moved again
+        if (cache_fits(c, uniform_u32(c.V().pod(p).req_cpu), uniform_u64(c.V().pod(p).req_ram))) return false;
+    }
     return true;
 }
 

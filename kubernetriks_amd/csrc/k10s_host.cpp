@@ -15,12 +15,12 @@
 
 using namespace k10s;
 
-hipError_t k10s_launch_init(const DevConst* h_dc, uint32_t n_replicas, hipStream_t s);
-hipError_t k10s_launch_run(const DevConst* h_dc, uint32_t n_replicas, int mode, double until_time, double max_time,
+hipError_t k10s_launch_init(const void* h_dc, uint32_t n_replicas, hipStream_t s);
+hipError_t k10s_launch_run(const void* h_dc, uint32_t n_replicas, int mode, double until_time, double max_time,
                            uint64_t budget, uint32_t* d_active, hipStream_t s);
 // the same two kernels with the score-plugin profile path compiled in (k10s_kernels_plugins.hip)
-hipError_t k10s_launch_init_plugins(const DevConst* h_dc, uint32_t n_replicas, hipStream_t s);
-hipError_t k10s_launch_run_plugins(const DevConst* h_dc, uint32_t n_replicas, int mode, double until_time,
+hipError_t k10s_launch_init_plugins(const void* h_dc, uint32_t n_replicas, hipStream_t s);
+hipError_t k10s_launch_run_plugins(const void* h_dc, uint32_t n_replicas, int mode, double until_time,
                                    double max_time, uint64_t budget, uint32_t* d_active, hipStream_t s);
 hipError_t k10s_launch_schedule(const uint32_t* alloc_cpu, const uint64_t* alloc_ram, const uint64_t* present,
                                 uint32_t n_nodes, uint32_t node_stride, const uint32_t* req_cpu, const uint64_t* req_ram,
@@ -55,7 +55,9 @@ struct k10s_engine {
     Params* d_params = nullptr;
     uint32_t* d_active = nullptr;
     uint32_t* h_active = nullptr;  // pinned
-    RepHdr* h_hdr = nullptr;       // pinned staging for the replica headers (results / profile readback)
+    RepHdr* h_hdr = nullptr;       // pinned staging for the replica headers (results / profile readback),
+                                   // allocated at create; hdr_mu serializes its fill-and-read
+    std::mutex hdr_mu;
     DevConst* h_dc = nullptr;      // pinned launch constants
     std::vector<Params> params;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -313,6 +315,7 @@ k10s_engine* k10s_engine_create_bulk(const char* scenario_text, const void* pods
         return fail("upload params");
     if (hipMalloc(&e->d_active, 64) != hipSuccess) return fail("hipMalloc active");
     if (hipHostMalloc(&e->h_active, 64) != hipSuccess) return fail("hipHostMalloc");
+    if (hipHostMalloc(&e->h_hdr, sizeof(RepHdr) * (size_t)e->R) != hipSuccess) return fail("hipHostMalloc");
     if (hipHostMalloc(&e->h_dc, sizeof(DevConst)) != hipSuccess) return fail("hipHostMalloc");
     std::memset(e->h_dc, 0, sizeof(DevConst));
     e->h_dc->sc = e->dsc;
@@ -382,27 +385,30 @@ int32_t k10s_engine_run(k10s_engine* e, int32_t mode, double until_time, double 
 }
 
 // All replica headers into the engine's pinned staging buffer (one strided DMA; a pageable
-// destination would be copied through a bounce buffer).
-static int32_t read_all_hdrs(const k10s_engine* ce) {
-    k10s_engine* e = const_cast<k10s_engine*>(ce);
+// destination would be copied through a bounce buffer).  The caller holds e->hdr_mu across the fill
+// and its reads of h_hdr, so concurrent read-back calls on one engine do not interleave.
+static int32_t read_all_hdrs(k10s_engine* e) {
     HIPCHK(hipSetDevice(e->device));
-    if (!e->h_hdr) HIPCHK(hipHostMalloc(&e->h_hdr, sizeof(RepHdr) * (size_t)e->R));
     HIPCHK(hipMemcpy2DAsync(e->h_hdr, sizeof(RepHdr), e->d_state + e->L.hdr, e->L.stride, sizeof(RepHdr), e->R,
                             hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     return K10S_OK;
 }
 
-int32_t k10s_engine_results(const k10s_engine* e, k10s_replica_result* out) {
-    if (!e || !out) return set_err(K10S_E_INVALID, "null");
+int32_t k10s_engine_results(const k10s_engine* ce, k10s_replica_result* out) {
+    if (!ce || !out) return set_err(K10S_E_INVALID, "null");
+    k10s_engine* e = const_cast<k10s_engine*>(ce);
+    std::lock_guard<std::mutex> g(e->hdr_mu);
     int32_t rc = read_all_hdrs(e);
     if (rc != K10S_OK) return rc;
     for (uint32_t r = 0; r < e->R; r++) hdr_to_result(e->h_hdr[r], out[r]);
     return K10S_OK;
 }
 
-int32_t k10s_engine_profile(const k10s_engine* e, uint64_t* out) {
-    if (!e || !out) return set_err(K10S_E_INVALID, "null");
+int32_t k10s_engine_profile(const k10s_engine* ce, uint64_t* out) {
+    if (!ce || !out) return set_err(K10S_E_INVALID, "null");
+    k10s_engine* e = const_cast<k10s_engine*>(ce);
+    std::lock_guard<std::mutex> g(e->hdr_mu);
     int32_t rc = read_all_hdrs(e);
     if (rc != K10S_OK) return rc;
     for (uint32_t r = 0; r < e->R; r++)

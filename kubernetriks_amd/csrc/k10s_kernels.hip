@@ -154,7 +154,11 @@ static hipError_t upload(const DevConst* h_dc, hipStream_t s) {
     return hipMemcpyToSymbolAsync(HIP_SYMBOL(k10s_dc), h_dc, sizeof(DevConst), 0, hipMemcpyHostToDevice, s);
 }
 
-hipError_t k10s_launch_init(const DevConst* h_dc, uint32_t n_replicas, hipStream_t s) {
+// The launchers take the constant block as an untyped pointer: the second copy of this file
+// (k10s_kernels_plugins.hip) compiles every engine type in its own namespace, so only C-level
+// types cross between the translation units.
+hipError_t k10s_launch_init(const void* h_dcv, uint32_t n_replicas, hipStream_t s) {
+    const DevConst* h_dc = (const DevConst*)h_dcv;
     std::lock_guard<std::mutex> g(g_launch_mu);
     hipError_t e = upload(h_dc, s);
     if (e != hipSuccess) return e;
@@ -162,8 +166,9 @@ hipError_t k10s_launch_init(const DevConst* h_dc, uint32_t n_replicas, hipStream
     return hipGetLastError();
 }
 
-hipError_t k10s_launch_run(const DevConst* h_dc, uint32_t n_replicas, int mode, double until_time, double max_time,
+hipError_t k10s_launch_run(const void* h_dcv, uint32_t n_replicas, int mode, double until_time, double max_time,
                            uint64_t budget, uint32_t* d_active, hipStream_t s) {
+    const DevConst* h_dc = (const DevConst*)h_dcv;
     std::lock_guard<std::mutex> g(g_launch_mu);
     hipError_t e = upload(h_dc, s);
     if (e != hipSuccess) return e;

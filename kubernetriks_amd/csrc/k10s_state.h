@@ -227,7 +227,10 @@ struct RepHdr {
     int64_t cont_k2;
     uint32_t cont_s2, cont_src;
     int64_t emit_kmin;            // (time key, id) of the smallest event emitted since
-    uint32_t emit_smin, cont_pad;
+    uint32_t emit_smin;
+    uint32_t unsched_missing;     // PS unscheduled-pod cache entries whose pod left storage (PF_UNSCHED
+                                  // without PF_IN_PS): scale_up_info would panic on them
+                                  // (persistent_storage.rs:137-145)
     HeapEv fq_win[K10S_NFQ * K10S_FQW];
     HeapEv heap_lds[K10S_HEAP_TOP];
 #if K10S_AQ_TOP
@@ -256,7 +259,9 @@ struct CAAct {
     uint32_t arg;           // def id (up) / node idx (down)
 };
 
-enum : uint8_t { NF_S_ASSIGN = 1, NF_PS_PRESENT = 2 };
+// NF_CA_ORIGIN: the node instance stored in PS carries origin = "cluster autoscaler"; its PS
+// assignment set is kept as a list (ps_head / ps_link) for the CA's scale-down
+enum : uint8_t { NF_S_ASSIGN = 1, NF_PS_PRESENT = 2, NF_CA_ORIGIN = 4 };
 enum : uint8_t { PF_IN_S = 1, PF_IN_PS = 2, PF_UNSCHED = 4 };
 
 // Per-pod state: every field an event handler touches for one pod, in one 64-B line.
@@ -313,12 +318,16 @@ struct Layout {
     uint64_t node, pend_rm, pod, prec, slot, pool_ring;
     uint64_t grp, grp_bits;
     uint64_t cag, ca_act, ca_cpu, ca_ram, ca_undo;
+    // cluster autoscaler only (0 bytes otherwise): the PS unscheduled-pod cache as a bitmap over pod
+    // indices (name order), the PS-present CA-origin nodes as a bitmap over node indices, the PS
+    // assignment sets of CA-origin nodes as intrusive lists, and a gather/sort scratch of 2·P entries
+    uint64_t ca_ubits, ca_live, ps_head, ps_link, ca_list;
     uint64_t heap, aq, uq, log, place, fq;
     uint64_t gauge, g_cpu, g_ram;        // gauge rows; node-component allocatable per slot
     uint32_t cap_fq;      // entries per delay-class ring (power of two; 0 = no rings)
     uint32_t pruned;      // 1: block bounds maintained, exact pruned scan where it applies
     uint32_t cap_heap, cap_aq, cap_uq, cap_act, cap_log, cap_place, cap_undo, rec_on;
-    uint32_t words_nodes, words_uids, words_group;
+    uint32_t words_nodes, words_uids, words_group, words_pods;
     uint32_t bshift;      // block = 2^bshift consecutive node indices (>= 64, <= 64 blocks)
     uint32_t nblocks;
     uint32_t cap_gauge;   // gauge rows per replica (0 = gauge recorder off)

@@ -66,12 +66,24 @@ def _gather(arr, group=None):
     return torch.cat(parts).cpu().numpy()
 
 
-def ensemble_summary(raw_results: Sequence, group=None) -> EnsembleSummary:
+def _collective(group, force: bool) -> bool:
+    """Run the cross-rank collective: always with more than one rank; with one rank only when
+    `force`d and a process group is initialised (so the RCCL path is exercised on one GPU)."""
+    n = _dist_group_size(group)
+    if n > 1:
+        return True
+    if not force:
+        return False
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
+def ensemble_summary(raw_results: Sequence, group=None, force: bool = False) -> EnsembleSummary:
     """Summary of every replica of the job (all ranks when torch.distributed is initialised; every
     rank must pass the same number of replicas).  Identical on every rank."""
     cnt, est, st = _rows(raw_results)
     hist = histogram_sum(raw_results)
-    if _dist_group_size(group) > 1:
+    if _collective(group, force):
         cnt, est, st = _gather(cnt, group), _gather(est, group), _gather(st, group)
         hist = _all_reduce_sum(hist, group)
     s = EnsembleSummary(COUNTER_NAMES, EST_NAMES)
@@ -100,9 +112,9 @@ def _all_reduce_sum(arr, group=None):
     return t.cpu().numpy()
 
 
-def max_over_ranks(values: Sequence[float], group=None, device: Optional[str] = None):
+def max_over_ranks(values: Sequence[float], group=None, device: Optional[str] = None, force: bool = False):
     """Element-wise max of a few scalars over the group (the bench's timing reduction)."""
-    if _dist_group_size(group) <= 1:
+    if not _collective(group, force):
         return list(values)
     import torch
     import torch.distributed as dist
@@ -112,11 +124,11 @@ def max_over_ranks(values: Sequence[float], group=None, device: Optional[str] = 
     return t.cpu().tolist()
 
 
-def sum_over_ranks(values: Sequence[int], group=None, device: Optional[str] = None):
+def sum_over_ranks(values: Sequence[int], group=None, device: Optional[str] = None, force: bool = False):
     """Element-wise sum of a u64 counter vector over the group (RCCL all-reduce on GPUs), in int64:
     exact for every count below 2^63 (a float64 sum would round above 2^53)."""
     vals = [int(v) for v in values]
-    if _dist_group_size(group) <= 1:
+    if not _collective(group, force):
         return vals
     import torch
     import torch.distributed as dist

@@ -219,6 +219,45 @@ def c4_parts(n_batch_pods: int = 400, seed: int = 7):
     return cfg, c, w
 
 
+# ---- C5 with the autoscalers live ------------------------------------------------------------
+CA_GROUPS_CONFIG_YAML = (("autoscaler_128cpu_256gb_node", 50, 128000, 274877906944),   # src/config.yaml:14-33
+                         ("autoscaler_64cpu_128gb_node", None, 64000, 137438953472))
+
+
+def c5_autoscaled_parts(n_nodes: int = 4096, n_pods: int = 16384, n_big: int = 600, arrival_window: float = 1200.0,
+                        seed: int = 2019, big_start: float = 300.0, big_window: float = 120.0):
+    """(config, cluster trace, workload trace) of the C5 sweep with its autoscaler axes live
+    (CA scale-down threshold and HPA tolerance over C3-shaped clusters).
+
+    * cluster: the C3 nodes (Alibaba-like machines, at most 128 GiB of RAM each);
+    * config: the cluster autoscaler of src/config.yaml:14-33 enabled (max_node_count 200; node
+      groups autoscaler_128cpu_256gb_node, max 50, and autoscaler_64cpu_128gb_node) and the HPA on;
+    * workload: n_pods - n_big Alibaba-like pods (c3_traces statistics) over `arrival_window`, a
+      burst of n_big pods of 16 cores / 180 GiB (135-225 GiB after seed perturbation) arriving over
+      [big_start, big_start + big_window] — they fit no trace node, only the 256-GiB template, so
+      they wait in the unscheduled cache, the CA scales that group up to its max and the Alibaba
+      pods that arrive meanwhile land on the new empty nodes (LeastAllocated); when the burst drains
+      the CA scales the nodes down once their remaining pods can be moved (scale_down) — and the
+      test_hpa.rs pod group (tests/test_hpa.rs:28-64) whose load cycle drives the HPA up and down.
+    """
+    cfg = SimulationConfig()
+    cfg.ca_enabled = True
+    cfg.ca_max_node_count = 200
+    cfg.ca_node_groups = [CANodeGroup(n, m, c, r) for n, m, c, r in CA_GROUPS_CONFIG_YAML]
+    cfg.hpa_enabled = True
+    cluster, small = c3_traces(n_nodes, n_pods - n_big, arrival_window, seed)
+    rng = random.Random(seed + 1)
+    w = GenericWorkloadTrace()
+    g = PodGroup("pod_group_1", 5, 100, Pod("pod_group_1", 100, 104857600, None), 0.6, None,
+                 UsageModel("pod_group", units=[(500.0, 8.0), (200.0, 2.0)]), None)
+    w.events.append(WorkloadEvent(59.5, "create_pod_group", pod_group=g))
+    w.events.extend(small.events)
+    for i in range(n_big):
+        t = float(int(big_start + rng.random() * big_window))
+        w.create_pod(t, Pod(f"batch_big_{i}", 16000, 180 << 30, float(rng.randint(200, 600))))
+    return cfg, cluster, w
+
+
 # ---- parameter sweep (C5) ---------------------------------------------------------------------
 def c5_params(defaults, n: int, base_seed: int = 123, replica_offset: int = 0):
     """Per-replica k10s_replica_params for the 65,536-replica sweep."""

@@ -149,3 +149,94 @@ def test_bench_world_size_mismatch_fails():
     p = _bench(["--gpus", "2", "--selftest-host", "--replicas", "1", "--nodes", "8", "--pods", "4", "--steps", "1",
                 "--warmup", "0", "--no-cpu-baseline"], {"WORLD_SIZE": "1", "RANK": "0"})
     assert p.returncode == 2 and "WORLD_SIZE=1" in p.stderr
+
+
+def test_launcher_builds_a_stale_library_once(tmp_path):
+    """bench.py --gpus 2 brings a stale engine library up to date in the launcher parent (hipcc only,
+    no GPU) before it spawns the ranks, so N ranks never compile into the same paths at once."""
+    lib = str(tmp_path / "libk10s.so")          # absent = stale
+    common = ["--selftest-host", "--nodes", "32", "--pods", "40", "--arrival-window", "30", "--steps", "1",
+              "--warmup", "0", "--no-cpu-baseline", "--replicas", "1"]
+    p = _bench(["--gpus", "2", *common], {"K10S_BUILD_OUT": lib})
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert p.stderr.count("[build] compiling") == 1, p.stderr[-2000:]
+    assert os.path.getsize(lib) > 0
+    assert not [f for f in os.listdir(tmp_path) if ".tmp" in f]   # published by rename
+    p2 = _bench(["--gpus", "2", *common], {"K10S_BUILD_OUT": lib})   # up to date now: no compile
+    assert p2.returncode == 0 and "[build] compiling" not in p2.stderr
+
+
+def _build_worker(out, q):
+    sys.path.insert(0, REPO)
+    import contextlib
+    import io
+    from kubernetriks_amd.build import build
+    err = io.StringIO()
+    with contextlib.redirect_stderr(err):
+        build(out=out)
+    q.put(err.getvalue())
+
+
+def test_concurrent_builds_compile_once(tmp_path):
+    """Three processes find the same library stale at once (ranks under torch.distributed.run): the
+    file lock lets one compile and the others reuse its result."""
+    out = str(tmp_path / "libk10s_race.so")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_build_worker, args=(out, q)) for _ in range(3)]
+    for p in procs:
+        p.start()
+    logs = [q.get(timeout=600) for _ in procs]
+    for p in procs:
+        p.join(60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert sum(s.count("[build] compiling") for s in logs) == 1, logs
+    import ctypes
+    lib = ctypes.CDLL(out)
+    assert lib.k10s_version
+
+
+_RCCL_ONE_RANK = r"""
+import os, sys
+sys.path[:0] = [{repo!r}, os.path.join({repo!r}, "tests")]
+import numpy as np, torch, torch.distributed as dist
+from kubernetriks_amd import ensemble, workloads as wl
+from kubernetriks_amd.native import Engine
+from kubernetriks_amd.scenario import SimulationConfig, scenario_text
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="{port}")
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+assert dist.get_backend() == "nccl"
+c, w = wl.c3_traces(n_nodes=64, n_pods=80, arrival_window=40.0, seed=4)
+scn = scenario_text(SimulationConfig(), c, w)
+params = ensemble.shard_params(Engine(scn, 1).default_params(), 6, 0, base_seed=9)
+eng = Engine(scn, 6, params=params)
+eng.run_until_all_finished(1e6)
+raw = eng.raw_results()
+a = ensemble.ensemble_summary(raw).as_dict()
+b = ensemble.ensemble_summary(raw, force=True).as_dict()       # all-gather + all-reduce over RCCL
+assert repr(a) == repr(b), (a, b)
+big = [2 ** 62 + 12345, 3, 0, 2 ** 53 + 1]
+assert ensemble.sum_over_ranks(big, force=True) == big           # int64 exact through RCCL
+assert ensemble.max_over_ranks([1.5, -2.0], force=True) == [1.5, -2.0]
+g = ensemble._gather(np.arange(12, dtype=np.int64).reshape(3, 4))
+assert g.tolist() == np.arange(12).reshape(3, 4).tolist()
+h = ensemble._all_reduce_sum(np.full((3, 32), 2 ** 40 + 7, dtype=np.int64))
+assert (h == 2 ** 40 + 7).all()
+dist.destroy_process_group()
+print("RCCL_ONE_RANK_OK", a["counters"]["placements"])
+"""
+
+
+@pytest.mark.gpu
+def test_rccl_collectives_one_rank_gpu():
+    """The nccl (= RCCL over xGMI) branches of ensemble._gather / _all_reduce_sum / sum_over_ranks /
+    max_over_ranks / ensemble_summary, forced on a one-rank group on the real GPU: they must give
+    exactly the local values (device tensors, int64 counters above 2^53)."""
+    import subprocess
+    code = _RCCL_ONE_RANK.format(repo=REPO, port=_free_port())
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0 and "RCCL_ONE_RANK_OK" in p.stdout, (p.stdout[-1000:], p.stderr[-3000:])

@@ -204,6 +204,45 @@ def test_stall_guard_stops_a_replica_that_cannot_finish(backend):
     assert h.results()[0]["status"] == "finished"
 
 
+@pytest.mark.parametrize("backend", ["host", pytest.param("gpu", marks=pytest.mark.gpu)])
+def test_stall_guard_waits_for_the_flush_under_conditional_move(backend):
+    """The conditional move (scheduler.rs:210-233) requeues after a pod finish only the waiting pods
+    that fit the resources that finish freed.  Pods of 6 and 4 CPU finish one after the other on a
+    10-CPU node: the waiting 8-CPU pod fits neither finish's budget, so it waits for the 300-s
+    flush (188-203) with only the periodic ticks pending.  The guard must not call that a stall:
+    the replica runs to RunUntilAllPodsAreFinished exactly like the oracle.  A pod that fits no
+    node at all still stalls it under the same flag."""
+    import oracle_bridge as ob
+    from kubernetriks_amd.scenario import GenericClusterTrace, Node, Pod
+    E = _engine(backend)
+    cfg = SimulationConfig(enable_unscheduled_pods_conditional_move=True)
+    cluster = GenericClusterTrace().create_node(0.0, Node("node_10cpu", 10000, 64 << 30))
+    for extra, want in ((None, "finished"), (Pod("pod_never_fits", 12000, 1 << 30, 30.0), "stalled")):
+        w = GenericWorkloadTrace()
+        w.create_pod(1.0, Pod("pod_a6", 6000, 8 << 30, 100.0))
+        w.create_pod(1.0, Pod("pod_b4", 4000, 8 << 30, 150.0))
+        w.create_pod(2.0, Pod("pod_c8", 8000, 8 << 30, 50.0))
+        if extra is not None:
+            w.create_pod(3.0, extra)
+        scn = scenario_text(cfg, cluster, w)
+        caps = parity.parity_caps(log=True)
+        caps.stall_guard = 1
+        eng = E(scn, 1, caps=caps)
+        eng.run_until_all_finished(1e5)
+        r = eng.results()[0]
+        assert r["status"] == want, r["status"]
+        assert r["counters"]["requeued"] >= 1 and r["counters"]["flushed"] >= 1
+        if want == "finished":
+            o = ob.OracleSim(scn, log=True)
+            st = o.run_until_all_finished(1e5)
+            od = o.result(placements=True, log=True)
+            od["status_name"] = parity.ORACLE_STATUS[st]
+            assert parity.compare(od, eng) == []
+            assert r["counters"]["pods_succeeded"] == 3
+        else:
+            assert r["counters"]["pods_succeeded"] == 3 and r["time"] < 2000.0
+
+
 def test_perturb_blob_matches_perturb_pod():
     import math
     from kubernetriks_amd.scenario import Pod
