@@ -1,13 +1,24 @@
 #!/usr/bin/env python3
 """Benchmark: pod placements/sec of the MI355X batched-ensemble engine on 4k-node clusters.
 
-Workloads (BASELINE.json configs[2] shape, the metric's "4k-node clusters"):
-  c3          every GPU runs R replicas (default 8,192) of a 4,096-node Alibaba-like cluster, each a
-              seed-perturbed copy of one synthetic 16,384-pod Alibaba-like trace (integer arrival
-              seconds, notebook statistics); light load, every attempt places its pod.
-  c3_backlog  the same cluster under load (rho ~ 1 of the RAM-bound capacity):
-              pods of 0.3-0.5 of a node's RAM staying ~1,200 s, so attempts fail, pods wait in the
-              unschedulable map, are moved back on every pod finish and flushed after 300 s.
+Workloads (BASELINE.json configs[2] and [4] shapes, the metric's "4k-node clusters"):
+  c3             every GPU runs R replicas (default 8,192) of a 4,096-node Alibaba-like cluster, each
+                 a seed-perturbed copy of one synthetic 16,384-pod Alibaba-like trace (integer arrival
+                 seconds, notebook statistics); light load (rho ~ 0.007 of the RAM-bound capacity:
+                 ~2,600 concurrent pods on room for ~360 k), every attempt places its pod.
+  c3_backlog     the same cluster under load (rho ~ 1.1 of the RAM-bound capacity):
+                 pods of 0.3-0.5 of a node's RAM staying ~1,500 s, so attempts fail, pods wait in the
+                 unschedulable map and are moved back to the action queue on every pod finish
+                 (move-all: the conditional move is off, so the 300-s flush rarely finds an entry).
+  c5             BASELINE configs[4]: the c3 replicas with the scheduler-parameter sweep of
+                 workloads.c5_params (cycle interval x conditional move x network delays x CA
+                 threshold x HPA tolerance; replica r of the job gets cell r), weak-scaled over the
+                 ranks (8 x 8,192 = 65,536 replicas on 8 GPUs).  The c3 cluster has no autoscaler,
+                 so the last two axes are inert here: see c5_autoscaled.
+  c5_autoscaled  the same sweep over workloads.c5_autoscaled_parts: the 4,096-node cluster with the
+                 cluster autoscaler of src/config.yaml:14-33 and the test_hpa pod group live, 16,384
+                 pods of which 48 need the CA's 256-GiB template, in two bursts (the CA scales up for
+                 each and back down when they drain).
 A step simulates every replica from initialize() until RunUntilAllPodsAreFinished stops it.
 Replicas are sharded over ranks with distinct seeds (weak scaling: R per GPU); nothing is exchanged
 while they run; at the end one RCCL all-reduce of the int64 counter vector (+ the estimator rows and
@@ -52,7 +63,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=("c3", "c3_backlog"), default="c3")
+    ap.add_argument("--workload", choices=("c3", "c3_backlog", "c5", "c5_autoscaled"), default="c3")
     ap.add_argument("--replicas", type=int, default=8192, help="replicas per GPU")
     ap.add_argument("--nodes", type=int, default=4096)
     ap.add_argument("--pods", type=int, default=16384)
@@ -150,10 +161,10 @@ def cpu_worker(args_tuple):
 def cpu_baseline(args, cfg, cluster, workload, params):
     from multiprocessing import get_context
     from kubernetriks_amd import workloads as wl
-    from kubernetriks_amd.scenario import scenario_text
     usable, cores_info = host_cores()
     workers = args.cpu_workers or usable
-    jobs = [(scenario_text(cfg, cluster, wl.perturb_workload(workload, params[i % len(params)].seed)), args.cpu_seconds)
+    # replica i's own scenario: its parameter cell (sweeps) and its seed-perturbed trace
+    jobs = [(wl.replica_scenario(cfg, cluster, workload, params[i % len(params)]), args.cpu_seconds)
             for i in range(workers)]
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_bridge as ob
@@ -182,17 +193,36 @@ def cpu_baseline(args, cfg, cluster, workload, params):
 
 # ---- the measurement ------------------------------------------------------------------------------
 def build_workload(args):
+    """(config, cluster trace, workload trace, description, sweep) of the selected workload."""
     from kubernetriks_amd import workloads as wl
+    from kubernetriks_amd.scenario import SimulationConfig
+    cfg, sweep = SimulationConfig(), False
     if args.workload == "c3_backlog":
         cluster, workload = wl.c3_backlog_traces(args.nodes, args.pods, args.arrival_window)
         desc = (f"C3 backlog: {args.replicas} replicas/GPU x {args.nodes}-node Alibaba-like cluster, {args.pods} pods/replica "
-                "of 0.3-0.5 node RAM for ~1200 s (rho ~ 1: failed attempts, unschedulable map, move-all on pod "
-                "finish, 300-s flush), run until all pods finished (RunUntilAllPodsAreFinished)")
+                "of 0.3-0.5 node RAM for ~1500 s (rho ~ 1.1 of the RAM-bound capacity: failed attempts, unschedulable "
+                "map, move-all on every pod finish; conditional move off), run until all pods finished "
+                "(RunUntilAllPodsAreFinished)")
+    elif args.workload == "c5_autoscaled":
+        cfg, cluster, workload = wl.c5_autoscaled_parts(args.nodes, args.pods, arrival_window=args.arrival_window)
+        sweep = True
+        desc = (f"C5 sweep with autoscalers live: {args.replicas} replicas/GPU x {args.nodes}-node Alibaba-like cluster + "
+                "cluster autoscaler (config.yaml:14-33, max 200 nodes) + HPA pod group (test_hpa.rs), "
+                f"{args.pods} pods/replica (48 that only the CA's 256-GiB template fits, in two bursts); replica r of the job runs "
+                "cell r of workloads.c5_params (cycle interval {1,5,10,30} x conditional move {F,T} x delays "
+                "x{0.5,1,2} x CA threshold {0.3,0.5,0.7} x HPA tolerance {0.05,0.1,0.2}); run until all pods finished")
     else:
         cluster, workload = wl.c3_traces(args.nodes, args.pods, args.arrival_window)
-        desc = (f"C3: {args.replicas} replicas/GPU x {args.nodes}-node Alibaba-like cluster, {args.pods} pods/replica, "
-                "run until all pods finished (RunUntilAllPodsAreFinished)")
-    return cluster, workload, desc
+        if args.workload == "c5":
+            sweep = True
+            desc = (f"C5 sweep: {args.replicas} replicas/GPU x {args.nodes}-node Alibaba-like cluster, {args.pods} "
+                    "pods/replica (the c3 trace, rho ~ 0.007); replica r of the job runs cell r of workloads.c5_params "
+                    "(cycle interval x conditional move x delays live; CA threshold / HPA tolerance inert without "
+                    "autoscalers: see c5_autoscaled); run until all pods finished")
+        else:
+            desc = (f"C3: {args.replicas} replicas/GPU x {args.nodes}-node Alibaba-like cluster, {args.pods} pods/replica "
+                    "(rho ~ 0.007 of the RAM-bound capacity), run until all pods finished (RunUntilAllPodsAreFinished)")
+    return cfg, cluster, workload, desc, sweep
 
 
 def main():
@@ -236,15 +266,15 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    cfg = SimulationConfig()
-    cluster, workload, desc = build_workload(args)
+    cfg, cluster, workload, desc, sweep = build_workload(args)
     # cluster trace as text, the create_pod events as the binary block (k10s_engine_create_bulk)
     scn, blob = scenario_bulk(cfg, cluster, workload)
     R = args.replicas
     probe = make_engine(scn, 1, blob=blob)
     defaults = probe.default_params()
     del probe
-    params = ensemble.shard_params(defaults, R, rank, base_seed=123, perturb=True)  # replicas [rank*R, (rank+1)*R)
+    # replicas [rank*R, (rank+1)*R) of the job: seed-perturbed copies, or sweep cells (C5)
+    params = ensemble.shard_params(defaults, R, rank, base_seed=123, perturb=True, sweep=sweep)
     t = time.perf_counter()
     caps = Capacities()
     caps.pruned_scan = 1 if args.pruned_scan else 0
@@ -404,7 +434,7 @@ def backlog_line(args, cfg, make_engine, caps, ensemble, num_counters, version):
     from kubernetriks_amd.scenario import scenario_bulk
     b = argparse.Namespace(**vars(args))
     b.workload = "c3_backlog"
-    cluster, workload, desc = build_workload(b)
+    cfg, cluster, workload, desc, _ = build_workload(b)
     scn, blob = scenario_bulk(cfg, cluster, workload)
     probe = make_engine(scn, 1, blob=blob)
     defaults = probe.default_params()

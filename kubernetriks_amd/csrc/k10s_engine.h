@@ -245,6 +245,8 @@ enum : int {
     FQ_AS_TO_HPA = 6,
     FQ_NOW = 7,          // emit_now (delay 0)
 };
+// The other two event sources: the shared trace stream and the heap.
+enum : int { SRC_TRACE = K10S_NFQ, SRC_HEAP = K10S_NFQ + 1 };
 
 // Heap position i: the top K10S_HEAP_TOP positions (levels 0-1; 0-2 for arity 8) are in the working
 // header, the rest in the replica's HBM heap array.  Level boundaries coincide with K10S_HEAP_TOP,
@@ -298,6 +300,9 @@ K10S_HD void heap_put(Ctx& c, uint32_t i, const HeapEv& e) {
 }
 #endif
 
+// An emission changed source q's head: mark it for the source list.
+K10S_HD void sl_mark(RepHdr& H, uint32_t q) { H.sl_dirty |= 1u << q; }
+
 K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uint32_t a, uint32_t b, double x,
                           int cls = FQ_HEAP) {
     RepHdr& H = c.H();
@@ -329,10 +334,6 @@ K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uin
     e.b = b;
     e.x = x;
     const int64_t k = total_key(e.time);
-    if (k < H.emit_kmin) {  // run continuation bound (continue_source); ids grow, so the first
-        H.emit_kmin = k;    // emission at a time key is the smallest (key, id) there
-        H.emit_smin = seq;
-    }
     if (cls >= 0 && cap) {
         if (tl - hd < cap && (tl == hd || k >= total_key(last))) {
             if (we == tl && tl - hd < K10S_FQW) {  // the window holds the whole ring: append
@@ -341,7 +342,10 @@ K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uin
             } else {
                 c.V().fq()[(uint32_t)cls * cap + (tl & (cap - 1))] = e;
             }
-            if (tl == hd) H.fq_top[cls] = e;
+            if (tl == hd) {  // the ring was empty: this event is its new head (source list update)
+                H.fq_top[cls] = e;
+                sl_mark(H, (uint32_t)cls);
+            }
             H.fq_tail[cls] = tl + 1;
             H.fq_last[cls] = e.time;
             H.next_seq = e.seq + 1;
@@ -365,7 +369,10 @@ K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uin
         pos = parent;
     }
     heap_put(c, pos, e);
-    if (pos == 0) H.heap_top = e;
+    if (pos == 0) {  // a new heap root (source list update)
+        H.heap_top = e;
+        sl_mark(H, SRC_HEAP);
+    }
     return e.seq;
 }
 K10S_HD uint32_t emit0(Ctx& c, uint32_t kind, double delay) { return emit(c, kind, delay, -1, 0, 0, 0.0); }
@@ -2691,187 +2698,107 @@ K10S_HD void init_replica(Ctx& c) {
 }
 
 // ---- event-queue merge -------------------------------------------------------------------------
-enum : int { SRC_TRACE = K10S_NFQ, SRC_HEAP = K10S_NFQ + 1 };
 
-// Which source holds the minimum (time, id): a FIFO class 0..K10S_NFQ-1, SRC_TRACE, SRC_HEAP, or
-// -1 when all are empty; also the minimum (k2, s2) over the OTHER sources (run continuation).
-// Device: lanes 0..7 hold the FIFO heads, lane 8 the trace head, lane 9 the heap root; a 4-step
-// DPP min of the 64-bit time keys over the 16-lane row, then the id minimum among the lanes at that
-// key (ids are unique, so it names one lane = the source), then the same two steps again with
-// that lane masked for the runner-up.
-#if K10S_DEVICE
-template <int S>
-K10S_D int64_t kmin_step(int64_t k) {
-    uint32_t la, lb, ha, hb;
-    xpair<S>((uint32_t)(uint64_t)k, la, lb);
-    xpair<S>((uint32_t)((uint64_t)k >> 32), ha, hb);
-    const int64_t ka = (int64_t)join64(la, ha), kb = (int64_t)join64(lb, hb);
-    return kb < ka ? kb : ka;
-}
-template <int S>
-K10S_D uint32_t umin_step(uint32_t v) {
-    uint32_t a, b;
-    xpair<S>(v, a, b);
-    return a < b ? a : b;
-}
-K10S_D int64_t row16_kmin(int64_t k) {
-    k = kmin_step<0>(k);
-    k = kmin_step<1>(k);
-    k = kmin_step<2>(k);
-    k = kmin_step<3>(k);
-    const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)k);
-    const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)k >> 32));
-    return (int64_t)(lo | (hi << 32));
-}
-K10S_D uint32_t row16_umin(uint32_t v) {
-    v = umin_step<0>(v);
-    v = umin_step<1>(v);
-    v = umin_step<2>(v);
-    v = umin_step<3>(v);
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-}
-#endif
-#ifndef K10S_SELECT_SPLIT
-#define K10S_SELECT_SPLIT 0   // 1: 32-bit row minima for the source selection (0.3-0.6 % slower, r02_v11)
-#endif
-K10S_HD int next_source(Ctx& c, uint32_t ntr, int64_t& k2, uint32_t& s2) {
+// The sorted source list.  Every event source keeps its own events in (time, id) order — a
+// delay-class FIFO ring is a sorted run, the heap has its root, the trace stream its cursor — so the
+// next event is the smallest of at most K10S_NSRC source heads.  The header keeps those heads sorted
+// (sl[0, sl_n), non-empty sources only) and updates the list exactly where a head changes: after
+// the consumed source advances, and after an emission into an empty ring or to a new heap root
+// (emit marks those in sl_dirty).  The next event is then simply sl[0] — no selection over the
+// sources per event (round 2 ran a 16-lane DPP minimum over all heads whenever the previous
+// source's next head did not precede the runner-up: 53 % of the events at C3, measured by a shadow
+// of this list on the host build, profiles/r03_selection_policy_sim.json).
+K10S_HD bool sl_less(int64_t ka, uint32_t sa, int64_t kb, uint32_t sb) { return ka < kb || (ka == kb && sa < sb); }
+
+// Current head (time key, id) of source q; false if q is empty.
+K10S_HD bool src_head(Ctx& c, uint32_t q, uint32_t ntr, int64_t& k, uint32_t& s) {
     const RepHdr& H = c.H();
-    const int64_t KMAX = 0x7FFFFFFFFFFFFFFFll;
-#if K10S_DEVICE
-    // every lane reads its candidate's fields in one batch of LDS reads (no branch in between), then
-    // masks invalid candidates: one LDS round trip per selection
-    const int lane = lane_id() & 15;
-    const uint32_t li = lane < K10S_NFQ ? (uint32_t)lane : 0u;
-    const uint32_t qh = H.fq_head[li], qt = H.fq_tail[li], qseq = H.fq_top[li].seq;
-    const double qtime = H.fq_top[li].time;
-    const uint32_t hs = H.heap_size, hseq = H.heap_top.seq;
-    const double htime = H.heap_top.time;
-    const uint32_t cur = H.trace_cursor, tseq = H.tr_seq;
-    const double ttime = H.tr_time;
-    bool valid = false;
-    double t = 0.0;
-    uint32_t sq = 0xFFFFFFFFu;
-    if (lane < K10S_NFQ) {
-        valid = qh != qt;
-        t = qtime;
-        sq = qseq;
-    } else if (lane == SRC_HEAP) {
-        valid = hs > 0;
-        t = htime;
-        sq = hseq;
-    } else if (lane == SRC_TRACE) {
-        valid = cur < ntr;
-        t = ttime;
-        sq = tseq;
+    if (q < (uint32_t)K10S_NFQ) {
+        const uint32_t hd = H.fq_head[q], tl = H.fq_tail[q];
+        k = total_key(H.fq_top[q].time);
+        s = H.fq_top[q].seq;
+        return hd != tl;
     }
-    int64_t k = valid ? total_key(t) : KMAX;
-    sq = valid ? sq : 0xFFFFFFFFu;
-#if K10S_SELECT_SPLIT
-    // The (key, id) minimum as three 32-bit row minima (fused v_min_u32 DPP steps): the biased key's
-    // high word, its low word among the lanes at that high word, the id among the lanes at that key;
-    // then the same three with the winning lane masked for the runner-up.  Biasing the int64 key by
-    // 2^63 makes its unsigned order the signed order, so the result is the 64-bit one bit for bit.
-    const uint64_t uk = (uint64_t)k ^ 0x8000000000000000ull;
-    const uint32_t kh = (uint32_t)(uk >> 32), kl = (uint32_t)uk;
-    const uint32_t mh = row16_umin(kh);
-    const uint32_t ml = row16_umin(kh == mh ? kl : 0xFFFFFFFFu);
-    if (mh == 0xFFFFFFFFu && ml == 0xFFFFFFFFu) {   // every key is KMAX: nothing pending
-        k2 = KMAX;
-        s2 = 0xFFFFFFFFu;
-        return -1;
+    if (q == (uint32_t)SRC_TRACE) {
+        k = total_key(H.tr_time);
+        s = H.tr_seq;
+        return H.trace_cursor < ntr;
     }
-    const bool at_min = kh == mh && kl == ml;
-    const uint32_t smin = row16_umin(at_min ? sq : 0xFFFFFFFFu);
-    const uint64_t win = __ballot(lane_id() < 16 && at_min && sq == smin) & 0xFFFFull;
-    const int src = (int)__builtin_ctzll(win);
-    const bool other = lane != src;
-    const uint32_t oh = other ? kh : 0xFFFFFFFFu, ol = other ? kl : 0xFFFFFFFFu;
-    const uint32_t mh2 = row16_umin(oh);
-    const uint32_t ml2 = row16_umin(oh == mh2 ? ol : 0xFFFFFFFFu);
-    k2 = (int64_t)((((uint64_t)mh2 << 32) | ml2) ^ 0x8000000000000000ull);
-    s2 = k2 == KMAX ? 0xFFFFFFFFu : row16_umin(oh == mh2 && ol == ml2 ? sq : 0xFFFFFFFFu);
-    return src;
-#else
-    const int64_t kmin = row16_kmin(k);
-    if (kmin == KMAX) {
-        k2 = KMAX;
-        s2 = 0xFFFFFFFFu;
-        return -1;
-    }
-    const uint32_t smin = row16_umin(k == kmin ? sq : 0xFFFFFFFFu);
-    const uint64_t win = __ballot(lane < 16 && k == kmin && sq == smin) & 0xFFFFull;
-    const int src = (int)__builtin_ctzll(win);
-    // the runner-up among the other sources
-    const bool other = lane != src;
-    const int64_t ko = other ? k : KMAX;
-    k2 = row16_kmin(ko);
-    s2 = k2 == KMAX ? 0xFFFFFFFFu : row16_umin(ko == k2 ? sq : 0xFFFFFFFFu);
-    return src;
-#endif
-#else
-    int64_t kk[K10S_NFQ + 2];
-    uint32_t ss[K10S_NFQ + 2];
-    for (int q = 0; q < K10S_NFQ + 2; q++) {
-        kk[q] = KMAX;
-        ss[q] = 0xFFFFFFFFu;
-    }
-    for (int q = 0; q < K10S_NFQ; q++)
-        if (H.fq_head[q] != H.fq_tail[q]) {
-            kk[q] = total_key(H.fq_top[q].time);
-            ss[q] = H.fq_top[q].seq;
-        }
-    if (H.trace_cursor < ntr) {
-        kk[SRC_TRACE] = total_key(H.tr_time);
-        ss[SRC_TRACE] = H.tr_seq;
-    }
-    if (H.heap_size > 0) {
-        kk[SRC_HEAP] = total_key(H.heap_top.time);
-        ss[SRC_HEAP] = H.heap_top.seq;
-    }
-    int src = -1;
-    for (int q = 0; q < K10S_NFQ + 2; q++)
-        if (kk[q] != KMAX && (src < 0 || kk[q] < kk[src] || (kk[q] == kk[src] && ss[q] < ss[src]))) src = q;
-    k2 = KMAX;
-    s2 = 0xFFFFFFFFu;
-    for (int q = 0; q < K10S_NFQ + 2; q++)
-        if (q != src && kk[q] != KMAX && (kk[q] < k2 || (kk[q] == k2 && ss[q] < s2))) {
-            k2 = kk[q];
-            s2 = ss[q];
-        }
-    return src;
-#endif
+    k = total_key(H.heap_top.time);
+    s = H.heap_top.seq;
+    return H.heap_size > 0;
 }
 
-// Run continuation: after an event of source `src`, its next event is the global minimum without a
-// full selection when it precedes (a) the runner-up of the last full selection — the other
-// sources' heads change only by emissions — and (b) every event emitted since (those carry larger
-// ids, so an equal time still comes after).  Returns the source or -1 (do a full selection).
-K10S_HD int continue_source(Ctx& c, uint32_t ntr) {
-    const RepHdr& H = c.H();
-    const uint32_t src = H.cont_src;
-    const int64_t k2 = H.cont_k2, ek = H.emit_kmin;
-    const uint32_t s2 = H.cont_s2, es = H.emit_smin;
-    double t;
-    uint32_t sq;
-    if (src < (uint32_t)K10S_NFQ) {
-        if (H.fq_head[src] == H.fq_tail[src]) return -1;
-        t = H.fq_top[src].time;
-        sq = H.fq_top[src].seq;
-    } else if (src == (uint32_t)SRC_TRACE) {
-        if (H.trace_cursor >= ntr) return -1;
-        t = H.tr_time;
-        sq = H.tr_seq;
-    } else if (src == (uint32_t)SRC_HEAP) {
-        if (H.heap_size == 0) return -1;
-        t = H.heap_top.time;
-        sq = H.heap_top.seq;
-    } else {
-        return -1;
+// Replace source q's entry by its new head (key, seq), or drop it (has == false).  Device: one
+// 16-B LDS read per lane (lane i = entry i), the new positions from two ballots, one scattered
+// 16-B write per kept entry and one for the new entry: no serial walk.
+K10S_HD void sl_update(Ctx& c, uint32_t q, bool has, int64_t key, uint32_t seq) {
+    RepHdr& H = c.H();
+#if K10S_DEVICE
+    const uint32_t n = uniform_u32(H.sl_n);
+    const uint32_t lane = (uint32_t)lane_id();
+    SrcEnt E;
+    E.key = 0x7FFFFFFFFFFFFFFFll;
+    E.seq = 0xFFFFFFFFu;
+    E.src = 0xFFFFFFFFu;
+    if (lane < n) E = H.sl[lane];
+    const bool keep = lane < n && E.src != q;
+    const bool less = keep && sl_less(E.key, E.seq, key, seq);
+    const uint64_t mk = __ballot(keep);
+    const uint32_t p = (uint32_t)__popcll(__ballot(less));   // the new entry's index
+    const uint32_t before = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+    const uint32_t idx = before + ((has && !less) ? 1u : 0u);
+    if (keep) H.sl[idx] = E;
+    if (has && lane == 0) {
+        SrcEnt N;
+        N.key = key;
+        N.seq = seq;
+        N.src = q;
+        H.sl[p] = N;
     }
-    const int64_t k = total_key(t);
-    if (k > ek || (k == ek && sq > es)) return -1;   // an emitted event comes first
-    if (k < k2 || (k == k2 && sq < s2)) return (int)src;
-    return -1;
+    H.sl_n = (uint32_t)__popcll(mk) + (has ? 1u : 0u);
+#else
+    uint32_t n = H.sl_n, w = 0;
+    for (uint32_t i = 0; i < n; i++)
+        if (H.sl[i].src != q) H.sl[w++] = H.sl[i];
+    n = w;
+    if (has) {
+        uint32_t i = n;
+        while (i > 0 && sl_less(key, seq, H.sl[i - 1].key, H.sl[i - 1].seq)) {
+            H.sl[i] = H.sl[i - 1];
+            i--;
+        }
+        H.sl[i].key = key;
+        H.sl[i].seq = seq;
+        H.sl[i].src = q;
+        n++;
+    }
+    H.sl_n = n;
+#endif
+}
+K10S_HD void sl_refresh(Ctx& c, uint32_t q, uint32_t ntr) {
+    int64_t k;
+    uint32_t s;
+    const bool has = src_head(c, q, ntr, k, s);
+    sl_update(c, q, has, uniform_u64((uint64_t)k), uniform_u32(s));
+}
+// Apply the head changes emissions made since the last update.
+K10S_HD void sl_apply_dirty(Ctx& c, uint32_t ntr) {
+    uint32_t d = uniform_u32(c.H().sl_dirty);
+    if (!d) return;
+    c.H().sl_dirty = 0;
+    do {
+        const uint32_t q = (uint32_t)__builtin_ctz(d);
+        d &= d - 1;
+        sl_refresh(c, q, ntr);
+    } while (d);
+}
+// Build the list from scratch (start of a launch: the header may come from anywhere).
+K10S_HD void sl_rebuild(Ctx& c, uint32_t ntr) {
+    c.H().sl_n = 0;
+    c.H().sl_dirty = 0;
+    for (uint32_t q = 0; q < (uint32_t)K10S_NSRC; q++) sl_refresh(c, q, ntr);
 }
 
 // Refill a drained delay-class window from the HBM ring: positions [hd, hd + min(W, tail - hd)),
@@ -2887,26 +2814,43 @@ K10S_HD void fq_refill(Ctx& c, int cls, uint32_t hd) {
     H.fq_wend[cls] = hd + n;
 }
 
-// Remove the event next_source selected; a FIFO takes its next head from its window.
-K10S_HD void consume_source(Ctx& c, int src) {
+// Remove the head event of source src (sl[0]) and move the source's entry in the source list to
+// its new head; a FIFO takes its next head from its window.
+K10S_HD void consume_source(Ctx& c, int src, uint32_t ntr) {
     RepHdr& H = c.H();
+    bool has;
+    int64_t key = 0;
+    uint32_t seq = 0;
     if (src == SRC_TRACE) {
         const uint32_t cur = H.trace_cursor + 1;
         H.trace_cursor = cur;
-        trace_head_load(c, cur);
+        has = cur < ntr;
+        if (has) {
+            const double t = c.S().trace[cur].time;
+            seq = c.S().trace[cur].seq;
+            H.tr_time = t;
+            H.tr_seq = seq;
+            key = total_key(t);
+        }
     } else if (src == SRC_HEAP) {
         const uint64_t t_hp = prof_now();
         heap_pop(c);
         K10S_PROF_ADD(c, PROF_HEAPPOP, t_hp);
         K10S_PROF_COUNT(c, PROF_NHEAPPOP);
+        has = src_head(c, SRC_HEAP, ntr, key, seq);
     } else {
-        const uint32_t hd = H.fq_head[src] + 1;
+        const uint32_t hd = H.fq_head[src] + 1, tl = H.fq_tail[src], we = H.fq_wend[src];
         H.fq_head[src] = hd;
-        if (hd != H.fq_tail[src]) {
-            if (hd == H.fq_wend[src]) fq_refill(c, src, hd);
-            H.fq_top[src] = H.fq_win[(uint32_t)src * K10S_FQW + (hd & (K10S_FQW - 1))];
+        has = hd != tl;
+        if (has) {
+            if (hd == we) fq_refill(c, src, hd);
+            const HeapEv t = H.fq_win[(uint32_t)src * K10S_FQW + (hd & (K10S_FQW - 1))];
+            H.fq_top[src] = t;
+            key = total_key(t.time);
+            seq = t.seq;
         }
     }
+    sl_update(c, (uint32_t)src, has, uniform_u64((uint64_t)key), uniform_u32(seq));
 }
 
 // Does some node of the scheduler cache fit a (cpu, ram) request (Fit::filter, plugin.rs:34-45)?
@@ -2954,9 +2898,6 @@ K10S_HD bool replica_stalled(Ctx& c) {
 }
 
 // ---- the event loop -----------------------------------------------------------------------------
-#ifndef K10S_CONTINUE
-#define K10S_CONTINUE 1   // run continuation (continue_source); 0 = a full selection per event
-#endif
 // Wave priorities (s_setprio) so that the replicas of one SIMD drain together.  The instruction
 // arbiter prefers the oldest wave among equal priorities, so with 8 identical replicas per SIMD the
 // oldest finished at 63 % of the launch and the youngest at 100 % (tools/wall_spread.py,
@@ -3042,9 +2983,8 @@ K10S_HD void fair_priority(uint64_t done) {
 K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, uint64_t budget) {
     RepHdr* h = &c.H();
     if (h->status != K10S_REPLICA_RUNNING) return 0;
-        h->cur_kind = 0xFFFF;
+    h->cur_kind = 0xFFFF;
     h->cur_seq = 0;
-    h->cont_src = 0xFFFFFFFFu;  // the first event of a launch takes a full selection
     // launch constants are re-read at each use (scalar loads through the opaque constant pointer)
     // rather than held in SGPRs across the loop, where they are spilled around the handler calls
 #define total_pods (c.S().total_pods_in_trace)
@@ -3067,30 +3007,23 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
     int more = 0;
     uint32_t status = K10S_REPLICA_RUNNING;
     const uint64_t t_loop = prof_now();
+    sl_rebuild(c, ntr);  // the sorted source list, from the sources' heads
     while (!h->error_code) {
         if (!until_mode() && h->counters[K10S_C_TERMINATED_PODS] >= total_pods &&
             is_multiple_of_1000(h->clock)) {
             status = K10S_REPLICA_FINISHED;
             break;
         }
-        // next non-canceled event: the minimum (time, id) over the shared trace stream, the heap
-        // root and the heads of the delay-class FIFOs (all cached: LDS / scalar cache)
+        // next non-canceled event: the head of the first source in the source list (the minimum
+        // (time, id) over the shared trace stream, the heap root and the delay-class FIFO heads)
         HeapEv e;
         int src = 0;
         bool have = false;
         const uint64_t t_sel = prof_now();
+        sl_apply_dirty(c, ntr);
         for (;;) {
-            src = K10S_CONTINUE ? continue_source(c, ntr) : -1;
-            if (src < 0) {
-                int64_t k2;
-                uint32_t s2;
-                src = next_source(c, ntr, k2, s2);
-                h->cont_k2 = k2;
-                h->cont_s2 = s2;
-                h->emit_kmin = 0x7FFFFFFFFFFFFFFFll;
-            }
-            h->cont_src = (uint32_t)src;
-            if (src < 0) break;
+            if (uniform_u32(h->sl_n) == 0) break;
+            src = (int)uniform_u32(h->sl[0].src);
             if (src == SRC_TRACE) {
                 const uint32_t cur = h->trace_cursor;
                 const uint32_t tk = c.S().trace[cur].kind, ta = c.S().trace[cur].arg;
@@ -3109,6 +3042,7 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
                 e = h->heap_top;
                 if (e.kind == K10S_EV_N_POD_FINISHED && c.V().pod(e.a).finish_seq != e.seq) {  // canceled
                     heap_pop(c);
+                    sl_refresh(c, SRC_HEAP, ntr);
                     continue;
                 }
             } else {
@@ -3134,7 +3068,7 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
             break;
         }
         const uint64_t t_con = prof_now();
-        consume_source(c, src);
+        consume_source(c, src, ntr);
         K10S_PROF_ADD(c, PROF_CONSUME, t_con);
         h->clock = e.time;
         h->cur_kind = e.kind;

@@ -83,6 +83,7 @@ __global__ K10S_RUN_BOUNDS void k10s_run_kernel(uint32_t n_replicas, int mode, d
     hdr_copy((uint32_t*)&k10s_hdr, hdr_global(r));
     Ctx c;
     int more = run_replica(c, mode, until_time, max_time, budget);
+    (void)more;
 #if K10S_WALL
     if (threadIdx.x == 0) {
         k10s_hdr.prof[0] = w0;

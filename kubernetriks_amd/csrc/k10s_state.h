@@ -139,6 +139,13 @@ struct HeapEv {             // dslab Event {id, time, dst, data}, 32 B
 // Delay-class FIFOs of the event queue (k10s_engine.h): events emitted with the same constant
 // delay are emitted in (time, id) order, so each class is an already-sorted run.
 #define K10S_NFQ 8
+#define K10S_NSRC (K10S_NFQ + 2)   // the FIFO classes, the trace stream, the heap
+// One entry of the sorted source list: the head (time key, id) of event source `src`.
+struct SrcEnt {
+    int64_t key;
+    uint32_t seq;
+    uint32_t src;
+};
 // The head of every delay-class ring lives in the working header (LDS on the device): ring
 // positions [fq_head, fq_wend) are held in a K10S_FQW-entry window, the rest in the HBM ring, and a
 // drained window is refilled K10S_FQW entries at a time by one lane-parallel load.
@@ -221,13 +228,11 @@ struct RepHdr {
     HeapEv heap_top;
     double tr_time;               // cached head of the shared trace stream (valid while
     uint32_t tr_seq, tr_pad;      // trace_cursor < n_trace)
-    // run continuation (k10s_engine.h run_replica): the smallest (time key, id) among the sources
-    // other than the last selected one, as of the last full selection, and the smallest time key
-    // emitted since then
-    int64_t cont_k2;
-    uint32_t cont_s2, cont_src;
-    int64_t emit_kmin;            // (time key, id) of the smallest event emitted since
-    uint32_t emit_smin;
+    // the event sources' heads in (time, id) order (k10s_engine.h "source list"): entries
+    // [0, sl_n) are the non-empty sources, sl[0] holds the next event; sl_dirty marks sources whose
+    // head an emission changed (an empty ring got its first entry, a new heap root)
+    SrcEnt sl[K10S_NSRC];
+    uint32_t sl_n, sl_dirty;
     uint32_t unsched_missing;     // PS unscheduled-pod cache entries whose pod left storage (PF_UNSCHED
                                   // without PF_IN_PS): scale_up_info would panic on them
                                   // (persistent_storage.rs:137-145)

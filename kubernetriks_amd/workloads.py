@@ -224,22 +224,28 @@ CA_GROUPS_CONFIG_YAML = (("autoscaler_128cpu_256gb_node", 50, 128000, 2748779069
                          ("autoscaler_64cpu_128gb_node", None, 64000, 137438953472))
 
 
-def c5_autoscaled_parts(n_nodes: int = 4096, n_pods: int = 16384, n_big: int = 600, arrival_window: float = 1200.0,
-                        seed: int = 2019, big_start: float = 300.0, big_window: float = 120.0):
+def c5_autoscaled_parts(n_nodes: int = 4096, n_pods: int = 16384, n_big: Optional[int] = None,
+                        arrival_window: float = 1200.0, seed: int = 2019, big_start: float = 300.0,
+                        big_window: float = 60.0, big_gap: float = 600.0):
     """(config, cluster trace, workload trace) of the C5 sweep with its autoscaler axes live
     (CA scale-down threshold and HPA tolerance over C3-shaped clusters).
 
     * cluster: the C3 nodes (Alibaba-like machines, at most 128 GiB of RAM each);
     * config: the cluster autoscaler of src/config.yaml:14-33 enabled (max_node_count 200; node
       groups autoscaler_128cpu_256gb_node, max 50, and autoscaler_64cpu_128gb_node) and the HPA on;
-    * workload: n_pods - n_big Alibaba-like pods (c3_traces statistics) over `arrival_window`, a
-      burst of n_big pods of 16 cores / 180 GiB (135-225 GiB after seed perturbation) arriving over
-      [big_start, big_start + big_window] — they fit no trace node, only the 256-GiB template, so
-      they wait in the unscheduled cache, the CA scales that group up to its max and the Alibaba
-      pods that arrive meanwhile land on the new empty nodes (LeastAllocated); when the burst drains
-      the CA scales the nodes down once their remaining pods can be moved (scale_down) — and the
-      test_hpa.rs pod group (tests/test_hpa.rs:28-64) whose load cycle drives the HPA up and down.
+    * workload: n_pods - n_big Alibaba-like pods (c3_traces statistics) over `arrival_window` and
+      two bursts of n_big / 2 pods of 16 cores / 180 GiB (135-225 GiB after seed perturbation), over
+      [big_start, big_start + big_window] and `big_gap` seconds later.  They fit no trace node, only
+      the 256-GiB template: they wait in the unscheduled cache, the CA scales that group up, and the
+      Alibaba pods that arrive meanwhile land on the new empty nodes (LeastAllocated); when a burst
+      drains, the CA scales those nodes down once their remaining pods can be moved elsewhere
+      (scale_down), then up again for the second burst.  Default n_big: 48 per 16,384 pods (within
+      the group's max of 50, so a burst does not queue behind itself: under move-all every pod
+      finish retries every waiting pod, and a queue of hundreds would turn the run into a retry storm);
+    * the test_hpa.rs pod group (tests/test_hpa.rs:28-64), whose load cycle drives the HPA up and down.
     """
+    if n_big is None:
+        n_big = max(2, round(n_pods * 48 / 16384))
     cfg = SimulationConfig()
     cfg.ca_enabled = True
     cfg.ca_max_node_count = 200
@@ -253,7 +259,7 @@ def c5_autoscaled_parts(n_nodes: int = 4096, n_pods: int = 16384, n_big: int = 6
     w.events.append(WorkloadEvent(59.5, "create_pod_group", pod_group=g))
     w.events.extend(small.events)
     for i in range(n_big):
-        t = float(int(big_start + rng.random() * big_window))
+        t = float(int(big_start + (big_gap if i % 2 else 0.0) + rng.random() * big_window))
         w.create_pod(t, Pod(f"batch_big_{i}", 16000, 180 << 30, float(rng.randint(200, 600))))
     return cfg, cluster, w
 

@@ -26,22 +26,19 @@ __global__ __launch_bounds__(64) void probe_dispatch(uint32_t a, uint32_t b, dou
     dispatch(c, e);
 }
 
-__global__ __launch_bounds__(64) void probe_select(uint32_t ntr) {
+__global__ __launch_bounds__(64) void probe_sl_update(uint32_t q, int64_t key, uint32_t seq) {
     Ctx c;
-    int64_t k2;
-    uint32_t s2;
-    int src = next_source(c, ntr, k2, s2);
-    c.H().flags = (uint32_t)src + s2;
+    sl_update(c, uniform_u32(q), true, (int64_t)uniform_u64((uint64_t)key), uniform_u32(seq));
 }
 
-__global__ __launch_bounds__(64) void probe_consume_fifo(int src) {
+__global__ __launch_bounds__(64) void probe_consume_fifo(int src, uint32_t ntr) {
     Ctx c;
-    consume_source(c, uniform_u32((uint32_t)src) & 7);
+    consume_source(c, uniform_u32((uint32_t)src) & 7, ntr);
 }
 
-__global__ __launch_bounds__(64) void probe_consume_heap() {
+__global__ __launch_bounds__(64) void probe_consume_heap(uint32_t ntr) {
     Ctx c;
-    consume_source(c, SRC_HEAP);
+    consume_source(c, SRC_HEAP, ntr);
 }
 
 __global__ __launch_bounds__(64) void probe_emit_fifo(uint32_t a, uint32_t b) {
@@ -83,9 +80,9 @@ __global__ __launch_bounds__(64) void probe_cycle(double t) {
     run_scheduling_cycle(c, t);
 }
 
-__global__ __launch_bounds__(64) void probe_continue(uint32_t ntr) {
+__global__ __launch_bounds__(64) void probe_sl_apply_dirty(uint32_t ntr) {
     Ctx c;
-    c.H().flags = (uint32_t)continue_source(c, ntr);
+    sl_apply_dirty(c, ntr);
 }
 
 __global__ __launch_bounds__(64) void probe_heap_pop() {
