@@ -164,7 +164,12 @@ typedef struct k10s_replica_params {
        filtered node scores 0.0).  Default K10S_SCORE_LEAST_ALLOCATED. */
     double most_allocated_weight;
     uint32_t score_plugins;
-    uint32_t reserved0;
+    /* Replica-specific trace length: the replica runs the scenario as if its workload trace held only
+       its first workload_prefix events (generic.rs order, before the timestamp sort); 0 = all.  Lets
+       one engine batch replicas whose traces are prefixes of one master trace, e.g. C2's per-replica
+       ceil(U * 10000) pods (tests/test_determinism.rs:49-68).  Ids, total_pods_in_trace and the
+       termination rule are those of the shortened trace. */
+    uint32_t workload_prefix;
 } k10s_replica_params;
 #define K10S_SCORE_LEAST_ALLOCATED 1u
 #define K10S_SCORE_MOST_ALLOCATED 2u

@@ -582,7 +582,7 @@ bool build_scenario(const std::string& text, uint32_t group_bound_in, uint32_t c
             e.time = t.ts;
             e.seq = seq++;
             e.kind = (uint32_t)t.kind;
-            e.pad = 0;
+            e.wpos = K10S_TRACE_CLUSTER;
             if (t.kind == K10S_EV_AS_CREATE_NODE_REQ) {
                 e.arg = cluster_def[i];
                 hs.total_nodes_in_trace++;
@@ -591,12 +591,19 @@ bool build_scenario(const std::string& text, uint32_t group_bound_in, uint32_t c
             }
             ct.push_back(e);
         }
+        hs.n_cluster_trace = (uint32_t)cluster.size();
+        // create_pod events among the first k workload events in file (generation) order: a replica
+        // with workload_prefix k keeps exactly those (k10s_replica_params.workload_prefix)
+        std::vector<uint32_t> is_pod(workload.size(), 0);
+        for (const BTrace& t : workload) is_pod[t.pos] = t.kind == K10S_EV_AS_CREATE_POD_REQ ? 1u : 0u;
+        hs.wl_pods_upto.assign(1, 0);
+        for (uint32_t x : is_pod) hs.wl_pods_upto.push_back(hs.wl_pods_upto.back() + x);
         for (const BTrace& t : workload) {
             TraceEv e;
             e.time = t.ts;
             e.seq = seq++;
             e.kind = (uint32_t)t.kind;
-            e.pad = 0;
+            e.wpos = t.pos;
             if (t.kind == K10S_EV_AS_CREATE_GROUP_REQ) e.arg = (uint32_t)grank[t.group];
             else e.arg = pod_of(t.name);
             if (t.kind == K10S_EV_AS_CREATE_POD_REQ) hs.total_pods_in_trace++;
@@ -664,6 +671,8 @@ std::vector<uint8_t> pack_scenario(const HostScenario& hs, Scenario& s) {
     s.ca_enabled = hs.ca_enabled;
     s.hpa_enabled = hs.hpa_enabled;
     s.first_dynamic_seq = 2 + s.n_trace;
+    s.n_cluster_trace = hs.n_cluster_trace;
+    s.n_workload_trace = s.n_trace - hs.n_cluster_trace;
     s.total_pods_in_trace = hs.total_pods_in_trace;
     s.total_nodes_in_trace = hs.total_nodes_in_trace;
     s.node_uid = pk.put(hs.node_uid);
@@ -681,6 +690,7 @@ std::vector<uint8_t> pack_scenario(const HostScenario& hs, Scenario& s) {
     s.pod_key = pk.put(hs.pod_key);
     s.default_defs = pk.put(hs.default_defs);
     s.trace = pk.put(hs.trace);
+    s.wl_pods_upto = pk.put(hs.wl_pods_upto);
     s.g_initial = pk.put(hs.g_initial);
     s.g_max = pk.put(hs.g_max);
     s.g_cpu = pk.put(hs.g_cpu);
@@ -714,7 +724,7 @@ Scenario rebase_scenario(const Scenario& o, const uint8_t* base) {
 #define RB(f) s.f = rb(o.f, base)
     RB(node_uid); RB(def_node); RB(def_cpu); RB(def_ram); RB(def_ca_group); RB(def_ca_origin);
     RB(pod_uid); RB(pod_cpu); RB(pod_ram); RB(pod_dur); RB(pod_flags); RB(pod_group); RB(pod_key);
-    RB(default_defs); RB(trace);
+    RB(default_defs); RB(trace); RB(wl_pods_upto);
     RB(g_initial); RB(g_max); RB(g_cpu); RB(g_ram); RB(g_flags); RB(g_tcpu); RB(g_tram);
     RB(g_cpu_kind); RB(g_ram_kind); RB(g_cpu_usage); RB(g_ram_usage); RB(g_cpu_uoff); RB(g_cpu_ucnt);
     RB(g_ram_uoff); RB(g_ram_ucnt); RB(g_pod); RB(g_pos); RB(g_sorted_k); RB(unit_dur); RB(unit_load);
@@ -724,9 +734,11 @@ Scenario rebase_scenario(const Scenario& o, const uint8_t* base) {
 }
 
 // ---- per-replica layout ----------------------------------------------------------------------
-std::string params_error(const Params& p) {
+std::string params_error(const Params& p, const HostScenario& hs) {
     if (p.score_plugins == 0 || p.score_plugins > (K10S_SCORE_LEAST_ALLOCATED | K10S_SCORE_MOST_ALLOCATED))
         return "score_plugins must be 1 (LeastAllocatedResources), 2 (MostAllocatedResources) or 3 (both)";
+    if (p.workload_prefix + 1 > hs.wl_pods_upto.size())
+        return "workload_prefix exceeds the workload trace (" + std::to_string(hs.wl_pods_upto.size() - 1) + " events)";
     return "";
 }
 

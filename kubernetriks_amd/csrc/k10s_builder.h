@@ -26,6 +26,8 @@ struct HostScenario {
     uint32_t group_bound = 0, ca_bound = 0;
     bool ca_enabled = false, hpa_enabled = false;
     uint64_t total_pods_in_trace = 0, total_nodes_in_trace = 0;
+    uint32_t n_cluster_trace = 0;           // cluster-trace events (ids 2 .. 2 + n_cluster_trace - 1)
+    std::vector<uint32_t> wl_pods_upto;     // [W + 1] create_pod events among the first k workload events
     Params defaults;
 
     std::vector<std::string> node_names, pod_names, group_names, ca_group_names;
@@ -71,6 +73,6 @@ Scenario rebase_scenario(const Scenario& view_offsets, const uint8_t* base);
 Layout make_layout(const HostScenario& hs, const k10s_capacities& caps);
 
 // Caller-supplied replica parameters the engine cannot run: "" when valid, else the reason.
-std::string params_error(const Params& p);
+std::string params_error(const Params& p, const HostScenario& hs);
 
 }  // namespace k10s

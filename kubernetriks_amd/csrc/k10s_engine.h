@@ -2098,6 +2098,7 @@ K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
         break;
     case K10S_EV_AS_POD_FINISHED:
         h->counters[K10S_C_TERMINATED_PODS] += 1;
+        h->pods_left -= 1;
         h->counters[K10S_C_PODS_SUCCEEDED] += 1;
         h->g_cur_pods -= 1;  // api_server.rs:262-265
         emit(c, K10S_EV_PS_POD_FINISHED, pr->as_to_ps_network_delay, -1, e.a, e.b, e.x, FQ_AS_TO_PS);
@@ -2162,6 +2163,7 @@ K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
     case K10S_EV_AS_POD_REMOVED:
         if (e.b) {
             h->counters[K10S_C_TERMINATED_PODS] += 1;
+            h->pods_left -= 1;
             h->counters[K10S_C_PODS_REMOVED] += 1;
             h->g_cur_pods -= 1;  // api_server.rs:388-391
         }
@@ -2533,6 +2535,7 @@ K10S_HD void dispatch(Ctx& c, const HeapEv& e) {
     case K10S_EV_AS_POD_FINISHED: {   // api_server.rs:262-265
         RepHdr& H = c.H();
         H.counters[K10S_C_TERMINATED_PODS] += 1;
+        H.pods_left -= 1;
         H.counters[K10S_C_PODS_SUCCEEDED] += 1;
         H.g_cur_pods -= 1;
         emit(c, K10S_EV_PS_POD_FINISHED, c.P().as_to_ps_network_delay, -1, e.a, e.b, e.x, FQ_AS_TO_PS);
@@ -2552,12 +2555,30 @@ K10S_HD void dispatch(Ctx& c, const HeapEv& e) {
     else on_hpa(c, e);
 }
 
-// Cache the trace stream's head (time, id) in the working header.
-K10S_HD void trace_head_load(Ctx& c, uint32_t cur) {
-    if (cur < c.S().n_trace) {
-        c.H().tr_time = c.S().trace[cur].time;
-        c.H().tr_seq = c.S().trace[cur].seq;
+// Advance the trace cursor from `cur` past the workload events that are not in this replica's
+// trace (file position >= trace_prefix: k10s_replica_params.workload_prefix) and cache the head
+// (time, id) in the working header.  The stream is in (time, id) order, which for workload events
+// is id order, so the replica's id of a kept workload event is its scenario id minus the workload
+// events skipped before it (the reference numbers only the events of the replica's own trace,
+// simulator.rs:234-253); cluster events precede every workload id and keep theirs.  Returns the
+// cursor; n_trace when the replica's trace is exhausted.
+K10S_HD uint32_t trace_head_load(Ctx& c, uint32_t cur) {
+    RepHdr& H = c.H();
+    const uint32_t n = c.S().n_trace, pre = H.trace_prefix;
+    uint32_t skip = H.tr_skip;
+    uint32_t wp = cur < n ? c.S().trace[cur].wpos : 0u;
+    while (cur < n && wp != K10S_TRACE_CLUSTER && wp >= pre) {
+        skip++;
+        cur++;
+        wp = cur < n ? c.S().trace[cur].wpos : 0u;
     }
+    if (cur < n) {
+        H.tr_time = c.S().trace[cur].time;
+        H.tr_seq = c.S().trace[cur].seq - (wp == K10S_TRACE_CLUSTER ? 0u : skip);
+    }
+    H.tr_skip = skip;
+    H.trace_cursor = cur;
+    return cur;
 }
 
 // ---- initialize (simulator.rs:68-275 minus the trace emission, which is the shared stream) -----
@@ -2646,7 +2667,14 @@ K10S_HD void init_replica(Ctx& c) {
     memset(&z, 0, sizeof z);
     *h = z;
     for (int i = 0; i < 3; i++) est_reset(h->est[i]);
-    h->counters[K10S_C_TOTAL_PODS_IN_TRACE] = sc->total_pods_in_trace;
+    // the replica's workload trace: its first workload_prefix events (0 = all)
+    const uint32_t pre = pr->workload_prefix && pr->workload_prefix < sc->n_workload_trace ? pr->workload_prefix
+                                                                                         : sc->n_workload_trace;
+    const uint32_t first_dyn = 2 + sc->n_cluster_trace + pre;
+    h->trace_prefix = pre;
+    h->tr_skip = 0;
+    h->counters[K10S_C_TOTAL_PODS_IN_TRACE] = sc->wl_pods_upto[pre];
+    h->pods_left = (int64_t)sc->wl_pods_upto[pre];
     h->counters[K10S_C_TOTAL_NODES_IN_TRACE] = sc->total_nodes_in_trace;
     h->pool_head = 0;
     h->pool_count = sc->n_pool;
@@ -2688,7 +2716,7 @@ K10S_HD void init_replica(Ctx& c) {
     h->cur_kind = 0xFFFF;
     emit0(c, K10S_EV_M_POD_METRICS_TICK, 0.0);  // id 0 (simulator.rs:156-158)
     emit0(c, K10S_EV_M_GAUGE_TICK, 0.0);        // id 1 (simulator.rs:159-161)
-    h->next_seq = sc->first_dynamic_seq;         // trace events hold ids 2 .. 2 + n_trace - 1
+    h->next_seq = first_dyn;                     // trace events hold ids 2 .. first_dyn - 1
     emit0(c, K10S_EV_S_RUN_CYCLE, 0.0);          // Scheduler::start (scheduler.rs:78-81)
     emit0(c, K10S_EV_S_FLUSH, 0.0);
     if (sc->ca_enabled) emit0(c, K10S_EV_CA_TICK, 0.0);
@@ -2822,15 +2850,11 @@ K10S_HD void consume_source(Ctx& c, int src, uint32_t ntr) {
     int64_t key = 0;
     uint32_t seq = 0;
     if (src == SRC_TRACE) {
-        const uint32_t cur = H.trace_cursor + 1;
-        H.trace_cursor = cur;
+        const uint32_t cur = trace_head_load(c, H.trace_cursor + 1);
         has = cur < ntr;
         if (has) {
-            const double t = c.S().trace[cur].time;
-            seq = c.S().trace[cur].seq;
-            H.tr_time = t;
-            H.tr_seq = seq;
-            key = total_key(t);
+            key = total_key(H.tr_time);
+            seq = H.tr_seq;
         }
     } else if (src == SRC_HEAP) {
         const uint64_t t_hp = prof_now();
@@ -2882,7 +2906,7 @@ K10S_HD bool cache_fits(Ctx& c, uint32_t rc, uint64_t rr) {
 // entry fits the cache now and keeps the replica running.)
 K10S_HD bool replica_stalled(Ctx& c) {
     const RepHdr& H = c.H();
-    if (H.counters[K10S_C_TERMINATED_PODS] >= c.S().total_pods_in_trace) return false;
+    if (H.pods_left <= 0) return false;
     if (H.trace_cursor < c.S().n_trace || H.heap_size != 4 || H.aq_size != 0) return false;
     if (c.S().ca_enabled || c.S().hpa_enabled) return false;
     for (int q = 0; q < K10S_NFQ; q++)
@@ -2987,7 +3011,6 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
     h->cur_seq = 0;
     // launch constants are re-read at each use (scalar loads through the opaque constant pointer)
     // rather than held in SGPRs across the loop, where they are spilled around the handler calls
-#define total_pods (c.S().total_pods_in_trace)
 #define ntr (c.S().n_trace)
 #define cap_log (c.Ly().cap_log)
     // one time limit per mode (until_time / max_time)
@@ -3009,8 +3032,7 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
     const uint64_t t_loop = prof_now();
     sl_rebuild(c, ntr);  // the sorted source list, from the sources' heads
     while (!h->error_code) {
-        if (!until_mode() && h->counters[K10S_C_TERMINATED_PODS] >= total_pods &&
-            is_multiple_of_1000(h->clock)) {
+        if (!until_mode() && h->pods_left <= 0 && is_multiple_of_1000(h->clock)) {
             status = K10S_REPLICA_FINISHED;
             break;
         }
@@ -3028,7 +3050,7 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
                 const uint32_t cur = h->trace_cursor;
                 const uint32_t tk = c.S().trace[cur].kind, ta = c.S().trace[cur].arg;
                 e.time = c.S().trace[cur].time;
-                e.seq = c.S().trace[cur].seq;
+                e.seq = h->tr_seq;   // the replica's id (k10s_replica_params.workload_prefix)
                 e.kind = (uint16_t)tk;
                 e.slot = -1;
                 e.x = 0.0;
@@ -3149,7 +3171,6 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
     if (h->error_code) status = K10S_REPLICA_ERROR;
     h->status = status;
     return more;
-#undef total_pods
 #undef ntr
 #undef cap_log
 #if K10S_DEVICE && K10S_RUN_ARGS_LDS

@@ -280,7 +280,7 @@ k10s_engine* k10s_engine_create_bulk(const char* scenario_text, const void* pods
         }
         e->params[r].ca_max_node_count = e->hs.defaults.ca_max_node_count;  // fixed by the node pool
         if (e->params[r].score_plugins != K10S_SCORE_LEAST_ALLOCATED) e->plugins = true;
-        const std::string perr = params_error(e->params[r]);
+        const std::string perr = params_error(e->params[r], e->hs);
         if (!perr.empty()) {
             set_err(K10S_E_INVALID, "params[" + std::to_string(r) + "]: " + perr);
             delete e;

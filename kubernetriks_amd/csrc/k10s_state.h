@@ -32,11 +32,14 @@ namespace k10s {
 
 struct TraceEv {          // one client-emitted trace event (simulator.rs:234-253)
     double time;
-    uint32_t seq;         // dslab event id: 2 + position in (cluster trace ++ workload trace)
+    uint32_t seq;         // dslab event id: 2 + position in (cluster trace ++ workload trace), both
+                          // stable-sorted by timestamp (generic.rs:78, 105)
     uint32_t kind;        // K10S_EV_AS_* kind delivered to the api server
     uint32_t arg;         // node def / node idx / pod idx / group idx
-    uint32_t pad;
+    uint32_t wpos;        // workload event: its position in the trace file (generation order);
+                          // cluster event: K10S_TRACE_CLUSTER
 };
+#define K10S_TRACE_CLUSTER 0xFFFFFFFFu
 
 enum : uint8_t {
     POD_HAS_DEF = 1,      // created by the trace or a pod group (else: only named by remove_pod)
@@ -51,6 +54,7 @@ struct Scenario {
     uint32_t n_groups, n_ca_groups, group_bound, ca_bound, n_units;
     uint32_t ca_enabled, hpa_enabled;
     uint32_t first_dynamic_seq;
+    uint32_t n_cluster_trace, n_workload_trace;
     uint64_t total_pods_in_trace, total_nodes_in_trace;
 
     K10S_RO(uint32_t) node_uid;      // [N]
@@ -68,6 +72,7 @@ struct Scenario {
     K10S_RO(uint32_t) pod_key;       // [P] perturbation key (workload-trace position)
     K10S_RO(uint32_t) default_defs;  // [n_default] defs of default-cluster nodes, slot order
     K10S_RO(TraceEv) trace;          // [n_trace] merged (time, seq) order
+    K10S_RO(uint32_t) wl_pods_upto;  // [n_workload_trace + 1] create_pod events among the first k
 
     // pod groups (name order)
     K10S_RO(uint32_t) g_initial;
@@ -228,6 +233,11 @@ struct RepHdr {
     HeapEv heap_top;
     double tr_time;               // cached head of the shared trace stream (valid while
     uint32_t tr_seq, tr_pad;      // trace_cursor < n_trace)
+    uint32_t trace_prefix;        // workload events at file positions >= this are not in this
+                                  // replica's trace (k10s_replica_params.workload_prefix; ~0 = all)
+    uint32_t tr_skip;             // workload events skipped so far: the replica's id of a later
+                                  // workload event is its scenario id minus tr_skip
+    int64_t pods_left;            // total_pods_in_trace - terminated_pods (the termination rule)
     // the event sources' heads in (time, id) order (k10s_engine.h "source list"): entries
     // [0, sl_n) are the non-empty sources, sl[0] holds the next event; sl_dirty marks sources whose
     // head an emission changed (an empty ring got its first entry, a new heap root)

@@ -72,7 +72,7 @@ class ReplicaParams(ctypes.Structure):
                 ("enable_unscheduled_pods_conditional_move", ctypes.c_uint32), ("perturb", ctypes.c_uint32),
                 ("seed", ctypes.c_uint64), ("ca_max_node_count", ctypes.c_uint64),
                 ("most_allocated_weight", ctypes.c_double), ("score_plugins", ctypes.c_uint32),
-                ("reserved0", ctypes.c_uint32)]
+                ("workload_prefix", ctypes.c_uint32)]
 
 
 SCORE_LEAST_ALLOCATED = 1   # k10s_replica_params.score_plugins bits (include/k10s.h)

@@ -105,6 +105,28 @@ def c2_scenario(n_pods: int = 2000, seed: int = 123) -> str:
     return scenario_text(*c2_parts(n_pods, seed))
 
 
+def c2_survey_parts(n_max: int = 10000, seed: int = 123, horizon: float = 100000.0):
+    """C2 at its SURVEY.md §8(d) size: the 31-node default cluster and a master trace of n_max pods
+    drawn like tests/test_determinism.rs:49-68 (arrival U*1e5 s, cpu ceil(U*1000) mcpu, ram
+    U*1e10 B, duration U*1000 s).  Replica r runs the first ceil(U_r * n_max) of them
+    (c2_survey_params: k10s_replica_params.workload_prefix), seed-perturbed."""
+    cfg = SimulationConfig()
+    cfg.default_cluster = default_cluster_31()
+    return cfg, GenericClusterTrace(), c2_workload(n_max, seed, horizon)
+
+
+def c2_survey_prefix(r: int, n_max: int = 10000, base_seed: int = 123) -> int:
+    """Replica r's trace length ceil(U * n_max), U from its own seed (test_determinism.rs:49)."""
+    return max(1, int(math.ceil(random.Random(base_seed + r).random() * n_max)))
+
+
+def c2_survey_params(defaults, n: int, base_seed: int = 123, n_max: int = 10000, replica_offset: int = 0):
+    out = replica_params(defaults, n, base_seed=base_seed, perturb=True, replica_offset=replica_offset)
+    for i, p in enumerate(out):
+        p.workload_prefix = c2_survey_prefix(replica_offset + i, n_max, base_seed)
+    return out
+
+
 # ---- Alibaba-like (C3) ------------------------------------------------------------------------
 ALIBABA_NODE_MEM = 0.6899697150104833   # modal machine memory (cluster.rs test fixture / notebook)
 GIB128 = 128 * 1024 * 1024 * 1024
@@ -243,6 +265,10 @@ def c5_autoscaled_parts(n_nodes: int = 4096, n_pods: int = 16384, n_big: Optiona
       the group's max of 50, so a burst does not queue behind itself: under move-all every pod
       finish retries every waiting pod, and a queue of hundreds would turn the run into a retry storm);
     * the test_hpa.rs pod group (tests/test_hpa.rs:28-64), whose load cycle drives the HPA up and down.
+    Some parameter cells hit a reference panic: the HPA removes a group pod whose node the CA has
+    just scaled down, and the node component unwraps its reclaimed runtime (node_component.rs
+    RemovePodRequest).  The engine stops such a replica with K10S_REPLICA_ERROR at the same event,
+    exactly like the oracle (about 8 % of the sweep's replicas at 1,500 pods).
     """
     if n_big is None:
         n_big = max(2, round(n_pods * 48 / 16384))
@@ -309,6 +335,8 @@ def replica_scenario(cfg: SimulationConfig, cluster: GenericClusterTrace, worklo
     """Scenario text of one replica as the oracle must see it: its parameters and, when perturbed,
     its seed-perturbed workload (the engine applies both on the device)."""
     w = perturb_workload(workload, p.seed) if p.perturb else workload
+    if p.workload_prefix:   # the replica's trace: the first workload_prefix events (generic.rs order)
+        w = GenericWorkloadTrace(list(w.events[:p.workload_prefix]))
     return scenario_text(config_for_params(cfg, p), cluster, w)
 
 

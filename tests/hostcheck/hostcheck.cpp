@@ -71,7 +71,7 @@ void* hc_create_bulk(const char* text, const void* blob, uint64_t blob_len, cons
             h->params[r].seed = h->hs.defaults.seed + r;
         }
         h->params[r].ca_max_node_count = h->hs.defaults.ca_max_node_count;
-        const std::string perr = params_error(h->params[r]);
+        const std::string perr = params_error(h->params[r], h->hs);
         if (!perr.empty()) {
             if (err) std::snprintf(err, (size_t)errlen, "params[%u]: %s", r, perr.c_str());
             delete h;

@@ -144,3 +144,60 @@ def test_c5_sweep_at_baseline_size_gpu():
     assert all(r["status"] == "finished" for r in res)
     _identity(res)
     assert len({tuple(r["estimators"]["pod_queue_time"][1:5]) for r in res}) >= 8   # cycle interval x cond. move
+
+
+# ---- per-replica trace lengths (k10s_replica_params.workload_prefix) ---------------------------
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_workload_prefix_replicas_match_their_own_traces(backend):
+    """Replicas that keep only the first k workload events (k spread over 0..all, including a prefix
+    that cuts before the pod group and the removals) run exactly like the oracle on the shortened
+    trace: ids, total_pods_in_trace and the termination rule follow the replica's own trace."""
+    cfg, c, w = wl.c4_parts(n_batch_pods=60, seed=5)
+    w.remove_pod(900.0, "batch_3")
+    w.remove_pod(950.0, "batch_7")
+    scn = scenario_text(cfg, c, w)
+    E = engine_cls(backend)
+    W = len(w.events)
+    prefixes = [0, 1, 2, 17, W - 3, W - 1, W]
+    params = wl.replica_params(E(scn, 1).default_params(), len(prefixes), base_seed=41, perturb=True)
+    for p, k in zip(params, prefixes):
+        p.workload_prefix = k
+    eng = E(scn, len(prefixes), params=params, caps=parity.parity_caps(False))
+    eng.step_until_time(2500.0)
+    for r, k in enumerate(prefixes):
+        o = ob.OracleSim(wl.replica_scenario(cfg, c, w, params[r]))
+        o.step_until_time(2500.0)
+        od = o.result(placements=True)
+        od["status_name"] = parity.ORACLE_STATUS[4] if not od["panicked"] else "error"
+        assert parity.compare(od, eng, r=r, log=False) == [], (r, k)
+    tot = [res["counters"]["total_pods_in_trace"] for res in eng.results()]
+    assert tot[0] == tot[-1] == sum(1 for e in w.events if e.kind == "create_pod")
+    assert tot[1] == 0 and tot[1:] == sorted(tot[1:])   # prefix 1 keeps only the pod group
+    bad = wl.replica_params(E(scn, 1).default_params(), 1)
+    bad[0].workload_prefix = W + 1
+    with pytest.raises(Exception):
+        E(scn, 1, params=bad)
+
+
+def test_c2_survey_size_host():
+    """C2 at SURVEY size, CPU-sized: per-replica ceil(U * n) prefixes of one master trace."""
+    parts = wl.c2_survey_parts(n_max=400, horizon=4000.0)
+    eng = _batch_parity("host", parts, lambda d, n: wl.c2_survey_params(d, n, n_max=400), 4, check=[0, 1, 2, 3])
+    res = eng.results()
+    assert [r["counters"]["total_pods_in_trace"] for r in res] == [wl.c2_survey_prefix(r, 400) for r in range(4)]
+
+
+@pytest.mark.gpu
+def test_c2_at_survey_size_gpu():
+    """C2 as SURVEY.md §8(d) sizes it: 1,024 replicas of the 31-node default cluster, replica r
+    running the first ceil(U_r * 10,000) pods of a test_determinism-style master trace (arrivals over
+    1e5 s), seed-perturbed, in one engine batch; oracle replays of the shortest, the longest and
+    replicas spread over the batch."""
+    R = 1024
+    pre = [wl.c2_survey_prefix(r) for r in range(R)]
+    check = sorted({0, 1, 511, 1023, pre.index(min(pre)), pre.index(max(pre))})
+    eng = _batch_parity("gpu", wl.c2_survey_parts(), lambda d, n: wl.c2_survey_params(d, n), R, check=check)
+    res = eng.results()
+    assert all(r["status"] == "finished" for r in res)
+    _identity(res)
+    assert [r["counters"]["total_pods_in_trace"] for r in res] == pre
