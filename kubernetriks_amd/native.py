@@ -13,6 +13,8 @@ from typing import Dict, List, Optional, Sequence
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("K10S_LIB") or os.path.join(REPO, "build", "libk10s.so")
+if not os.path.isabs(LIB_PATH):   # a variant library named relative to the repository (tools/gpu.sh env: steps)
+    LIB_PATH = os.path.join(REPO, LIB_PATH)
 
 NUM_COUNTERS = 19
 COUNTER_NAMES = [
