@@ -177,6 +177,31 @@ K10S_HD void uniform_event(HeapEv& e) {
 #endif
 }
 
+// How an event reaches its out-of-line handler.  K10S_EV_BYREF=1 (default): as the address of its
+// LDS copy (the head entry of its source, which the loop consumes only after the handler ran; a
+// trace event is first written to the header's cur_ev slot), so a call passes one 32-bit VGPR and
+// the loop reads only the fields it tests.  0: by value in 8 VGPRs (the loop reads all 8 dwords to
+// SGPRs, writes them back into the argument VGPRs, the handler reads them to SGPRs again).
+#ifndef K10S_EV_BYREF
+#define K10S_EV_BYREF 1
+#endif
+#if K10S_DEVICE
+typedef const __attribute__((address_space(3))) HeapEv* EvRef;
+#define K10S_EVREF(x) ((EvRef)(x))
+#else
+typedef const HeapEv* EvRef;
+#define K10S_EVREF(x) ((EvRef)(x))
+#endif
+#if K10S_EV_BYREF
+#define K10S_EVARG EvRef ep
+#define K10S_EV_PROLOGUE \
+    HeapEv e = *ep;      \
+    uniform_event(e)
+#else
+#define K10S_EVARG HeapEv e
+#define K10S_EV_PROLOGUE uniform_event(e)
+#endif
+
 // ---- cycle attribution (K10S_PROF builds: tooling only, semantics-neutral) ----------------------
 // s_memtime deltas per loop phase, accumulated in RepHdr::prof and read by k10s_engine_profile.
 enum : int { PROF_LOOP = 0, PROF_SELECT = 1, PROF_CONSUME = 2, PROF_DISPATCH = 3, PROF_CYCLE = 4, PROF_SCAN = 5,
@@ -1851,8 +1876,8 @@ K10S_HD void ps_clean_up(Ctx& c, uint32_t p) {  // 173-182
     }
 }
 
-K10S_WARM void on_ps(Ctx& c, HeapEv e) {
-    uniform_event(e);
+K10S_WARM void on_ps(Ctx& c, K10S_EVARG) {
+    K10S_EV_PROLOGUE;
     RepHdr* h = &c.H();
     const Params* pr = &c.P();
     switch (e.kind) {
@@ -2024,8 +2049,8 @@ K10S_WARM void on_ps(Ctx& c, HeapEv e) {
 }
 
 // ---- api server (api_server.rs:127-457) --------------------------------------------------------
-K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
-    uniform_event(e);
+K10S_WARM void on_api_server(Ctx& c, K10S_EVARG) {
+    K10S_EV_PROLOGUE;
     RepHdr* h = &c.H();
     const Params* pr = &c.P();
     const Scenario* sc = &c.S();
@@ -2199,8 +2224,8 @@ K10S_WARM void on_api_server(Ctx& c, HeapEv e) {
 }
 
 // ---- node components (node_component.rs:178-335) ------------------------------------------------
-K10S_WARM void on_node(Ctx& c, HeapEv e) {
-    uniform_event(e);
+K10S_WARM void on_node(Ctx& c, K10S_EVARG) {
+    K10S_EV_PROLOGUE;
     const Params* pr = &c.P();
     int32_t slot = e.slot;
     switch (e.kind) {
@@ -2298,8 +2323,8 @@ K10S_WARM void on_node(Ctx& c, HeapEv e) {
 }
 
 // ---- cluster autoscaler proxy (cluster_autoscaler.rs:230-334) --------------------------------
-K10S_COLD void on_ca(Ctx& c, HeapEv e) {
-    uniform_event(e);
+K10S_COLD void on_ca(Ctx& c, K10S_EVARG) {
+    K10S_EV_PROLOGUE;
     RepHdr* h = &c.H();
     const Params* pr = &c.P();
     if (e.kind == K10S_EV_CA_TICK) {
@@ -2332,8 +2357,8 @@ K10S_HD uint32_t hpa_desired_by_metric(uint32_t cur, double value, double target
     return d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
 }
 
-K10S_COLD void on_hpa(Ctx& c, HeapEv e) {
-    uniform_event(e);
+K10S_COLD void on_hpa(Ctx& c, K10S_EVARG) {
+    K10S_EV_PROLOGUE;
     RepHdr* h = &c.H();
     const Scenario* sc = &c.S();
     const uint32_t B = sc->group_bound;
@@ -2492,8 +2517,8 @@ K10S_COLD void gauge_record(Ctx& c, double t) {
     h->gauge_n += 1;
 }
 
-K10S_COLD void on_metrics(Ctx& c, HeapEv e) {
-    uniform_event(e);
+K10S_COLD void on_metrics(Ctx& c, K10S_EVARG) {
+    K10S_EV_PROLOGUE;
     if (e.kind == K10S_EV_M_GAUGE_TICK) {  // CSV gauge record: no simulation state (collector.rs:392-407)
         if (c.Ly().cap_gauge) gauge_record(c, e.time);
         emit0(c, K10S_EV_M_GAUGE_TICK, 5.0);
@@ -2520,6 +2545,20 @@ K10S_COLD void on_metrics(Ctx& c, HeapEv e) {
 #ifndef K10S_FAST_DISPATCH
 #define K10S_FAST_DISPATCH 0
 #endif
+#if K10S_EV_BYREF
+K10S_HD void dispatch(Ctx& c, EvRef ep, uint32_t k) {
+    if (k <= K10S_EV_M_GAUGE_TICK) on_metrics(c, ep);
+    else if (k <= K10S_EV_AS_CREATE_GROUP_REQ) on_api_server(c, ep);
+    else if (k <= K10S_EV_PS_POD_REMOVED) on_ps(c, ep);
+    else if (k <= K10S_EV_S_REMOVE_POD) {
+        HeapEv e = *ep;
+        uniform_event(e);
+        on_scheduler(c, e);
+    } else if (k <= K10S_EV_N_REMOVE_POD) on_node(c, ep);
+    else if (k <= K10S_EV_CA_RESP) on_ca(c, ep);
+    else on_hpa(c, ep);
+}
+#else
 K10S_HD void dispatch(Ctx& c, const HeapEv& e) {
     uint32_t k = e.kind;
 #if K10S_FAST_DISPATCH
@@ -2554,6 +2593,7 @@ K10S_HD void dispatch(Ctx& c, const HeapEv& e) {
     else if (k <= K10S_EV_CA_RESP) on_ca(c, e);
     else on_hpa(c, e);
 }
+#endif
 
 // Advance the trace cursor from `cur` past the workload events that are not in this replica's
 // trace (file position >= trace_prefix: k10s_replica_params.workload_prefix) and cache the head
@@ -2843,7 +2883,11 @@ K10S_HD void fq_refill(Ctx& c, int cls, uint32_t hd) {
 }
 
 // Remove the head event of source src (sl[0]) and move the source's entry in the source list to
-// its new head; a FIFO takes its next head from its window.
+// its new head; a FIFO takes its next head from its window.  K10S_SL_FAST (default 1): when the new
+// head still precedes sl[1], only sl[0]'s key is rewritten (tuning knob, semantics-neutral).
+#ifndef K10S_SL_FAST
+#define K10S_SL_FAST 1
+#endif
 K10S_HD void consume_source(Ctx& c, int src, uint32_t ntr) {
     RepHdr& H = c.H();
     bool has;
@@ -2874,7 +2918,21 @@ K10S_HD void consume_source(Ctx& c, int src, uint32_t ntr) {
             seq = t.seq;
         }
     }
-    sl_update(c, (uint32_t)src, has, uniform_u64((uint64_t)key), uniform_u32(seq));
+    key = (int64_t)uniform_u64((uint64_t)key);
+    seq = uniform_u32(seq);
+    // src is sl[0]: while its new head still precedes the second source (47 % of the events at C3,
+    // profiles/r03_selection_policy_sim.json) only sl[0]'s key changes — no lane-parallel update
+    if (K10S_SL_FAST && has) {
+        const uint32_t n = uniform_u32(H.sl_n);
+        bool stays = n <= 1;
+        if (!stays) stays = sl_less(key, seq, (int64_t)uniform_u64((uint64_t)H.sl[1].key), uniform_u32(H.sl[1].seq));
+        if (stays) {
+            H.sl[0].key = key;
+            H.sl[0].seq = seq;
+            return;
+        }
+    }
+    sl_update(c, (uint32_t)src, has, key, seq);
 }
 
 // Does some node of the scheduler cache fit a (cpu, ram) request (Fit::filter, plugin.rs:34-45)?
@@ -3043,6 +3101,9 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
         bool have = false;
         const uint64_t t_sel = prof_now();
         sl_apply_dirty(c, ntr);
+#if K10S_EV_BYREF
+        EvRef ep = K10S_EVREF(&h->heap_top);
+#endif
         for (;;) {
             if (uniform_u32(h->sl_n) == 0) break;
             src = (int)uniform_u32(h->sl[0].src);
@@ -3060,17 +3121,40 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
                     e.a = c.S().def_node[ta];
                     e.b = ta;
                 }
+                uniform_event(e);
+#if K10S_EV_BYREF
+                h->cur_ev = e;
+                ep = K10S_EVREF(&h->cur_ev);
+#endif
             } else if (src == SRC_HEAP) {
+#if K10S_EV_BYREF
+                e.kind = (uint16_t)uniform_u32(h->heap_top.kind);
+                e.a = uniform_u32(h->heap_top.a);
+                e.seq = uniform_u32(h->heap_top.seq);
+                e.time = uniform_f64(h->heap_top.time);
+#else
                 e = h->heap_top;
+                uniform_event(e);
+#endif
                 if (e.kind == K10S_EV_N_POD_FINISHED && c.V().pod(e.a).finish_seq != e.seq) {  // canceled
                     heap_pop(c);
                     sl_refresh(c, SRC_HEAP, ntr);
                     continue;
                 }
+#if K10S_EV_BYREF
+                ep = K10S_EVREF(&h->heap_top);
+#endif
             } else {
+#if K10S_EV_BYREF
+                ep = K10S_EVREF(&h->fq_top[src]);
+                e.time = uniform_f64(ep->time);
+                e.seq = uniform_u32(ep->seq);
+                e.kind = (uint16_t)uniform_u32(ep->kind);
+#else
                 e = h->fq_top[src];
+                uniform_event(e);
+#endif
             }
-            uniform_event(e);
             have = true;
             break;
         }
@@ -3089,15 +3173,21 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
             more = 1;
             break;
         }
+#if !K10S_EV_BYREF
         const uint64_t t_con = prof_now();
         consume_source(c, src, ntr);
         K10S_PROF_ADD(c, PROF_CONSUME, t_con);
+#endif
         h->clock = e.time;
         h->cur_kind = e.kind;
         h->cur_seq = e.seq;
         fair_priority(done);
         done++;  // counters[K10S_C_EVENTS] takes the launch's count once, at exit (no per-event LDS RMW)
         if (cap_log) {
+#if K10S_EV_BYREF
+            e = *ep;   // parity logging: the whole event
+            uniform_event(e);
+#endif
             uint32_t k = h->log_n;
             if (k < cap_log) {
                 k10s_log_entry le;
@@ -3154,7 +3244,17 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
         }
 #endif
         const uint64_t t_dis = prof_now();
+#if K10S_EV_BYREF
+        dispatch(c, ep, e.kind);
+        {   // the event stayed at the head of its source during the handler (an emission lands after
+            // it: larger id, time >= clock); remove it now
+            const uint64_t t_con = prof_now();
+            consume_source(c, src, ntr);
+            K10S_PROF_ADD(c, PROF_CONSUME, t_con);
+        }
+#else
         dispatch(c, e);
+#endif
         K10S_PROF_ADD(c, PROF_DISPATCH, t_dis);
 #if K10S_PROF
         h->prof[K10S_PROF_KIND0 + e.kind] += prof_now() - t_dis;

@@ -231,6 +231,7 @@ struct RepHdr {
     double fq_last[K10S_NFQ];
     HeapEv fq_top[K10S_NFQ];
     HeapEv heap_top;
+    HeapEv cur_ev;                // a trace event being handled (k10s_engine.h K10S_EV_BYREF)
     double tr_time;               // cached head of the shared trace stream (valid while
     uint32_t tr_seq, tr_pad;      // trace_cursor < n_trace)
     uint32_t trace_prefix;        // workload events at file positions >= this are not in this
