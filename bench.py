@@ -77,6 +77,8 @@ def parse():
     ap.add_argument("--no-backlog-line", action="store_true",
                     help="skip the one-launch c3_backlog measurement reported beside a c3 run")
     ap.add_argument("--pruned-scan", action="store_true", help="exact block-bound pruned scan (DESIGN.md §3)")
+    ap.add_argument("--delay-fifo", type=int, default=0,
+                    help="entries per delay-class event ring (k10s_capacities.delay_fifo; 0 = engine default)")
     ap.add_argument("--profile", action="store_true", help="print the K10S_PROF cycle attribution (variant builds)")
     ap.add_argument("--selftest-host", action="store_true",
                     help="TEST ONLY: run the launcher and the cross-rank reduction on CPU (gloo) over the "
@@ -298,6 +300,7 @@ def main():
     t = time.perf_counter()
     caps = Capacities()
     caps.pruned_scan = 1 if args.pruned_scan else 0
+    caps.delay_fifo = args.delay_fifo
     eng = make_engine(scn, R, params=params, caps=caps, blob=blob)
     log(f"[rank {rank}] engine: {R} replicas x {eng.replica_bytes / 2**20:.1f} MiB, init {time.perf_counter() - t:.2f}s")
 

@@ -179,7 +179,8 @@ typedef struct k10s_capacities {
     uint32_t event_heap, active_queue, unschedulable, group_name_bound, ca_name_bound;
     uint32_t event_log, placement_log;   /* parity mode logs; 0 = off */
     uint32_t pod_records;                /* 1 = keep per-pod start/finish/removal times */
-    uint32_t delay_fifo;                 /* entries per delay-class event ring: 0 = default (512),
+    uint32_t delay_fifo;                 /* entries per delay-class event ring: 0 = default (the node
+                                            count rounded up to a power of two, within [512, 8192]),
                                             K10S_FIFO_OFF = every event in the heap */
     uint32_t pruned_scan;                /* 0 = every attempt scans every node (default);
                                             1 = exact block-bound pruned scan where it applies

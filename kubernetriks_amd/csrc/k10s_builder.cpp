@@ -763,7 +763,10 @@ Layout make_layout(const HostScenario& hs, const k10s_capacities& caps) {
     if (caps.delay_fifo == K10S_FIFO_OFF) {
         L.cap_fq = 0;
     } else {
-        uint32_t want = caps.delay_fifo ? caps.delay_fifo : 512u;
+        // default: room for a burst of one event per node (the cluster trace creates every node at
+        // once: 4,096 PS create requests in one ring at C3, which a 512-entry ring spilled to the
+        // heap), at least 512, at most 8,192 entries per class (2 MiB per replica)
+        uint32_t want = caps.delay_fifo ? caps.delay_fifo : (uint32_t)std::min<uint64_t>(std::max<uint64_t>(512, N), 8192);
         if (want > (1u << 20)) want = 1u << 20;
         L.cap_fq = 1;
         while (L.cap_fq < want) L.cap_fq <<= 1;
