@@ -194,26 +194,6 @@ def cpu_baseline(args, cfg, cluster, workload, params):
 
 
 # ---- the measurement ------------------------------------------------------------------------------
-def pmc_traffic(workload, config, engine, scan_mode="full"):
-    """HBM bytes per launch of k10s_run_kernel from the committed rocprofv3 PMC pass for this workload
-    (profiles/pmc_run_kernel.json for c3, profiles/pmc_run_kernel_<workload>.json otherwise; made by
-    tools/pmc_summary.py), or None unless that pass was taken on this exact kernel build, config,
-    workload and scan mode."""
-    name = "pmc_run_kernel.json" if workload == "c3" else f"pmc_run_kernel_{workload}.json"
-    path = os.path.join(REPO, "profiles", name)
-    if not os.path.exists(path):
-        return None
-    try:
-        pm = json.load(open(path))
-        if pm.get("config") == list(config) and pm.get("engine") == engine and \
-                pm.get("workload", "c3") == workload and pm.get("scan_mode") == scan_mode:
-            return pm.get("hbm_bytes_per_launch")
-    except Exception:
-        return None
-    return None
-
-
-
 def build_workload(args):
     """(config, cluster trace, workload trace, description, sweep) of the selected workload."""
     from kubernetriks_amd import workloads as wl
@@ -356,8 +336,18 @@ def main():
     achieved = per_launch_bytes / (mean_kernel_ms * 1e-3) if mean_kernel_ms > 0 else 0.0
     # what the scans actually read (pruned scan: block bounds + scanned blocks + bound upkeep)
     touched_bytes = (12.0 * nread + 12.0 * attempts + 12.0 * placements) / (args.steps * world)
-    traffic = None if args.selftest_host else \
-        pmc_traffic(args.workload, (R, args.nodes, args.pods), version(), "pruned" if args.pruned_scan else "full")
+    traffic = None
+    pmc_path = os.path.join(REPO, "profiles", "pmc_run_kernel.json")
+    if os.path.exists(pmc_path) and not args.selftest_host:
+        try:
+            pm = json.load(open(pmc_path))
+            # only a PMC pass over this exact kernel build, config, workload and scan mode counts
+            if pm.get("config") == [R, args.nodes, args.pods] and pm.get("engine") == version() and \
+                    pm.get("workload", "c3") == args.workload and \
+                    pm.get("scan_mode") == ("pruned" if args.pruned_scan else "full"):
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
 
     out = {
         "metric": METRIC,
@@ -468,9 +458,7 @@ def backlog_line(args, cfg, make_engine, caps, ensemble, num_counters, version):
             "placements_per_s": placements / elapsed, "attempts_per_s": attempts / elapsed,
             "ms_per_step": elapsed * 1e3, "kernel_ms_per_launch": ms,
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK, "algorithmic_bytes_per_launch": per_launch,
-                         "traffic": pmc_traffic("c3_backlog", (args.replicas, args.nodes, args.pods), version(),
-                                                "pruned" if args.pruned_scan else "full")},
+                         "frac": achieved / HBM_PEAK, "algorithmic_bytes_per_launch": per_launch},
             "totals": {"placements": placements, "attempts": attempts, "requeued": int(c[17]), "flushed": int(c[18])},
             "engine": version()}
 

@@ -784,8 +784,6 @@ Layout make_layout(const HostScenario& hs, const k10s_capacities& caps) {
     L.s_present = take(8 * (uint64_t)L.words_nodes);
     L.s_ccpu = take(4 * N);
     L.s_cram = take(8 * N);
-    L.s_ia = take(4 * N);
-    L.s_ir = take(4 * N);
     L.pruned = caps.pruned_scan ? 1u : 0u;
     L.stall = caps.stall_guard ? 1u : 0u;
     L.bshift = 6;

@@ -81,8 +81,6 @@ struct Rep {
     K10S_HD uint64_t* s_present() const { return at<uint64_t>(L().s_present); }
     K10S_HD uint32_t* s_bcpu() const { return at<uint32_t>(L().s_bcpu); }
     K10S_HD uint32_t* s_ccpu() const { return at<uint32_t>(L().s_ccpu); }
-    K10S_HD float* s_ia() const { return at<float>(L().s_ia); }
-    K10S_HD float* s_ir() const { return at<float>(L().s_ir); }
     K10S_HD uint64_t* s_cram() const { return at<uint64_t>(L().s_cram); }
     K10S_HD uint64_t* s_bram() const { return at<uint64_t>(L().s_bram); }
     K10S_HD NodeState& node(uint32_t n) const { return at<NodeState>(L().node)[n]; }
@@ -589,16 +587,6 @@ K10S_HELPER void uq_insert(Ctx& c, const QInfo& q) {
 
 K10S_HD bool pod_in_s(const Ctx& c, uint32_t p) { return (c.V().pod(p).flags & PF_IN_S) != 0; }
 
-// One scheduler-cache entry (the scan target): allocatable cpu / ram and, for the event loop's
-// screened scan (scan_lanes_inv), their f32 reciprocals, IEEE-rounded (an absent node's (0, 0) gives
-// +inf, so no finite threshold admits it).
-K10S_HD void cache_set(const Ctx& c, uint32_t n, uint32_t ac, uint64_t ar) {
-    c.V().s_cpu()[n] = ac;
-    c.V().s_ram()[n] = ar;
-    c.V().s_ia()[n] = 1.0f / (float)ac;
-    c.V().s_ir()[n] = 1.0f / (float)ar;
-}
-
 // move_pods_to_active_queue over a selection, in key order (scheduler.rs:174-185)
 // mode 0: all (move_all_to_active_queue, 235-244); 1: flush (188-203, stay > 300 s);
 // 2: freed-resources conditional (366-379); 3: inverted add-node conditional (396-405).
@@ -888,12 +876,6 @@ K10S_HD bool scan_screen(uint32_t ac, uint64_t ar, float fa, float fr, float T) 
     const float fR = __builtin_fmaf((float)(uint32_t)(ar >> 32), 4294967296.0f, (float)(uint32_t)ar);
     return __builtin_fmaf(fa, fR, fr * fA) > fA * fR * T;
 }
-// The reciprocal form of the screen (scan_lanes_inv): u' = fl(fa·fl(1/A) + fl(fr·fl(1/R))) > T, with
-// fa = fl32(rc), fr = fl32(rr) correctly rounded, as the device forms it (packed f32 mul / fma).
-K10S_HD bool scan_screen_inv(uint32_t ac, uint64_t ar, float fa, float fr, float T) {
-    const float ia = 1.0f / (float)ac, ir = 1.0f / (float)ar;
-    return __builtin_fmaf(fa, ia, fr * ir) > T;
-}
 // u of a scored node from its exact score: (100 − s)/50, rounded to f32.
 K10S_HD float screen_u(double s) { return (float)((100.0 - s) * 0.02); }
 
@@ -1063,73 +1045,10 @@ K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, cons
 }
 #endif
 
-#if K10S_DEVICE
-// ---- reciprocal screen (event loop, weight 1.0, rc > 0, rr > 0; K10S_SCAN_INV) ------------------
-// The same decision rule as scan_lanes_screen with the screen's inputs precomputed per node: the
-// scheduler cache keeps ia = fl32(1/A) and ir = fl32(1/R) next to A and R (cache_set), so a lane
-// screens its 4 nodes with two 16-B loads and u' = fl(fa*ia + fl(fr*ir)) (two packed f32 ops per 2
-// nodes) against T = thr + eps, and loads A and R — Fit and the exact score — only for the nodes
-// the screen cannot rule out (all of step 0, then a few per scan).  The scan streams 8 B per node
-// instead of 12.  Soundness: fa, fr, ia, ir and the two operations each round once (relative error
-// <= 2^-24), so |u' - u| <= 4.1 * 2^-24 * u; for u' <= 3, u' > T implies u(x) > u(y) + 9.1e-6, whose
-// exact scores differ by more than 4.5e-4 (the computed f64 scores are within 3.4e-14 of exact),
-// and for u' > 3, u(x) > 2.99 > u(y) + 0.99 (u(y) <= 2 for a fitting node).  An absent node's
-// (0, 0) gives u' = +inf: ruled out by any finite T, by Fit at step 0.  tests/test_scan_screen.py
-// checks the rule through the host form scan_screen_inv.
-#ifndef K10S_SCAN_INV
-#define K10S_SCAN_INV 1
-#endif
-K10S_D void scan_lanes_inv(const uint32_t* s_cpu, const uint64_t* s_ram, const float* s_ia, const float* s_ir,
-                           uint32_t n_nodes, uint32_t rc, uint64_t rr, double& best_s, int32_t& best_n) {
-    const uint32_t l4 = 4u * (uint32_t)lane_id();
-    rc = uniform_u32(rc);
-    rr = uniform_u64(rr);
-    const double frc = uniform_f64((double)rc), frr = uniform_f64(u64_f64(rr));
-    const float fa = __builtin_bit_cast(float, uniform_u32(__builtin_bit_cast(uint32_t, (float)rc)));
-    const float fr = __builtin_bit_cast(float, uniform_u32(__builtin_bit_cast(uint32_t, (float)rr)));
-    if (n_nodes == 0) return;
-    uint32_t la = 0;   // the lane best's allocatables (0: none; a fitting node has both >= 1)
-    uint64_t lr = 0;
-    float lu = __builtin_inff();
-    float T = __builtin_inff();  // thr + eps: +inf screens nothing out (the first step)
-    const f32x2 va = {fa, fa}, vr = {fr, fr};
-    for (uint32_t base = 0; base < n_nodes; base += 256) {
-        const uint32_t n0 = base + l4;
-        const uint32_t a = n0 < n_nodes ? n0 : 0u;
-        const float4 ia = *reinterpret_cast<const float4*>(s_ia + a);
-        const float4 ir = *reinterpret_cast<const float4*>(s_ir + a);
-        const uint32_t valid = n0 < n_nodes ? (n_nodes - n0 >= 4 ? 0xFu : ((1u << (n_nodes - n0)) - 1u)) : 0u;
-        const f32x2 ia01 = {ia.x, ia.y}, ia23 = {ia.z, ia.w}, ir01 = {ir.x, ir.y}, ir23 = {ir.z, ir.w};
-        const f32x2 u01 = __builtin_elementwise_fma(va, ia01, vr * ir01);
-        const f32x2 u23 = __builtin_elementwise_fma(va, ia23, vr * ir23);
-        const uint32_t out = (uint32_t)(u01.x > T) | ((uint32_t)(u01.y > T) << 1) | ((uint32_t)(u23.x > T) << 2) |
-                             ((uint32_t)(u23.y > T) << 3);
-        uint32_t need = valid & ~out;
-        if (need) {
-            const uint4 cv = *reinterpret_cast<const uint4*>(s_cpu + a);
-            const ulonglong2 r01 = *reinterpret_cast<const ulonglong2*>(s_ram + a);
-            const ulonglong2 r23 = *reinterpret_cast<const ulonglong2*>(s_ram + a + 2);
-            need &= (uint32_t)(rc <= cv.x && rr <= r01.x) | ((uint32_t)(rc <= cv.y && rr <= r01.y) << 1) |
-                    ((uint32_t)(rc <= cv.z && rr <= r23.x) << 2) | ((uint32_t)(rc <= cv.w && rr <= r23.y) << 3);
-            if (need & 1u) score_node_exact(n0, cv.x, r01.x, rr, frc, frr, best_s, best_n, la, lr, lu);
-            if (need & 2u) score_node_exact(n0 + 1, cv.y, r01.y, rr, frc, frr, best_s, best_n, la, lr, lu);
-            if (need & 4u) score_node_exact(n0 + 2, cv.z, r23.x, rr, frc, frr, best_s, best_n, la, lr, lu);
-            if (need & 8u) score_node_exact(n0 + 3, cv.w, r23.y, rr, frc, frr, best_s, best_n, la, lr, lu);
-        }
-        // thr only moves when some lane scored a node exactly this step
-        if (__ballot(need != 0)) {
-            const float thr = __builtin_bit_cast(float, uniform_u32(__builtin_bit_cast(uint32_t, wave_min_f32(lu))));
-            T = thr + K10S_SCREEN_EPS;
-        }
-    }
-}
-#endif
-
 // LOOP: the event loop's scans (K10S_LOOP_SCAN_PIPE) rather than the unit surface's (K10S_SCAN_PIPE).
 template <bool LOOP = false>
 K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
-                          uint32_t rc, uint64_t rr, double weight, int32_t* chosen, const float* s_ia = nullptr,
-                          const float* s_ir = nullptr) {
+                          uint32_t rc, uint64_t rr, double weight, int32_t* chosen) {
     uint64_t best_key = 0;
     int32_t best_n = -1;
     int32_t first = 0x7fffffff;
@@ -1139,9 +1058,7 @@ K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const ui
         // A fitting node has alloc >= request > 0 in both resources, so neither term is 0/0 and every
         // score is a finite number >= 0: filtered[0] is never NaN, "some node fits" <=> best_n >= 0,
         // and neither filtered[0] nor its re-scored value is needed (kube_scheduler.rs:140-148).
-        if (LOOP && K10S_SCAN_INV)
-            scan_lanes_inv(s_cpu, s_ram, s_ia, s_ir, n_nodes, rc, rr, best_s, best_n);
-        else if (LOOP && K10S_SCAN_SCREEN)
+        if (LOOP && K10S_SCAN_SCREEN)
             scan_lanes_screen<K10S_LOOP_SCAN_PIPE, true>(s_cpu, s_ram, present, n_nodes, rc, rr, best_s, best_n);
         else if (!LOOP && K10S_UNIT_SCREEN)
             scan_lanes_screen<K10S_SCAN_PIPE, false>(s_cpu, s_ram, present, n_nodes, rc, rr, best_s, best_n);
@@ -1424,7 +1341,7 @@ K10S_CYCLE_FN void run_scheduling_cycle_t(Ctx& c, double t) {
             }
             if (st < 0) {
                 st = schedule_scan<true>(c.V().s_cpu(), c.V().s_ram(), c.V().s_present(), c.S().n_nodes, rc, rr, w,
-                                         &chosen, c.V().s_ia(), c.V().s_ir());
+                                         &chosen);
                 nread = c.S().n_nodes;
             }
             h->counters[K10S_C_NODES_READ] += nread;
@@ -1438,7 +1355,8 @@ K10S_CYCLE_FN void run_scheduling_cycle_t(Ctx& c, double t) {
             continue;
         }
         uint32_t n = (uint32_t)chosen;
-        cache_set(c, n, c.V().s_cpu()[n] - rc, c.V().s_ram()[n] - rr);  // reserve_node_resources (118-123)
+        c.V().s_cpu()[n] -= rc;  // reserve_node_resources (118-123)
+        c.V().s_ram()[n] -= rr;
         node_bound_changed(c, n);
         c.V().node(n).flags |= NF_S_ASSIGN;  // assign_node_to_pod (125-151)
         c.V().pod(p).s_assigned = (int32_t)n;
@@ -1494,7 +1412,8 @@ K10S_HD void s_release(Ctx& c, uint32_t p) {  // release_node_resources (153-162
         fail(c, K10S_PANIC_MISSING_NODE);
         return;
     }
-    cache_set(c, (uint32_t)n, c.V().s_cpu()[n] + c.V().pod(p).req_cpu, c.V().s_ram()[n] + c.V().pod(p).req_ram);
+    c.V().s_cpu()[n] += c.V().pod(p).req_cpu;
+    c.V().s_ram()[n] += c.V().pod(p).req_ram;
     node_bound_changed(c, (uint32_t)n);
 }
 
@@ -1522,7 +1441,8 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
         uint32_t n = e.a;
         uint32_t ac = e.b;
         uint64_t ar = f2u(e.x);
-        cache_set(c, n, ac, ar);
+        c.V().s_cpu()[n] = ac;
+        c.V().s_ram()[n] = ar;
         // the stored node's capacity: a node reaches the scheduler straight from its creation,
         // allocatable = capacity (node.rs:60-66); only MostAllocated reads it
         c.V().s_ccpu()[n] = ac;
@@ -1576,8 +1496,13 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
         }
-        if (sa == (int32_t)n) cache_set(c, n, n_cpu + rc, n_ram + rr);
-        else cache_set(c, (uint32_t)sa, c.V().s_cpu()[sa] + rc, c.V().s_ram()[sa] + rr);
+        if (sa == (int32_t)n) {
+            c.V().s_cpu()[n] = n_cpu + rc;
+            c.V().s_ram()[n] = n_ram + rr;
+        } else {
+            c.V().s_cpu()[sa] += rc;
+            c.V().s_ram()[sa] += rr;
+        }
         node_bound_changed(c, (uint32_t)sa);
         s_move_after_free(c, rc, rr);
         break;
@@ -1591,7 +1516,8 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
         bit_clear(c.V().s_present(), n);
         // invariant: an absent node's cache entry is (0, 0), as after initialize, so no request with
         // cpu > 0 fits it and the event loop's screened scan needs no presence words
-        cache_set(c, n, 0, 0);
+        c.V().s_cpu()[n] = 0;
+        c.V().s_ram()[n] = 0;
         h->s_node_count -= 1;
         node_bound_changed(c, n);
         if (c.V().node(n).flags & NF_S_ASSIGN) {  // reschedule_unfinished_pods (352-364), name order
@@ -2717,8 +2643,11 @@ K10S_HD void init_replica(Ctx& c) {
     memset(&ns, 0, sizeof ns);
     ns.as_slot = -1;
     ns.pend_def = -1;
+    uint32_t* s_cpu = v.s_cpu();
+    uint64_t* s_ram = v.s_ram();
     for (uint32_t i = lane; i < N; i += K10S_LANES) {
-        cache_set(c, i, 0, 0);
+        s_cpu[i] = 0;
+        s_ram[i] = 0;
         v.node(i) = ns;
     }
     for (uint32_t i = lane; i < L->words_nodes; i += K10S_LANES) v.s_present()[i] = 0;
@@ -2811,7 +2740,8 @@ K10S_HD void init_replica(Ctx& c) {
             v.g_cpu()[slot] = sc->def_cpu[def];
             v.g_ram()[slot] = sc->def_ram[def];
         }
-        cache_set(c, n, sc->def_cpu[def], sc->def_ram[def]);
+        s_cpu[n] = sc->def_cpu[def];
+        s_ram[n] = sc->def_ram[def];
         v.s_ccpu()[n] = sc->def_cpu[def];
         v.s_cram()[n] = sc->def_ram[def];
         bit_set(v.s_present(), n);

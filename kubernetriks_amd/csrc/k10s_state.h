@@ -331,7 +331,6 @@ struct Layout {
     uint64_t s_cpu, s_ram, s_present;    // hot scheduler-cache SoA (scan target)
     uint64_t s_bcpu, s_bram;             // per-block maxima of the present nodes' allocatable
     uint64_t s_ccpu, s_cram;             // scheduler-cache capacity SoA (MostAllocated, an extension)
-    uint64_t s_ia, s_ir;                 // f32 reciprocals 1/alloc_cpu, 1/alloc_ram (the screened scan)
     uint64_t node, pend_rm, pod, prec, slot, pool_ring;
     uint64_t grp, grp_bits;
     uint64_t cag, ca_act, ca_cpu, ca_ram, ca_undo;

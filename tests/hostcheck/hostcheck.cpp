@@ -199,7 +199,3 @@ extern "C" int hc_scan_screen(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr
     return scan_screen(ac, ar, fa, fr, thr + K10S_SCREEN_EPS) ? 1 : 0;
 }
 extern "C" float hc_screen_u(double s) { return screen_u(s); }
-// The reciprocal screen of scan_lanes_inv (the default build's event-loop scan).
-extern "C" int hc_scan_screen_inv(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr, float thr) {
-    return scan_screen_inv(ac, ar, (float)rc, (float)rr, thr + K10S_SCREEN_EPS) ? 1 : 0;
-}

@@ -21,14 +21,10 @@ from kubernetriks_amd.scenario import GenericClusterTrace, GenericWorkloadTrace,
 from test_scan_adversarial import EPS, U64, adversarial_problems, la, reference_argmax
 
 
-SCREENS = ["hc_scan_screen", "hc_scan_screen_inv"]   # scan_lanes_screen, scan_lanes_inv (default)
-
-
 def _hc():
     L = hclib()
-    for f in SCREENS:
-        getattr(L, f).argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float]
-        getattr(L, f).restype = ctypes.c_int
+    L.hc_scan_screen.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float]
+    L.hc_scan_screen.restype = ctypes.c_int
     L.hc_screen_u.argtypes = [ctypes.c_double]
     L.hc_screen_u.restype = ctypes.c_float
     return L
@@ -40,13 +36,11 @@ def _rand_req(rng, cap_c, cap_r):
     return min(rc, cap_c), min(rr, cap_r)
 
 
-@pytest.mark.parametrize("screen", SCREENS)
-def test_screen_sound_near_threshold(screen):
+def test_screen_sound_near_threshold():
     """Nodes built to sit within a few eps of the threshold (u(x) - u(y) in [-eps, 3 eps]) and random
     ones: every node the screen drops scores strictly below y; it drops nearly all nodes more than
     2.2 eps above (so it does prune)."""
     L = _hc()
-    scr = getattr(L, screen)
     rng = random.Random(7)
     dropped = far = far_dropped = 0
     for _ in range(1500):
@@ -65,26 +59,24 @@ def test_screen_sound_near_threshold(screen):
             for R2 in (R - 1, R, R + 1, rng.randint(rr, max(rr, 2 * S))):
                 if not (rr <= R2 <= U64) or R2 < 1:
                     continue
-                if scr(A, R2, rc, rr, thr):
+                if L.hc_scan_screen(A, R2, rc, rr, thr):
                     dropped += 1
                     assert la(A, R2, rc, rr) < sy, (A, R2, rc, rr, B, S)
                 if rc / A + rr / R2 > uy + 2.2 * EPS:
                     far += 1
-                    far_dropped += scr(A, R2, rc, rr, thr)
+                    far_dropped += L.hc_scan_screen(A, R2, rc, rr, thr)
     assert dropped > 5000
     assert far_dropped >= 0.99 * far
 
 
-@pytest.mark.parametrize("screen", SCREENS)
-def test_screen_keeps_everything_before_the_first_threshold(screen):
-    scr = getattr(_hc(), screen)
-    assert not scr(64000, 1 << 37, 500, 1 << 30, float("inf"))
-    assert not scr((1 << 32) - 1, U64, 1, 1, float("inf"))
+def test_screen_keeps_everything_before_the_first_threshold():
+    L = _hc()
+    assert not L.hc_scan_screen(64000, 1 << 37, 500, 1 << 30, float("inf"))
+    assert not L.hc_scan_screen((1 << 32) - 1, U64, 1, 1, float("inf"))
 
 
-def screen_model(L, cpu, ram, present, rc, rr, stats=None, screen="hc_scan_screen"):
-    """The chosen index (or -1): scan_lanes_screen (or scan_lanes_inv) step by step on 64 lanes."""
-    scr = getattr(L, screen)
+def screen_model(L, cpu, ram, present, rc, rr, stats=None):
+    """The chosen index (or -1): scan_lanes_screen step by step on 64 lanes."""
     N = len(cpu)
     lanes = [{"s": None, "n": -1, "a": 0, "r": 0, "u": float("inf")} for _ in range(64)]
     thr = float("inf")
@@ -98,7 +90,7 @@ def screen_model(L, cpu, ram, present, rc, rr, stats=None, screen="hc_scan_scree
                 a, r = cpu[n], ram[n]
                 if a == st["a"] and r == st["r"]:
                     st["n"] = n
-                elif not scr(a, r, rc, rr, thr):
+                elif not L.hc_scan_screen(a, r, rc, rr, thr):
                     scored += 1
                     s = la(a, r, rc, rr)
                     if st["s"] is None or s >= st["s"]:
@@ -112,16 +104,14 @@ def screen_model(L, cpu, ram, present, rc, rr, stats=None, screen="hc_scan_scree
     return max(best)[1] if best else -1
 
 
-@pytest.mark.parametrize("screen", SCREENS)
-def test_screen_model_matches_reference_argmax(screen):
+def test_screen_model_matches_reference_argmax():
     L = _hc()
     stats = {}
     for seed in range(3):
         for cpu, ram, present, rc, rr in adversarial_problems(seed, N=2048, count=16):
             if rc == 0 or rr == 0:
                 continue
-            assert screen_model(L, cpu, ram, present, rc, rr, stats, screen) == \
-                reference_argmax(cpu, ram, present, rc, rr)
+            assert screen_model(L, cpu, ram, present, rc, rr, stats) == reference_argmax(cpu, ram, present, rc, rr)
     assert stats["scored"] < 0.8 * stats["nodes"]
 
 
