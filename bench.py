@@ -79,6 +79,9 @@ def parse():
     ap.add_argument("--pruned-scan", action="store_true", help="exact block-bound pruned scan (DESIGN.md §3)")
     ap.add_argument("--delay-fifo", type=int, default=0,
                     help="entries per delay-class event ring (k10s_capacities.delay_fifo; 0 = engine default)")
+    ap.add_argument("--score-plugins", choices=("least", "most", "both"), default="least",
+                    help="score plugins of every replica (k10s_replica_params.score_plugins): LeastAllocated "
+                         "(the reference's only one), MostAllocated (extension), or both (weights 1 and 1)")
     ap.add_argument("--profile", action="store_true", help="print the K10S_PROF cycle attribution (variant builds)")
     ap.add_argument("--selftest-host", action="store_true",
                     help="TEST ONLY: run the launcher and the cross-rank reduction on CPU (gloo) over the "
@@ -277,6 +280,11 @@ def main():
     del probe
     # replicas [rank*R, (rank+1)*R) of the job: seed-perturbed copies, or sweep cells (C5)
     params = ensemble.shard_params(defaults, R, rank, base_seed=123, perturb=True, sweep=sweep)
+    plugins = {"least": 1, "most": 2, "both": 3}[args.score_plugins]
+    for p in params:
+        p.score_plugins = plugins
+        if plugins & 2 and p.most_allocated_weight == 0.0:
+            p.most_allocated_weight = 1.0
     t = time.perf_counter()
     caps = Capacities()
     caps.pruned_scan = 1 if args.pruned_scan else 0
@@ -332,10 +340,13 @@ def main():
     value = placements / elapsed
 
     # roofline for the dominant kernel (per launch, this rank's launch time, all-rank bytes / world)
-    per_launch_bytes = (12.0 * scanned + 12.0 * attempts + 12.0 * placements) / (args.steps * world)
+    # 12 B per scanned node (available cpu u32 + ram u64); MostAllocated also reads the node's
+    # capacity (another 12 B)
+    node_b = 12.0 if args.score_plugins == "least" else 24.0
+    per_launch_bytes = (node_b * scanned + 12.0 * attempts + 12.0 * placements) / (args.steps * world)
     achieved = per_launch_bytes / (mean_kernel_ms * 1e-3) if mean_kernel_ms > 0 else 0.0
     # what the scans actually read (pruned scan: block bounds + scanned blocks + bound upkeep)
-    touched_bytes = (12.0 * nread + 12.0 * attempts + 12.0 * placements) / (args.steps * world)
+    touched_bytes = (node_b * nread + 12.0 * attempts + 12.0 * placements) / (args.steps * world)
     traffic = None
     pmc_path = os.path.join(REPO, "profiles", "pmc_run_kernel.json")
     if os.path.exists(pmc_path) and not args.selftest_host:
@@ -344,7 +355,8 @@ def main():
             # only a PMC pass over this exact kernel build, config, workload and scan mode counts
             if pm.get("config") == [R, args.nodes, args.pods] and pm.get("engine") == version() and \
                     pm.get("workload", "c3") == args.workload and \
-                    pm.get("scan_mode") == ("pruned" if args.pruned_scan else "full"):
+                    pm.get("scan_mode") == ("pruned" if args.pruned_scan else "full") and \
+                    pm.get("score_plugins", "least") == args.score_plugins:
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -365,6 +377,7 @@ def main():
                  "seed-perturbed per replica") if not args.selftest_host else "selftest (host-check build on CPU)",
         "config": {"workload": desc, "workload_name": args.workload,
                    "replicas_per_gpu": R, "total_replicas": R * world, "nodes": args.nodes, "pods_per_replica": args.pods,
+                   "score_plugins": args.score_plugins,
                    "parallelism": f"replica-sharded x{world} (RCCL all-reduce of counters and histograms only)"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK, "traffic": traffic,
@@ -414,7 +427,7 @@ def main():
             out["profile"]["by_kind"] = {EVENT_KIND_NAMES.get(k, str(k)): {"count": kn[k], "share_of_loop": kc[k] / loop,
                                                                          "cycles_per_event": kc[k] / max(kn[k], 1)}
                                          for k in range(len(kc)) if kn[k]}
-    if rank == 0 and world == 1 and args.workload == "c3" and not args.no_backlog_line and not args.selftest_host:
+    if rank == 0 and world == 1 and args.workload == "c3" and args.score_plugins == "least" and not args.no_backlog_line and not args.selftest_host:
         # the same replicas under load (failed attempts, unschedulable map, move-all, flush): one launch
         try:
             del eng

@@ -1115,6 +1115,38 @@ K10S_HD double plugin_score(uint32_t ac, uint64_t ar, uint32_t cc, uint64_t cr, 
 #ifndef K10S_SCORE_PLUGINS
 #define K10S_SCORE_PLUGINS 1   // 0: the plugin path is not compiled (k10s_kernels.hip's default copy)
 #endif
+#if K10S_DEVICE
+// plugin_score on the device, bit-identical: the same operations with la_score_d's division (rcp +
+// Newton, exact for these integer operands with quotients in [0, 100]; 0/0 still gives NaN) and
+// (c + r) / 2.0 as an exact halving.
+K10S_D double ma_score_d(uint32_t ac, uint64_t ar, uint32_t cc, uint64_t cr, uint32_t rc, uint64_t rr) {
+    const double cs = div_rn((double)(uint32_t)(cc - ac + rc) * 100.0, (double)cc);
+    const double rs = div_rn(u64_f64((uint64_t)(cr - ar + rr)) * 100.0, u64_f64(cr));
+    return (cs + rs) * 0.5;
+}
+K10S_D double plugin_score_d(uint32_t ac, uint64_t ar, uint32_t cc, uint64_t cr, uint32_t rc, uint64_t rr,
+                             uint32_t plugins, double w_la, double w_ma) {
+    double s = 0.0;
+    if (plugins & K10S_SCORE_LEAST_ALLOCATED) s += la_score_d(ac, ar, rc, rr) * w_la;
+    if (plugins & K10S_SCORE_MOST_ALLOCATED) s += ma_score_d(ac, ar, cc, cr, rc, rr) * w_ma;
+    return s;
+}
+K10S_D void plugin_node(uint32_t n, bool present, uint32_t ac, uint64_t ar, uint32_t cc, uint64_t cr, uint32_t rc,
+                        uint64_t rr, uint32_t plugins, double w_la, double w_ma, int32_t& first, uint64_t& best_key,
+                        int32_t& best_n) {
+    if (present && rc <= ac && rr <= ar) {
+        first = (int32_t)n < first ? (int32_t)n : first;
+        const double s = plugin_score_d(ac, ar, cc, cr, rc, rr, plugins, w_la, w_ma);
+        if (!is_nan(s)) {
+            const uint64_t k = score_key(s);
+            if (k >= best_key) {
+                best_key = k;
+                best_n = (int32_t)n;
+            }
+        }
+    }
+}
+#endif
 K10S_HD int schedule_scan_plugins(Ctx& c, uint32_t rc, uint64_t rr, int32_t* chosen) {
     const uint32_t N = c.S().n_nodes;
     const uint32_t* cpu = c.V().s_cpu();
@@ -1127,6 +1159,37 @@ K10S_HD int schedule_scan_plugins(Ctx& c, uint32_t rc, uint64_t rr, int32_t* cho
     uint64_t best_key = 0;
     int32_t best_n = -1;
     int32_t first = 0x7fffffff;
+#if K10S_DEVICE
+    // each lane owns 4 consecutive nodes per 256-node step, as the LeastAllocated scan: one 16-B
+    // load per u32 array and two per u64 array (sections 256-B aligned and padded; a lane past the
+    // end re-reads nodes 0..3 and grp_bits masks them out); ascending per lane, then the cross-lane
+    // (score_key, index) max reproduces the left-to-right argmax
+    rc = uniform_u32(rc);
+    rr = uniform_u64(rr);
+    const uint32_t l4 = 4u * (uint32_t)lane_id();
+    for (uint32_t base = 0; base < N; base += 256) {
+        const uint32_t n0 = base + l4;
+        const ScanGrp g = scan_load(cpu, ram, pres, N, n0);
+        const uint32_t a = n0 < N ? n0 : 0u;
+        const uint4 cc = *reinterpret_cast<const uint4*>(ccpu + a);
+        const ulonglong2 c01 = *reinterpret_cast<const ulonglong2*>(cram + a);
+        const ulonglong2 c23 = *reinterpret_cast<const ulonglong2*>(cram + a + 2);
+        const uint32_t bits = grp_bits(g, n0, N);
+        if (bits) {
+            plugin_node(n0, bits & 1u, g.cv.x, g.r01.x, cc.x, c01.x, rc, rr, plugins, w_la, w_ma, first, best_key, best_n);
+            plugin_node(n0 + 1, bits & 2u, g.cv.y, g.r01.y, cc.y, c01.y, rc, rr, plugins, w_la, w_ma, first, best_key, best_n);
+            plugin_node(n0 + 2, bits & 4u, g.cv.z, g.r23.x, cc.z, c23.x, rc, rr, plugins, w_la, w_ma, first, best_key, best_n);
+            plugin_node(n0 + 3, bits & 8u, g.cv.w, g.r23.y, cc.w, c23.y, rc, rr, plugins, w_la, w_ma, first, best_key, best_n);
+        }
+    }
+    first = wave_min_i32(first);
+    wave_argmax(best_key, best_n);
+    if (first == 0x7fffffff) return K10S_SCHED_NO_SUFFICIENT_RESOURCES;
+    const uint32_t f = (uint32_t)uniform_u32((uint32_t)first);
+    const double s0 = plugin_score_d(cpu[f], ram[f], ccpu[f], cram[f], rc, rr, plugins, w_la, w_ma);
+    *chosen = is_nan(s0) ? (int32_t)f : best_n;
+    return K10S_SCHED_OK;
+#else
     for (uint32_t n = (uint32_t)lane_id(); n < N; n += K10S_LANES) {
         if (!bit_test(pres, n)) continue;
         const uint32_t ac = cpu[n];
@@ -1150,6 +1213,7 @@ K10S_HD int schedule_scan_plugins(Ctx& c, uint32_t rc, uint64_t rr, int32_t* cho
     const double s0 = plugin_score(cpu[f], ram[f], ccpu[f], cram[f], rc, rr, plugins, w_la, w_ma);
     *chosen = is_nan(s0) ? (int32_t)f : best_n;
     return K10S_SCHED_OK;
+#endif
 }
 
 // ---- block bounds of the scheduler cache and the exact pruned scan ------------------------------

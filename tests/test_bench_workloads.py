@@ -1,0 +1,60 @@
+"""The exact workloads bench.py measures, oracle-checked: the same traces, the same
+bulk scenario path (scenario_bulk + k10s_engine_create_bulk), the same replica count and the same
+per-replica parameters (ensemble.shard_params at the bench seed), with bit-exact oracle replays of
+replicas at the start, middle and end of the batch.  Only the result logs differ from bench.py's
+engine (placements and pod records are kept here so they can be compared); they do not change
+what a replica simulates."""
+import pytest
+
+import oracle_jobs
+import parity
+from kubernetriks_amd import ensemble
+from kubernetriks_amd import workloads as wl
+from kubernetriks_amd.scenario import SimulationConfig, scenario_bulk
+
+R, NODES, PODS, WINDOW = 8192, 4096, 16384, 1200.0   # bench.py defaults
+CHECK = [0, 4095, 8191]
+
+
+def _bench_batch(cluster, workload, check, score_plugins=1):
+    from kubernetriks_amd.native import Engine
+    cfg = SimulationConfig()
+    scn, blob = scenario_bulk(cfg, cluster, workload)
+    defaults = Engine(scn, 1, pods_blob=blob).default_params()
+    params = ensemble.shard_params(defaults, R, 0, base_seed=123, perturb=True)
+    for p in params:
+        p.score_plugins = score_plugins
+        if score_plugins & 2:
+            p.most_allocated_weight = 1.0
+    caps = parity.parity_caps(False)
+    caps.placement_log = PODS + 1024
+    eng = Engine(scn, R, params=params, caps=caps, pods_blob=blob)
+    eng.run_until_all_finished(1e7)
+    ods = oracle_jobs.replay_many([wl.replica_scenario(cfg, cluster, workload, params[r]) for r in check], 1e7)
+    for r, od in zip(check, ods):
+        assert parity.compare(od, eng, r=r, log=False) == [], r
+    res = eng.results()
+    assert all(x["status"] == "finished" for x in res)
+    return res
+
+
+@pytest.mark.gpu
+def test_bench_c3_workload_gpu():
+    cluster, workload = wl.c3_traces(NODES, PODS, WINDOW)
+    res = _bench_batch(cluster, workload, CHECK)
+    assert all(x["counters"]["placements"] == PODS for x in res)
+
+
+@pytest.mark.gpu
+def test_bench_c3_backlog_workload_gpu():
+    cluster, workload = wl.c3_backlog_traces(NODES, PODS, WINDOW)
+    res = _bench_batch(cluster, workload, CHECK)
+    # the regime it is there for: failed attempts and unschedulable-map traffic in every replica
+    assert all(x["counters"]["attempts"] > x["counters"]["placements"] for x in res)
+
+
+@pytest.mark.gpu
+def test_bench_c3_most_allocated_gpu():
+    """bench.py --score-plugins both (LeastAllocated + MostAllocated, weights 1 and 1)."""
+    cluster, workload = wl.c3_traces(NODES, PODS, WINDOW)
+    _bench_batch(cluster, workload, [0, 8191], score_plugins=3)
