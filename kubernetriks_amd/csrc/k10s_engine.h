@@ -367,10 +367,7 @@ K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uin
             } else {
                 c.V().fq()[(uint32_t)cls * cap + (tl & (cap - 1))] = e;
             }
-            if (tl == hd) {  // the ring was empty: this event is its new head (source list update)
-                H.fq_top[cls] = e;
-                sl_mark(H, (uint32_t)cls);
-            }
+            if (tl == hd) sl_mark(H, (uint32_t)cls);  // the ring was empty: a new head (source list)
             H.fq_tail[cls] = tl + 1;
             H.fq_last[cls] = e.time;
             H.next_seq = e.seq + 1;
@@ -2847,8 +2844,9 @@ K10S_HD bool src_head(Ctx& c, uint32_t q, uint32_t ntr, int64_t& k, uint32_t& s)
     const RepHdr& H = c.H();
     if (q < (uint32_t)K10S_NFQ) {
         const uint32_t hd = H.fq_head[q], tl = H.fq_tail[q];
-        k = total_key(H.fq_top[q].time);
-        s = H.fq_top[q].seq;
+        const HeapEv& t = H.fq_win[q * K10S_FQW + (hd & (K10S_FQW - 1))];
+        k = total_key(t.time);
+        s = t.seq;
         return hd != tl;
     }
     if (q == (uint32_t)SRC_TRACE) {
@@ -2976,8 +2974,7 @@ K10S_HD void consume_source(Ctx& c, int src, uint32_t ntr) {
         has = hd != tl;
         if (has) {
             if (hd == we) fq_refill(c, src, hd);
-            const HeapEv t = H.fq_win[(uint32_t)src * K10S_FQW + (hd & (K10S_FQW - 1))];
-            H.fq_top[src] = t;
+            const HeapEv& t = H.fq_win[(uint32_t)src * K10S_FQW + (hd & (K10S_FQW - 1))];
             key = total_key(t.time);
             seq = t.seq;
         }
@@ -3210,12 +3207,12 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
 #endif
             } else {
 #if K10S_EV_BYREF
-                ep = K10S_EVREF(&h->fq_top[src]);
+                ep = K10S_EVREF(&h->fq_win[(uint32_t)src * K10S_FQW + (uniform_u32(h->fq_head[src]) & (K10S_FQW - 1))]);
                 e.time = uniform_f64(ep->time);
                 e.seq = uniform_u32(ep->seq);
                 e.kind = (uint16_t)uniform_u32(ep->kind);
 #else
-                e = h->fq_top[src];
+                e = h->fq_win[(uint32_t)src * K10S_FQW + (h->fq_head[src] & (K10S_FQW - 1))];
                 uniform_event(e);
 #endif
             }

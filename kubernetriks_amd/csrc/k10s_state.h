@@ -224,12 +224,12 @@ struct RepHdr {
     uint32_t cur_kind, cur_seq;   // event being handled (panic attribution)
     uint32_t gauge_n;             // gauge rows recorded
     uint64_t g_cur_nodes, g_cur_pods, g_pods_q;   // GaugeMetrics counters (collector.rs:169-190)
-    // event queue: delay-class FIFO rings (head/tail counters, newest time, cached head entries)
-    // and the cached root of the heap (valid while heap_size > 0)
+    // event queue: delay-class FIFO rings (head/tail counters, newest time; a non-empty ring's head
+    // entry is fq_win[ring * K10S_FQW + (fq_head & (K10S_FQW - 1))]) and the cached root of the
+    // heap (valid while heap_size > 0)
     uint32_t fq_head[K10S_NFQ], fq_tail[K10S_NFQ];
     uint32_t fq_wend[K10S_NFQ];   // the window holds ring positions [fq_head, fq_wend)
     double fq_last[K10S_NFQ];
-    HeapEv fq_top[K10S_NFQ];
     HeapEv heap_top;
     HeapEv cur_ev;                // a trace event being handled (k10s_engine.h K10S_EV_BYREF)
     double tr_time;               // cached head of the shared trace stream (valid while

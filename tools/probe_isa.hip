@@ -23,7 +23,8 @@ __global__ __launch_bounds__(64) void probe_dispatch(uint32_t a, uint32_t b, dou
     e.b = b;
     e.x = x;
     uniform_event(e);
-    dispatch(c, e);
+    c.H().cur_ev = e;
+    dispatch(c, K10S_EVREF(&c.H().cur_ev), (uint32_t)K);
 }
 
 __global__ __launch_bounds__(64) void probe_sl_update(uint32_t q, int64_t key, uint32_t seq) {

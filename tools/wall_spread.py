@@ -34,11 +34,11 @@ def main():
     import bench
     from kubernetriks_amd import ensemble
     from kubernetriks_amd.native import Capacities, Engine
-    from kubernetriks_amd.scenario import SimulationConfig, scenario_bulk
-    cluster, workload, desc = bench.build_workload(a)
-    scn, blob = scenario_bulk(SimulationConfig(), cluster, workload)
+    from kubernetriks_amd.scenario import scenario_bulk
+    cfg, cluster, workload, desc, sweep = bench.build_workload(a)
+    scn, blob = scenario_bulk(cfg, cluster, workload)
     probe = Engine(scn, 1, pods_blob=blob)
-    params = ensemble.shard_params(probe.default_params(), a.replicas, 0, base_seed=123, perturb=True)
+    params = ensemble.shard_params(probe.default_params(), a.replicas, 0, base_seed=123, perturb=True, sweep=sweep)
     del probe
     eng = Engine(scn, a.replicas, params=params, caps=Capacities(), pods_blob=blob)
     eng.run_until_all_finished(max_time=1e7)      # warm-up launch
