@@ -197,6 +197,23 @@ def cpu_baseline(args, cfg, cluster, workload, params):
 
 
 # ---- the measurement ------------------------------------------------------------------------------
+def pmc_traffic(workload, R, nodes, pods, pruned, score_plugins, engine):
+    """HBM bytes per launch of k10s_run_kernel from the committed rocprofv3 PMC summary of this
+    workload (profiles/pmc_run_kernel.json for c3, pmc_run_kernel_<workload>.json otherwise;
+    tools/pmc_summary.py), only if it was taken on this exact engine build, config, scan mode and
+    score plugins; else None."""
+    name = "pmc_run_kernel.json" if workload == "c3" else f"pmc_run_kernel_{workload}.json"
+    try:
+        pm = json.load(open(os.path.join(REPO, "profiles", name)))
+    except Exception:
+        return None
+    if pm.get("config") == [R, nodes, pods] and pm.get("engine") == engine and \
+            pm.get("workload", "c3") == workload and pm.get("scan_mode") == ("pruned" if pruned else "full") and \
+            pm.get("score_plugins", "least") == score_plugins:
+        return pm.get("hbm_bytes_per_launch")
+    return None
+
+
 def build_workload(args):
     """(config, cluster trace, workload trace, description, sweep) of the selected workload."""
     from kubernetriks_amd import workloads as wl
@@ -340,27 +357,17 @@ def main():
     value = placements / elapsed
 
     # roofline for the dominant kernel (per launch, this rank's launch time, all-rank bytes / world)
-    # 12 B per scanned node (available cpu u32 + ram u64); MostAllocated also reads the node's
-    # capacity (another 12 B)
-    node_b = 12.0 if args.score_plugins == "least" else 24.0
-    per_launch_bytes = (node_b * scanned + 12.0 * attempts + 12.0 * placements) / (args.steps * world)
+    # per scanned node: the node-cache entry (8 B packed cpu << 40 | ram, 12 B wide u32 + u64;
+    # k10s_capacities.node_cache); MostAllocated also reads the node's capacity (12 B, wide only).
+    # Per attempt the pod's request (12 B); per placement the entry's reservation write.
+    entry_b = float(eng.node_entry_bytes)
+    node_b = entry_b + (0.0 if args.score_plugins == "least" else 12.0)
+    per_launch_bytes = (node_b * scanned + 12.0 * attempts + entry_b * placements) / (args.steps * world)
     achieved = per_launch_bytes / (mean_kernel_ms * 1e-3) if mean_kernel_ms > 0 else 0.0
     # what the scans actually read (pruned scan: block bounds + scanned blocks + bound upkeep)
-    touched_bytes = (node_b * nread + 12.0 * attempts + 12.0 * placements) / (args.steps * world)
-    traffic = None
-    pmc_path = os.path.join(REPO, "profiles", "pmc_run_kernel.json")
-    if os.path.exists(pmc_path) and not args.selftest_host:
-        try:
-            pm = json.load(open(pmc_path))
-            # only a PMC pass over this exact kernel build, config, workload and scan mode counts
-            if pm.get("config") == [R, args.nodes, args.pods] and pm.get("engine") == version() and \
-                    pm.get("workload", "c3") == args.workload and \
-                    pm.get("scan_mode") == ("pruned" if args.pruned_scan else "full") and \
-                    pm.get("score_plugins", "least") == args.score_plugins:
-                traffic = pm.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-
+    touched_bytes = (node_b * nread + 12.0 * attempts + entry_b * placements) / (args.steps * world)
+    traffic = None if args.selftest_host else pmc_traffic(args.workload, R, args.nodes, args.pods, args.pruned_scan,
+                                                            args.score_plugins, version())
     out = {
         "metric": METRIC,
         "value": value,
@@ -377,7 +384,7 @@ def main():
                  "seed-perturbed per replica") if not args.selftest_host else "selftest (host-check build on CPU)",
         "config": {"workload": desc, "workload_name": args.workload,
                    "replicas_per_gpu": R, "total_replicas": R * world, "nodes": args.nodes, "pods_per_replica": args.pods,
-                   "score_plugins": args.score_plugins,
+                   "score_plugins": args.score_plugins, "node_entry_bytes": int(entry_b),
                    "parallelism": f"replica-sharded x{world} (RCCL all-reduce of counters and histograms only)"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK, "traffic": traffic,
@@ -464,14 +471,17 @@ def backlog_line(args, cfg, make_engine, caps, ensemble, num_counters, version):
     elapsed = time.perf_counter() - t0
     c = eng.counter_matrix().sum(axis=0, dtype=np.uint64).astype(np.int64)
     placements, attempts, scanned = int(c[12]), int(c[13]), int(c[15])
-    per_launch = 12.0 * scanned + 12.0 * attempts + 12.0 * placements
+    entry_b = float(eng.node_entry_bytes)
+    per_launch = entry_b * scanned + 12.0 * attempts + entry_b * placements
     achieved = per_launch / (ms * 1e-3) if ms > 0 else 0.0
     log(f"backlog: {placements / elapsed / 1e6:.2f} M placements/s, run {ms:.1f} ms")
     return {"workload": desc, "workload_name": "c3_backlog", "steps": 1, "warmup": 0,
             "placements_per_s": placements / elapsed, "attempts_per_s": attempts / elapsed,
             "ms_per_step": elapsed * 1e3, "kernel_ms_per_launch": ms,
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK, "algorithmic_bytes_per_launch": per_launch},
+                         "frac": achieved / HBM_PEAK, "algorithmic_bytes_per_launch": per_launch,
+                         "traffic": pmc_traffic("c3_backlog", args.replicas, args.nodes, args.pods, args.pruned_scan,
+                                                "least", version())},
             "totals": {"placements": placements, "attempts": attempts, "requeued": int(c[17]), "flushed": int(c[18])},
             "engine": version()}
 

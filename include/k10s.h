@@ -83,6 +83,9 @@ extern "C" {
 #define K10S_ERR_NAME_BOUND 102            /* engine capacity: generated-name universe bound */
 #define K10S_ERR_SEQ_OVERFLOW 103          /* engine capacity: 2^32 event ids in one replica */
 #define K10S_ERR_CA_BUFFER 104             /* engine capacity: CA action buffer */
+#define K10S_ERR_NODE_CACHE_RANGE 105      /* engine capacity: a packed node-cache entry would exceed its
+                                              field (allocatable cpu >= 2^24 or ram >= 2^40 after a
+                                              release; cannot happen while allocatable <= capacity) */
 
 /* ---- counters (printer.rs:90-101 + engine throughput counters) ---------------------------- */
 enum k10s_counter {
@@ -189,7 +192,17 @@ typedef struct k10s_capacities {
     uint32_t stall_guard;                /* 1 = stop a run-until-all-finished replica that can no longer
                                             make progress with K10S_REPLICA_STALLED; 0 = off (reference
                                             behaviour: it runs to max_time) */
+    uint32_t node_cache;                 /* layout of the scheduler's node cache (the scan target):
+                                            K10S_NODE_CACHE_AUTO (0) = packed, one u64 per node (cpu in
+                                            bits 40-63, ram in bits 0-39: 8 B per node and scan), when
+                                            every node definition has cpu < 2^24 and ram < 2^40, no
+                                            replica uses a score plugin beyond LeastAllocated and
+                                            pruned_scan is off; otherwise wide.  K10S_NODE_CACHE_WIDE (1)
+                                            = always the u32 cpu + u64 ram SoA (12 B per node).  Results
+                                            are identical either way. */
 } k10s_capacities;
+#define K10S_NODE_CACHE_AUTO 0u
+#define K10S_NODE_CACHE_WIDE 1u
 
 /* One row of the gauge recorder (MetricsCollector::record_gauge_metrics, collector.rs:352-407,
    written every 5 s of simulated time as the reference's gauge CSV).  The two node averages sum
@@ -339,6 +352,9 @@ const char* k10s_engine_group_name(const k10s_engine* e, uint32_t idx);
 /* Per-replica device-state footprint in bytes and device pointer of replica r's scheduler
    cache SoA (for profiling tools). */
 uint64_t k10s_engine_replica_bytes(const k10s_engine* e);
+/* Bytes per node of the scheduler's node cache that every scheduling attempt reads: 8 (packed) or
+   12 (wide: u32 cpu + u64 ram); see k10s_capacities.node_cache.  0 for a null engine. */
+uint32_t k10s_engine_node_entry_bytes(const k10s_engine* e);
 
 /* Tooling: per-replica cycle attribution of the event loop, 8 words per replica
    (loop, select, consume, dispatch, scheduling cycle, scan, scans, bound maintenance; s_memtime

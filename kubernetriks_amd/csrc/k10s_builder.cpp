@@ -742,9 +742,16 @@ std::string params_error(const Params& p, const HostScenario& hs) {
     return "";
 }
 
-Layout make_layout(const HostScenario& hs, const k10s_capacities& caps) {
+bool nodes_packable(const HostScenario& hs) {
+    for (size_t d = 0; d < hs.def_cpu.size(); d++)
+        if (hs.def_cpu[d] >= (1u << 24) || hs.def_ram[d] >= (1ull << 40)) return false;
+    return true;
+}
+
+Layout make_layout(const HostScenario& hs, const k10s_capacities& caps, bool allow_packed) {
     Layout L;
     std::memset(&L, 0, sizeof L);
+    L.packed = (allow_packed && caps.node_cache == K10S_NODE_CACHE_AUTO && !caps.pruned_scan && nodes_packable(hs)) ? 1u : 0u;
     const uint64_t N = hs.n_nodes, P = hs.n_pods, S = hs.n_slots, G = hs.group_names.size(),
                    CG = hs.ca_group_names.size();
     L.words_nodes = (uint32_t)((N + 63) / 64);
@@ -779,11 +786,13 @@ Layout make_layout(const HostScenario& hs, const k10s_capacities& caps) {
     };
     L.hdr = take(sizeof(RepHdr));
     // hot scheduler-cache SoA first (the scan target), then per-entity records
-    L.s_cpu = take(4 * N);
-    L.s_ram = take(8 * N);
+    const uint64_t wide = L.packed ? 0 : 1;
+    L.s_node = take(L.packed ? 8 * N : 0);
+    L.s_cpu = take(wide * 4 * N);
+    L.s_ram = take(wide * 8 * N);
     L.s_present = take(8 * (uint64_t)L.words_nodes);
-    L.s_ccpu = take(4 * N);
-    L.s_cram = take(8 * N);
+    L.s_ccpu = take(wide * 4 * N);   // capacities: MostAllocated only (wide layout)
+    L.s_cram = take(wide * 8 * N);
     L.pruned = caps.pruned_scan ? 1u : 0u;
     L.stall = caps.stall_guard ? 1u : 0u;
     L.bshift = 6;

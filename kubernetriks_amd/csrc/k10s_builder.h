@@ -70,7 +70,11 @@ bool build_scenario(const std::string& text, uint32_t group_bound, uint32_t ca_b
 std::vector<uint8_t> pack_scenario(const HostScenario& hs, Scenario& view_offsets);
 Scenario rebase_scenario(const Scenario& view_offsets, const uint8_t* base);
 
-Layout make_layout(const HostScenario& hs, const k10s_capacities& caps);
+// allow_packed: false when some replica needs the wide node cache (a score plugin beyond
+// LeastAllocated: the plugin kernel reads capacities from the wide SoA).
+Layout make_layout(const HostScenario& hs, const k10s_capacities& caps, bool allow_packed);
+// Every node definition fits the packed node-cache entry (cpu < 2^24, ram < 2^40).
+bool nodes_packable(const HostScenario& hs);
 
 // Caller-supplied replica parameters the engine cannot run: "" when valid, else the reason.
 std::string params_error(const Params& p, const HostScenario& hs);

@@ -76,6 +76,7 @@ struct Rep {
     template <typename T>
     K10S_HD T* at(uint64_t off) const { return (T*)(b + off); }
     K10S_HD RepHdr* h() const { return at<RepHdr>(L().hdr); }
+    K10S_HD uint64_t* s_node() const { return at<uint64_t>(L().s_node); }
     K10S_HD uint32_t* s_cpu() const { return at<uint32_t>(L().s_cpu); }
     K10S_HD uint64_t* s_ram() const { return at<uint64_t>(L().s_ram); }
     K10S_HD uint64_t* s_present() const { return at<uint64_t>(L().s_present); }
@@ -156,6 +157,79 @@ K10S_HD void fail(Ctx& c, uint32_t code) {
         h.error_seq = h.cur_seq;
         h.error_time = h.clock;
     }
+}
+
+// ---- the scheduler's node cache (allocatable per node in name order: the scan target) -----------
+// Two layouts of the same values (Layout.packed, chosen per engine by make_layout):
+//  * packed: one u64 per node, cpu in bits 40..63, ram in bits 0..39 (every node definition of the
+//    scenario has cpu < 2^24 and ram < 2^40, and allocatable <= capacity), so a scan streams 8 B
+//    per node instead of 12 and a reservation is one 64-bit subtraction;
+//  * wide: the u32 cpu + u64 ram SoA (larger nodes, pruned scans, and the score-plugin kernel, which
+//    also reads the capacity SoA).
+// Device: k10s_kernels.hip is compiled packed-only and k10s_kernels_plugins.hip wide-only
+// (K10S_PACKED); the host check build follows the layout at run time.
+#define K10S_PK_SHIFT 40
+#define K10S_PK_RAM ((1ull << K10S_PK_SHIFT) - 1)
+#define K10S_PK_CPU ((1u << (64 - K10S_PK_SHIFT)) - 1)
+#if K10S_DEVICE
+#ifndef K10S_PACKED
+#define K10S_PACKED 1
+#endif
+K10S_HD constexpr bool nc_packed(const Ctx&) { return K10S_PACKED != 0; }
+#else
+inline bool nc_packed(const Ctx& c) { return c.Ly().packed != 0; }
+#endif
+struct NcEnt {
+    uint32_t cpu;
+    uint64_t ram;
+};
+K10S_HD uint64_t nc_pack(uint32_t cpu, uint64_t ram) { return ((uint64_t)cpu << K10S_PK_SHIFT) | ram; }
+K10S_HD NcEnt nc_unpack(uint64_t x) {
+    NcEnt v;
+    v.cpu = (uint32_t)(x >> K10S_PK_SHIFT);
+    v.ram = x & K10S_PK_RAM;
+    return v;
+}
+K10S_HD NcEnt nc_get(Ctx& c, uint32_t n) {
+    if (nc_packed(c)) return nc_unpack(c.V().s_node()[n]);
+    NcEnt v;
+    v.cpu = c.V().s_cpu()[n];
+    v.ram = c.V().s_ram()[n];
+    return v;
+}
+// (cpu, ram) must fit the packed fields when packed (every caller stores allocatable <= capacity,
+// or 0, or checks with nc_release)
+K10S_HD void nc_put(Ctx& c, uint32_t n, NcEnt v) {
+    if (nc_packed(c)) {
+        c.V().s_node()[n] = nc_pack(v.cpu, v.ram);
+    } else {
+        c.V().s_cpu()[n] = v.cpu;
+        c.V().s_ram()[n] = v.ram;
+    }
+}
+// reserve_node_resources (scheduler.rs:118-123) after Fit: request <= allocatable, no borrow
+K10S_HD void nc_reserve(Ctx& c, uint32_t n, uint32_t rc, uint64_t rr) {
+    if (nc_packed(c)) {
+        c.V().s_node()[n] -= nc_pack(rc, rr);
+    } else {
+        c.V().s_cpu()[n] -= rc;
+        c.V().s_ram()[n] -= rr;
+    }
+}
+// release_node_resources (scheduler.rs:153-162) onto entry v of node n: false (and the replica
+// stops with K10S_ERR_NODE_CACHE_RANGE) if a packed field would overflow
+K10S_HD bool nc_release(Ctx& c, uint32_t n, NcEnt v, uint32_t rc, uint64_t rr) {
+    if (nc_packed(c)) {
+        if (rc > K10S_PK_CPU - v.cpu || rr > K10S_PK_RAM - v.ram) {
+            fail(c, K10S_ERR_NODE_CACHE_RANGE);
+            return false;
+        }
+        c.V().s_node()[n] = nc_pack(v.cpu + rc, v.ram + rr);
+    } else {
+        c.V().s_cpu()[n] = v.cpu + rc;
+        c.V().s_ram()[n] = v.ram + rr;
+    }
+    return true;
 }
 
 // Broadcast an event loaded by vector loads to scalar registers: every field is wave-uniform by
@@ -740,6 +814,31 @@ K10S_D ScanGrp scan_load_np(const uint32_t* s_cpu, const uint64_t* s_ram, uint32
     g.r23 = *reinterpret_cast<const ulonglong2*>(s_ram + a + 2);
     return g;
 }
+// The packed node cache (nc_*): a lane's 4 consecutive u64 entries (two 16-B loads, 32 B instead of
+// 48), split into the same (cpu, ram) group the wide loads give.  PRES: read the presence word.
+K10S_D ScanGrp scan_load_pk(const uint64_t* s_node, const uint64_t* present, uint32_t n_nodes, uint32_t n0,
+                            bool pres) {
+    const uint32_t a = n0 < n_nodes ? n0 : 0u;
+    ScanGrp g;
+    g.pw = pres ? present[a >> 6] : ~0ull;
+    const ulonglong2 x01 = *reinterpret_cast<const ulonglong2*>(s_node + a);
+    const ulonglong2 x23 = *reinterpret_cast<const ulonglong2*>(s_node + a + 2);
+    g.cv.x = (uint32_t)(x01.x >> K10S_PK_SHIFT);
+    g.cv.y = (uint32_t)(x01.y >> K10S_PK_SHIFT);
+    g.cv.z = (uint32_t)(x23.x >> K10S_PK_SHIFT);
+    g.cv.w = (uint32_t)(x23.y >> K10S_PK_SHIFT);
+    g.r01.x = x01.x & K10S_PK_RAM;
+    g.r01.y = x01.y & K10S_PK_RAM;
+    g.r23.x = x23.x & K10S_PK_RAM;
+    g.r23.y = x23.y & K10S_PK_RAM;
+    return g;
+}
+// PK: s_ram is the packed node array (s_cpu unused)
+template <bool PK>
+K10S_D ScanGrp scan_load_x(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
+                           uint32_t n0) {
+    return PK ? scan_load_pk(s_ram, present, n_nodes, n0, true) : scan_load(s_cpu, s_ram, present, n_nodes, n0);
+}
 K10S_D uint32_t grp_bits(const ScanGrp& g, uint32_t n0, uint32_t n_nodes) {
     if (n0 >= n_nodes) return 0;
     const uint32_t valid = n_nodes - n0;
@@ -832,7 +931,7 @@ K10S_D void scan_grp(const ScanGrp& g, uint32_t n0, uint32_t n_nodes, uint32_t r
         scan_node_d<W1, TF>(n0 + 3, bits & 8u, g.cv.w, g.r23.y, rc, rr, frc, frr, weight, first, best_s, best_n);
     }
 }
-template <bool W1, bool TF, int PIPE>
+template <bool W1, bool TF, int PIPE, bool PK = false>
 K10S_D void scan_lanes(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
                        uint32_t rc, uint64_t rr, double weight, int32_t& first, double& best_s, int32_t& best_n) {
     const uint32_t l4 = 4u * (uint32_t)lane_id();
@@ -844,9 +943,9 @@ K10S_D void scan_lanes(const uint32_t* s_cpu, const uint64_t* s_ram, const uint6
     // Software pipeline: loads run PIPE steps (of 256 nodes) ahead of the arithmetic.
     ScanGrp g[PIPE + 1];
 #pragma unroll
-    for (int i = 0; i < PIPE; i++) g[i] = scan_load(s_cpu, s_ram, present, n_nodes, 256u * i + l4);
+    for (int i = 0; i < PIPE; i++) g[i] = scan_load_x<PK>(s_cpu, s_ram, present, n_nodes, 256u * i + l4);
     for (uint32_t base = 0; base < n_nodes; base += 256) {
-        g[PIPE] = scan_load(s_cpu, s_ram, present, n_nodes, base + 256u * PIPE + l4);
+        g[PIPE] = scan_load_x<PK>(s_cpu, s_ram, present, n_nodes, base + 256u * PIPE + l4);
         scan_grp<W1, TF>(g[0], base + l4, n_nodes, rc, rr, frc, frr, weight, first, best_s, best_n);
 #pragma unroll
         for (int i = 0; i < PIPE; i++) g[i] = g[i + 1];
@@ -983,13 +1082,15 @@ K10S_D float wave_min_f32(float v) {
 #endif
 // NP: the event loop's own node cache (absent nodes hold (0, 0): no presence words read); the unit
 // surface's caller-owned buffers keep their presence bitmap.
-#define SCREEN_LOAD(c, r, p, n, n0) ((NP && K10S_SCREEN_NO_PRESENCE) ? scan_load_np(c, r, n, n0) : scan_load(c, r, p, n, n0))
+#define SCREEN_LOAD(c, r, p, n, n0)                                                                   \
+    (PK ? scan_load_pk(r, p, n, n0, !(NP && K10S_SCREEN_NO_PRESENCE))                                  \
+        : ((NP && K10S_SCREEN_NO_PRESENCE) ? scan_load_np(c, r, n, n0) : scan_load(c, r, p, n, n0)))
 // K10S_UNIT_SCREEN (default 1): the unit surface (k10s_schedule_kernel) screens too.  Scoring every
 // node exactly (two f64 divisions) made it VALU-bound below the HBM roofline.
 #ifndef K10S_UNIT_SCREEN
 #define K10S_UNIT_SCREEN 1
 #endif
-template <int PIPE, bool NP = true>
+template <int PIPE, bool NP = true, bool PK = false>
 K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
                               uint32_t rc, uint64_t rr, double& best_s, int32_t& best_n) {
     const uint32_t l4 = 4u * (uint32_t)lane_id();
@@ -1043,7 +1144,8 @@ K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, cons
 #endif
 
 // LOOP: the event loop's scans (K10S_LOOP_SCAN_PIPE) rather than the unit surface's (K10S_SCAN_PIPE).
-template <bool LOOP = false>
+// PK: s_ram is the packed node array (nc_*), s_cpu is not read.
+template <bool LOOP = false, bool PK = false>
 K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
                           uint32_t rc, uint64_t rr, double weight, int32_t* chosen) {
     uint64_t best_key = 0;
@@ -1056,12 +1158,12 @@ K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const ui
         // score is a finite number >= 0: filtered[0] is never NaN, "some node fits" <=> best_n >= 0,
         // and neither filtered[0] nor its re-scored value is needed (kube_scheduler.rs:140-148).
         if (LOOP && K10S_SCAN_SCREEN)
-            scan_lanes_screen<K10S_LOOP_SCAN_PIPE, true>(s_cpu, s_ram, present, n_nodes, rc, rr, best_s, best_n);
+            scan_lanes_screen<K10S_LOOP_SCAN_PIPE, true, PK>(s_cpu, s_ram, present, n_nodes, rc, rr, best_s, best_n);
         else if (!LOOP && K10S_UNIT_SCREEN)
-            scan_lanes_screen<K10S_SCAN_PIPE, false>(s_cpu, s_ram, present, n_nodes, rc, rr, best_s, best_n);
+            scan_lanes_screen<K10S_SCAN_PIPE, false, PK>(s_cpu, s_ram, present, n_nodes, rc, rr, best_s, best_n);
         else
-            scan_lanes<true, false, LOOP ? K10S_LOOP_SCAN_PIPE : K10S_SCAN_PIPE>(s_cpu, s_ram, present, n_nodes, rc,
-                                                                                rr, weight, first, best_s, best_n);
+            scan_lanes<true, false, LOOP ? K10S_LOOP_SCAN_PIPE : K10S_SCAN_PIPE, PK>(s_cpu, s_ram, present, n_nodes, rc,
+                                                                                    rr, weight, first, best_s, best_n);
         best_key = best_n >= 0 ? score_key(best_s) : 0;
         wave_argmax(best_key, best_n);
         if (best_n < 0) return K10S_SCHED_NO_SUFFICIENT_RESOURCES;
@@ -1069,18 +1171,22 @@ K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const ui
         return K10S_SCHED_OK;
     }
     constexpr int P = LOOP ? K10S_LOOP_SCAN_PIPE : K10S_SCAN_PIPE;
-    if (weight == 1.0) scan_lanes<true, true, P>(s_cpu, s_ram, present, n_nodes, rc, rr, weight, first, best_s, best_n);
-    else scan_lanes<false, true, P>(s_cpu, s_ram, present, n_nodes, rc, rr, weight, first, best_s, best_n);
+    if (weight == 1.0) scan_lanes<true, true, P, PK>(s_cpu, s_ram, present, n_nodes, rc, rr, weight, first, best_s, best_n);
+    else scan_lanes<false, true, P, PK>(s_cpu, s_ram, present, n_nodes, rc, rr, weight, first, best_s, best_n);
     best_key = best_n >= 0 ? score_key(best_s) : 0;
 #else
-    for (uint32_t n = 0; n < n_nodes; n++)
-        if ((present[n >> 6] >> (n & 63)) & 1ull) scan_node(n, s_cpu[n], s_ram[n], rc, rr, weight, first, best_key, best_n);
+    for (uint32_t n = 0; n < n_nodes; n++) {
+        if (!((present[n >> 6] >> (n & 63)) & 1ull)) continue;
+        const NcEnt v = PK ? nc_unpack(s_ram[n]) : NcEnt{s_cpu[n], s_ram[n]};
+        scan_node(n, v.cpu, v.ram, rc, rr, weight, first, best_key, best_n);
+    }
 #endif
     first = wave_min_i32(first);
     wave_argmax(best_key, best_n);
     if (first == 0x7fffffff) return K10S_SCHED_NO_SUFFICIENT_RESOURCES;
     // kube_scheduler.rs:140-148: start from filtered[0]; if its score is NaN nothing replaces it
-    double s0 = 0.0 + la_score(s_cpu[first], s_ram[first], rc, rr) * weight;
+    const NcEnt v0 = PK ? nc_unpack(s_ram[first]) : NcEnt{s_cpu[first], s_ram[first]};
+    double s0 = 0.0 + la_score(v0.cpu, v0.ram, rc, rr) * weight;
     *chosen = is_nan(s0) ? first : best_n;
     return K10S_SCHED_OK;
 }
@@ -1249,7 +1355,7 @@ K10S_HD void block_recompute(Ctx& c, uint32_t b) {
     c.H().counters[K10S_C_NODES_READ] += hi - lo;
 }
 K10S_HD void node_bound_changed(Ctx& c, uint32_t n) {
-    if (!c.Ly().pruned) return;
+    if (nc_packed(c) || !c.Ly().pruned) return;   // bounds: pruned scans only, wide layout only
     const uint64_t t0 = prof_now();
     block_recompute(c, n >> c.Ly().bshift);
     K10S_PROF_ADD(c, PROF_BOUNDS, t0);
@@ -1397,12 +1503,16 @@ K10S_CYCLE_FN void run_scheduling_cycle_t(Ctx& c, double t) {
             if (PLUG) {
                 st = schedule_scan_plugins(c, rc, rr, &chosen);
                 nread = c.S().n_nodes;
-            } else if (c.Ly().pruned && w == 1.0 && rc > 0 && rr > 0) {
+            } else if (!nc_packed(c) && c.Ly().pruned && w == 1.0 && rc > 0 && rr > 0) {
                 st = schedule_scan_pruned(c, rc, rr, &chosen, &nread);
             }
             if (st < 0) {
-                st = schedule_scan<true>(c.V().s_cpu(), c.V().s_ram(), c.V().s_present(), c.S().n_nodes, rc, rr, w,
-                                         &chosen);
+                if (nc_packed(c))
+                    st = schedule_scan<true, true>(nullptr, c.V().s_node(), c.V().s_present(), c.S().n_nodes, rc, rr,
+                                                   w, &chosen);
+                else
+                    st = schedule_scan<true, false>(c.V().s_cpu(), c.V().s_ram(), c.V().s_present(), c.S().n_nodes, rc,
+                                                    rr, w, &chosen);
                 nread = c.S().n_nodes;
             }
             h->counters[K10S_C_NODES_READ] += nread;
@@ -1416,8 +1526,7 @@ K10S_CYCLE_FN void run_scheduling_cycle_t(Ctx& c, double t) {
             continue;
         }
         uint32_t n = (uint32_t)chosen;
-        c.V().s_cpu()[n] -= rc;  // reserve_node_resources (118-123)
-        c.V().s_ram()[n] -= rr;
+        nc_reserve(c, n, rc, rr);  // reserve_node_resources (118-123)
         node_bound_changed(c, n);
         c.V().node(n).flags |= NF_S_ASSIGN;  // assign_node_to_pod (125-151)
         c.V().pod(p).s_assigned = (int32_t)n;
@@ -1473,8 +1582,7 @@ K10S_HD void s_release(Ctx& c, uint32_t p) {  // release_node_resources (153-162
         fail(c, K10S_PANIC_MISSING_NODE);
         return;
     }
-    c.V().s_cpu()[n] += c.V().pod(p).req_cpu;
-    c.V().s_ram()[n] += c.V().pod(p).req_ram;
+    if (!nc_release(c, (uint32_t)n, nc_get(c, (uint32_t)n), c.V().pod(p).req_cpu, c.V().pod(p).req_ram)) return;
     node_bound_changed(c, (uint32_t)n);
 }
 
@@ -1502,12 +1610,14 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
         uint32_t n = e.a;
         uint32_t ac = e.b;
         uint64_t ar = f2u(e.x);
-        c.V().s_cpu()[n] = ac;
-        c.V().s_ram()[n] = ar;
+        const NcEnt cap = {ac, ar};
+        nc_put(c, n, cap);
         // the stored node's capacity: a node reaches the scheduler straight from its creation,
-        // allocatable = capacity (node.rs:60-66); only MostAllocated reads it
-        c.V().s_ccpu()[n] = ac;
-        c.V().s_cram()[n] = ar;
+        // allocatable = capacity (node.rs:60-66); only MostAllocated reads it (wide layout)
+        if (!nc_packed(c)) {
+            c.V().s_ccpu()[n] = ac;
+            c.V().s_cram()[n] = ar;
+        }
         if (!bit_test(c.V().s_present(), n)) {
             bit_set(c.V().s_present(), n);
             h->s_node_count += 1;
@@ -1540,8 +1650,7 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
         const uint64_t rr = P.req_ram;
         const uint8_t nf = c.V().node(n).flags;
         const bool n_present = bit_test(c.V().s_present(), n);
-        const uint32_t n_cpu = c.V().s_cpu()[n];
-        const uint64_t n_ram = c.V().s_ram()[n];
+        const NcEnt nv = nc_get(c, n);
         if (!(pf & PF_IN_S)) {
             fail(c, K10S_PANIC_MISSING_POD);
             return;
@@ -1557,13 +1666,7 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
             fail(c, K10S_PANIC_MISSING_NODE);
             return;
         }
-        if (sa == (int32_t)n) {
-            c.V().s_cpu()[n] = n_cpu + rc;
-            c.V().s_ram()[n] = n_ram + rr;
-        } else {
-            c.V().s_cpu()[sa] += rc;
-            c.V().s_ram()[sa] += rr;
-        }
+        if (!nc_release(c, (uint32_t)sa, sa == (int32_t)n ? nv : nc_get(c, (uint32_t)sa), rc, rr)) return;
         node_bound_changed(c, (uint32_t)sa);
         s_move_after_free(c, rc, rr);
         break;
@@ -1577,8 +1680,8 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
         bit_clear(c.V().s_present(), n);
         // invariant: an absent node's cache entry is (0, 0), as after initialize, so no request with
         // cpu > 0 fits it and the event loop's screened scan needs no presence words
-        c.V().s_cpu()[n] = 0;
-        c.V().s_ram()[n] = 0;
+        const NcEnt zero = {0u, 0ull};
+        nc_put(c, n, zero);
         h->s_node_count -= 1;
         node_bound_changed(c, n);
         if (c.V().node(n).flags & NF_S_ASSIGN) {  // reschedule_unfinished_pods (352-364), name order
@@ -2704,11 +2807,9 @@ K10S_HD void init_replica(Ctx& c) {
     memset(&ns, 0, sizeof ns);
     ns.as_slot = -1;
     ns.pend_def = -1;
-    uint32_t* s_cpu = v.s_cpu();
-    uint64_t* s_ram = v.s_ram();
+    const NcEnt zero = {0u, 0ull};
     for (uint32_t i = lane; i < N; i += K10S_LANES) {
-        s_cpu[i] = 0;
-        s_ram[i] = 0;
+        nc_put(c, i, zero);
         v.node(i) = ns;
     }
     for (uint32_t i = lane; i < L->words_nodes; i += K10S_LANES) v.s_present()[i] = 0;
@@ -2801,15 +2902,18 @@ K10S_HD void init_replica(Ctx& c) {
             v.g_cpu()[slot] = sc->def_cpu[def];
             v.g_ram()[slot] = sc->def_ram[def];
         }
-        s_cpu[n] = sc->def_cpu[def];
-        s_ram[n] = sc->def_ram[def];
-        v.s_ccpu()[n] = sc->def_cpu[def];
-        v.s_cram()[n] = sc->def_ram[def];
+        const NcEnt cap = {sc->def_cpu[def], sc->def_ram[def]};
+        nc_put(c, n, cap);
+        if (!nc_packed(c)) {   // capacities (MostAllocated): wide layout only
+            v.s_ccpu()[n] = cap.cpu;
+            v.s_cram()[n] = cap.ram;
+        }
         bit_set(v.s_present(), n);
     }
     h->s_node_count = sc->n_default;
     wave_sync();
-    for (uint32_t b = 0; b < L->nblocks; b++) block_recompute(c, b);  // zero bounds for absent nodes
+    if (!nc_packed(c))   // block bounds (pruned scan): wide layout only; zero for absent nodes
+        for (uint32_t b = 0; b < L->nblocks; b++) block_recompute(c, b);
     h->counters[K10S_C_NODES_READ] = 0;
     h->ps_node_count = sc->n_default;
     h->as_node_count = sc->n_default;
@@ -3002,12 +3106,14 @@ K10S_HD void consume_source(Ctx& c, int src, uint32_t ntr) {
 K10S_HD bool cache_fits(Ctx& c, uint32_t rc, uint64_t rr) {
     if (rc == 0 && rr == 0) return false;
     const uint32_t N = c.S().n_nodes;
-    const uint32_t* cpu = c.V().s_cpu();
-    const uint64_t* ram = c.V().s_ram();
     const uint64_t* pres = c.V().s_present();
     for (uint32_t base = 0; base < N; base += K10S_LANES) {
         const uint32_t n = base + (uint32_t)lane_id();
-        const bool f = n < N && bit_test(pres, n) && rc <= cpu[n] && rr <= ram[n];
+        bool f = false;
+        if (n < N && bit_test(pres, n)) {
+            const NcEnt v = nc_get(c, n);
+            f = rc <= v.cpu && rr <= v.ram;
+        }
         if (wave_any(f)) return true;
     }
     return false;
@@ -3295,6 +3401,15 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
 #if K10S_DEVICE && defined(K10S_DBG_VALU)
         // bottleneck probe (tooling builds only): K10S_DBG_VALU extra independent VALU ops per event
         for (int i = 0; i < K10S_DBG_VALU; i++) asm volatile("v_mov_b32 v0, v0" ::: "v0");
+#endif
+#if K10S_DEVICE && defined(K10S_DBG_SALU)
+        // bottleneck probe (tooling builds only): K10S_DBG_SALU extra independent SALU ops per event
+        for (int i = 0; i < K10S_DBG_SALU; i++) asm volatile("s_add_u32 s0, s0, 0" ::: "s0", "scc");
+#endif
+#if K10S_DEVICE && defined(K10S_DBG_STORE)
+        // bottleneck probe: one extra HBM store per event just before the handler call (to the HBM
+        // copy of the header, which the launch's copy-out overwrites)
+        if (lane_id() == 0) ((volatile uint32_t*)&c.V().h()->tr_pad)[0] = (uint32_t)done;
 #endif
 #if K10S_DEVICE && defined(K10S_DBG_LAT)
         // bottleneck probe: K10S_DBG_LAT extra dependent LDS round trips per event

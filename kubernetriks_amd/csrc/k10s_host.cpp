@@ -62,6 +62,8 @@ struct k10s_engine {
     std::vector<Params> params;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool plugins = false;          // some replica's profile is not LeastAllocated alone
+    bool wide = false;             // launch the wide-cache kernel copy (k10s_kernels_plugins.hip): a
+                                   // plugin replica, or a node cache that is not packed (L.packed == 0)
 };
 
 // All engines of a device launch on one stream: the launch constants are one __constant__ block per
@@ -93,7 +95,7 @@ static void engine_free(k10s_engine* e) {
 
 static int32_t engine_init(k10s_engine* e) {
     HIPCHK(hipSetDevice(e->device));
-    HIPCHK((e->plugins ? k10s_launch_init_plugins : k10s_launch_init)(e->h_dc, e->R, e->stream));
+    HIPCHK((e->wide ? k10s_launch_init_plugins : k10s_launch_init)(e->h_dc, e->R, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     return K10S_OK;
 }
@@ -269,7 +271,6 @@ k10s_engine* k10s_engine_create_bulk(const char* scenario_text, const void* pods
         delete e;
         return nullptr;
     }
-    e->L = make_layout(e->hs, c);
     e->params.resize(n_replicas);
     for (uint32_t r = 0; r < n_replicas; r++) {
         if (params) {
@@ -287,6 +288,9 @@ k10s_engine* k10s_engine_create_bulk(const char* scenario_text, const void* pods
             return nullptr;
         }
     }
+    // the node cache is packed unless some replica needs the wide SoA (k10s_capacities.node_cache)
+    e->L = make_layout(e->hs, c, !e->plugins);
+    e->wide = e->plugins || !e->L.packed;
     auto fail = [&](const std::string& m) -> k10s_engine* {
         set_err(K10S_E_HIP, m);
         engine_free(e);
@@ -351,7 +355,7 @@ int32_t k10s_engine_step_async(k10s_engine* e, int32_t mode, double until_time, 
     if (mode != K10S_RUN_UNTIL_ALL_FINISHED && mode != K10S_RUN_UNTIL_TIME) return set_err(K10S_E_INVALID, "bad mode");
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipMemsetAsync(e->d_active, 0, 4, e->stream));
-    HIPCHK((e->plugins ? k10s_launch_run_plugins : k10s_launch_run)(e->h_dc, e->R, mode, until_time, max_time,
+    HIPCHK((e->wide ? k10s_launch_run_plugins : k10s_launch_run)(e->h_dc, e->R, mode, until_time, max_time,
                                                                      max_events_per_launch, e->d_active, e->stream));
     HIPCHK(hipMemcpyAsync(e->h_active, e->d_active, 4, hipMemcpyDeviceToHost, e->stream));
     return K10S_OK;
@@ -503,5 +507,6 @@ const char* k10s_engine_group_name(const k10s_engine* e, uint32_t i) {
     return (e && i < e->hs.group_names.size()) ? e->hs.group_names[i].c_str() : "";
 }
 uint64_t k10s_engine_replica_bytes(const k10s_engine* e) { return e ? e->L.stride : 0; }
+uint32_t k10s_engine_node_entry_bytes(const k10s_engine* e) { return e ? (e->L.packed ? 8u : 12u) : 0u; }
 
 }  // extern "C"

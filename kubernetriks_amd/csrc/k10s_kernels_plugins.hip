@@ -1,12 +1,15 @@
 // k10s_kernels_plugins.hip — the event-loop kernels (init + run) compiled a second time with the
 // score-plugin profile path in (K10S_SCORE_PLUGINS=1: MostAllocatedResources and multi-plugin
-// profiles, k10s_engine.h run_scheduling_cycle_plugins).  Symbols are renamed so both copies live in
-// one library; k10s_host.cpp launches this copy only for engines with such a replica.  Every engine
+// profiles, k10s_engine.h run_scheduling_cycle_plugins) and the wide node-cache layout
+// (K10S_PACKED=0).  Symbols are renamed so both copies live in one library; k10s_host.cpp launches
+// this copy for engines with such a replica or whose node cache is not packed (Layout.packed).  Every engine
 // function and type of this copy lives in namespace k10s_plugins (the `k10s` token renamed), so the
 // two copies' handlers — different bodies of the same inline functions — never share a mangled
 // name (no ODR clash if the library is ever linked with -fgpu-rdc or LTO).
 #define k10s k10s_plugins
 #define K10S_SCORE_PLUGINS 1
+#define K10S_PACKED 0   // the wide node cache (u32 cpu + u64 ram SoA): plugin replicas read the capacity
+                        // SoA beside it, and scenarios whose nodes do not fit the packed entry run here
 #define K10S_PLUGINS_TU 1
 #define k10s_dc k10s_dc_plugins
 #define k10s_hdr k10s_hdr_plugins

@@ -328,7 +328,8 @@ static_assert(sizeof(SlotState) == 32, "SlotState must be 32 B");
 struct Layout {
     uint64_t stride;
     uint64_t hdr;
-    uint64_t s_cpu, s_ram, s_present;    // hot scheduler-cache SoA (scan target)
+    uint64_t s_cpu, s_ram, s_present;    // hot scheduler-cache SoA (scan target; wide layout)
+    uint64_t s_node;                     // packed layout: u64 per node, cpu << 40 | ram (k10s_engine.h nc_*)
     uint64_t s_bcpu, s_bram;             // per-block maxima of the present nodes' allocatable
     uint64_t s_ccpu, s_cram;             // scheduler-cache capacity SoA (MostAllocated, an extension)
     uint64_t node, pend_rm, pod, prec, slot, pool_ring;
@@ -348,6 +349,8 @@ struct Layout {
     uint32_t nblocks;
     uint32_t cap_gauge;   // gauge rows per replica (0 = gauge recorder off)
     uint32_t stall;       // 1: stall guard on (k10s_capacities.stall_guard)
+    uint32_t packed;      // 1: node cache packed in s_node (8 B per node); 0: wide SoA s_cpu / s_ram
+    uint32_t pad_l;
 };
 
 // Everything a launch reads but never writes, as one block (device: __constant__ memory).

@@ -87,7 +87,7 @@ class Capacities(ctypes.Structure):
                 ("ca_name_bound", ctypes.c_uint32), ("event_log", ctypes.c_uint32),
                 ("placement_log", ctypes.c_uint32), ("pod_records", ctypes.c_uint32),
                 ("delay_fifo", ctypes.c_uint32), ("pruned_scan", ctypes.c_uint32), ("gauge_log", ctypes.c_uint32),
-                ("stall_guard", ctypes.c_uint32)]
+                ("stall_guard", ctypes.c_uint32), ("node_cache", ctypes.c_uint32)]
 
 
 class GaugeRow(ctypes.Structure):  # k10s_gauge_row (collector.rs:392-407 CSV columns)
@@ -140,10 +140,13 @@ def _decl(L, prefix: str):
         "num_nodes": (u32, [vp]), "num_pods": (u32, [vp]), "num_groups": (u32, [vp]),
         "node_name": (ctypes.c_char_p, [vp, u32]), "pod_name": (ctypes.c_char_p, [vp, u32]),
         "group_name": (ctypes.c_char_p, [vp, u32]), "replica_bytes": (u64, [vp]),
+        "node_entry_bytes": (u32, [vp]),
         "default_params": (i32, [vp, P(ReplicaParams)]),
     }
     out = {}
     for name, (res, args) in sig.items():
+        if name == "node_entry_bytes" and not hasattr(L, prefix + name):
+            continue   # a library from before the packed node cache (A/B tooling): wide, 12 B
         f = getattr(L, prefix + name)
         f.restype = res
         f.argtypes = args
@@ -253,6 +256,13 @@ class EngineBase:
     @property
     def replica_bytes(self) -> int:
         return int(self._fn["replica_bytes"](self._h))
+
+    @property
+    def node_entry_bytes(self) -> int:
+        """Bytes per node of the node cache each scheduling attempt reads: 8 packed, 12 wide
+        (k10s_capacities.node_cache)."""
+        f = self._fn.get("node_entry_bytes")
+        return int(f(self._h)) if f else 12
 
     def _check(self, rc):
         if rc != 0:

@@ -60,7 +60,6 @@ void* hc_create_bulk(const char* text, const void* blob, uint64_t blob_len, cons
     Scenario offs;
     h->scen_bytes = pack_scenario(h->hs, offs);
     h->sc = rebase_scenario(offs, h->scen_bytes.data());
-    h->L = make_layout(h->hs, c);
     h->R = R;
     h->params.resize(R);
     for (uint32_t r = 0; r < R; r++) {
@@ -78,6 +77,9 @@ void* hc_create_bulk(const char* text, const void* blob, uint64_t blob_len, cons
             return nullptr;
         }
     }
+    bool plugins = false;
+    for (uint32_t r = 0; r < R; r++) plugins |= h->params[r].score_plugins != K10S_SCORE_LEAST_ALLOCATED;
+    h->L = make_layout(h->hs, c, !plugins);
     h->state.assign((size_t)h->L.stride * R, 0);
     for (uint32_t r = 0; r < R; r++) {
         RepHdr work;
@@ -167,6 +169,7 @@ const char* hc_node_name(void* p, uint32_t i) { return ((HC*)p)->hs.node_names[i
 const char* hc_pod_name(void* p, uint32_t i) { return ((HC*)p)->hs.pod_names[i].c_str(); }
 const char* hc_group_name(void* p, uint32_t i) { return ((HC*)p)->hs.group_names[i].c_str(); }
 uint64_t hc_replica_bytes(void* p) { return ((HC*)p)->L.stride; }
+uint32_t hc_node_entry_bytes(void* p) { return ((HC*)p)->L.packed ? 8u : 12u; }
 
 }  // extern "C"
 

@@ -42,7 +42,7 @@ def parity_caps(log: bool = True, fifo: int = 0, pruned: int = 0, gauges: int = 
 
 def run_pair(engine_cls, scenario: str, mode: int = RUN_UNTIL_ALL_FINISHED, until: Optional[float] = None,
              max_time: float = 1e7, budget: int = 0, log: bool = True, params=None, fifo: int = 0,
-             pruned: int = 0, ca_name_bound: int = 0):
+             pruned: int = 0, ca_name_bound: int = 0, node_cache: int = 0):
     """Run the oracle and one engine replica on the same scenario; return (oracle dict, engine, res)."""
     o = ob.OracleSim(scenario, log=log, gauges=GAUGE_ROWS)
     if mode == RUN_UNTIL_ALL_FINISHED:
@@ -53,6 +53,7 @@ def run_pair(engine_cls, scenario: str, mode: int = RUN_UNTIL_ALL_FINISHED, unti
     od["status_name"] = ORACLE_STATUS[st] if not od["panicked"] else "error"
     caps = parity_caps(log, fifo, pruned, GAUGE_ROWS)
     caps.ca_name_bound = ca_name_bound
+    caps.node_cache = node_cache
     eng = engine_cls(scenario, 1, params=params, caps=caps)
     if mode == RUN_UNTIL_ALL_FINISHED:
         eng.run_until_all_finished(max_time, budget)

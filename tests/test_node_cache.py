@@ -1,0 +1,86 @@
+"""The scheduler's node cache in its two layouts (k10s_engine.h nc_*, k10s_capacities.node_cache):
+packed (one u64 per node, cpu << 40 | ram: 8 B per node and scan) wherever every node definition
+fits (cpu < 2^24, ram < 2^40) and no replica needs the wide SoA, else wide (u32 cpu + u64 ram).
+Both layouts run the same scenarios bit-exactly against the oracle; the wide one on the GPU is the
+second kernel copy (k10s_kernels_plugins.hip) with LeastAllocated-only replicas.  The packed
+field edges (cpu 2^24 - 1, ram 2^40 - 1) are exercised with nodes exactly at the limits."""
+import pytest
+
+import gen
+import parity
+from hostcheck_bridge import HostEngine
+from kubernetriks_amd import workloads as wl
+from kubernetriks_amd.native import RUN_UNTIL_ALL_FINISHED, RUN_UNTIL_TIME
+from kubernetriks_amd.scenario import GenericClusterTrace, GenericWorkloadTrace, Node, Pod, SimulationConfig, scenario_text
+
+BACKENDS = [pytest.param("host", id="host"), pytest.param("gpu", id="gpu", marks=pytest.mark.gpu)]
+WIDE = 1
+
+
+def engine_cls(backend):
+    if backend == "host":
+        return HostEngine
+    from kubernetriks_amd.native import Engine
+    return Engine
+
+
+SEEDS = list(range(0, 24))
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+@pytest.mark.parametrize("seed", SEEDS)
+def test_wide_layout_matches_oracle(backend, seed):
+    """The fuzz scenarios (packed by default in every other test) forced onto the wide layout."""
+    kw = dict(ca=(seed % 3 == 1), hpa=(seed % 4 == 2))
+    mode = RUN_UNTIL_TIME if kw["hpa"] else RUN_UNTIL_ALL_FINISHED
+    od, eng = parity.run_pair(engine_cls(backend), gen.random_scenario(seed, **kw), mode=mode, until=3000.0,
+                              max_time=20000.0, node_cache=WIDE)
+    assert eng.node_entry_bytes == 12
+    assert parity.compare(od, eng) == [], seed
+
+
+def edge_scenario(cpu: int, ram: int, seed: int = 0) -> str:
+    """Nodes at (and one step below) the given capacities, pods sized so nodes fill up, release and
+    refill: allocatable crosses every field value from 0 to the capacity."""
+    import random
+    rng = random.Random(seed)
+    c = GenericClusterTrace()
+    for k in range(6):
+        c.create_node(0.0, Node(f"node_{k}", cpu - (k % 2), ram - (k % 3)))
+    w = GenericWorkloadTrace()
+    for i in range(120):
+        rc = rng.choice([1, cpu // 7, cpu // 3, cpu // 2 + 1, cpu - 1])
+        rr = rng.choice([1, ram // 5, ram // 3, ram // 2 + 1, ram - 2])
+        w.create_pod(float(rng.randint(0, 300)), Pod(f"pod_{i:03d}", max(rc, 1), max(rr, 1), float(rng.randint(5, 200))))
+    return scenario_text(SimulationConfig(), c, w)
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_packed_field_limits(backend):
+    """cpu 2^24 - 1 and ram 2^40 - 1 are packable and run bit-exactly; one more unit of either makes
+    the engine fall back to the wide layout, also bit-exact."""
+    E = engine_cls(backend)
+    for cpu, ram, nb in (((1 << 24) - 1, (1 << 40) - 1, 8), (1 << 24, (1 << 40) - 1, 12), ((1 << 24) - 1, 1 << 40, 12)):
+        od, eng = parity.run_pair(E, edge_scenario(cpu, ram), max_time=1e6)
+        assert eng.node_entry_bytes == nb, (cpu, ram)
+        assert parity.compare(od, eng) == [], (cpu, ram)
+        assert eng.results()[0]["counters"]["placements"] > 50
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_layout_choice(backend):
+    """Packed for the bench's Alibaba-like clusters; wide for the pruned scan, for a replica with a
+    score plugin beyond LeastAllocated, and on request."""
+    E = engine_cls(backend)
+    c, w = wl.c3_traces(n_nodes=64, n_pods=100, arrival_window=50.0, seed=3)
+    scn = scenario_text(SimulationConfig(), c, w)
+    assert E(scn, 2).node_entry_bytes == 8
+    assert E(scn, 2, caps=parity.parity_caps(False, pruned=1)).node_entry_bytes == 12
+    caps = parity.parity_caps(False)
+    caps.node_cache = WIDE
+    assert E(scn, 2, caps=caps).node_entry_bytes == 12
+    params = wl.replica_params(E(scn, 1).default_params(), 2)
+    params[1].score_plugins = 3
+    params[1].most_allocated_weight = 1.0
+    assert E(scn, 2, params=params).node_entry_bytes == 12
+    assert E(scn, 2).replica_bytes < E(scn, 2, caps=caps).replica_bytes   # 8 B/node and no capacity SoA

@@ -34,6 +34,7 @@ def main():
         "kernel": kernel, "config": json.loads(config), "workload": cfg.get("workload_name", "c3"),
         "launches": [nf, nw],
         "engine": b.get("engine"), "scan_mode": b.get("roofline", {}).get("scan_mode", "full"),
+        "score_plugins": cfg.get("score_plugins", "least"),
         "fetch_size_kib": fk, "write_size_kib": wk,
         "hbm_bytes_per_launch": (2.0 * fk + wk) * 1024.0 if fk is not None and wk is not None else None,
     }
