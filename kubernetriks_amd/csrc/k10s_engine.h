@@ -736,7 +736,11 @@ K10S_HD void run_remove(Ctx& c, uint32_t p) {
         c.V().g_ram()[slot] += c.V().pod(p).req_ram;
     }
     c.V().pod(p).run_slot = -1;
-    c.V().pod(p).finish_seq = 0;  // cancels a pending finish event (dslab cancel_event)
+    // cancels a pending finish event (dslab cancel_event) unless it is the one being handled: the
+    // canceled event stays in the heap until popped (counted in stale_fin)
+    const uint32_t fs = c.V().pod(p).finish_seq;
+    if (fs != 0 && !(c.H().cur_kind == K10S_EV_N_POD_FINISHED && c.H().cur_seq == fs)) c.H().stale_fin += 1;
+    c.V().pod(p).finish_seq = 0;
     int32_t g = c.S().pod_group[p];
     if (g >= 0) c.V().grp()[g].running -= 1;
 }
@@ -1080,6 +1084,9 @@ K10S_D float wave_min_f32(float v) {
 #ifndef K10S_SCREEN_NO_PRESENCE
 #define K10S_SCREEN_NO_PRESENCE 1
 #endif
+#ifndef K10S_SCAN_STEPS2
+#define K10S_SCAN_STEPS2 1
+#endif
 // NP: the event loop's own node cache (absent nodes hold (0, 0): no presence words read); the unit
 // surface's caller-owned buffers keep their presence bitmap.
 #define SCREEN_LOAD(c, r, p, n, n0)                                                                   \
@@ -1104,6 +1111,35 @@ K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, cons
     uint64_t lr = 0;
     float lu = __builtin_inff();
     float T = __builtin_inff();  // thr + eps: +inf screens nothing out (the first step)
+#if K10S_SCREEN_PACKED
+    // one 256-node step of a lane's group g at n0 (screen, exact scores, threshold)
+    auto step = [&](const ScanGrp& g, uint32_t n0) {
+        const uint32_t bits = grp_bits(g, n0, n_nodes);
+        const uint32_t need = screen_grp(g, bits, rc, rr, fa, fr, T);
+        if (need) {
+            if (need & 1u) score_node_exact(n0, g.cv.x, g.r01.x, rr, frc, frr, best_s, best_n, la, lr, lu);
+            if (need & 2u) score_node_exact(n0 + 1, g.cv.y, g.r01.y, rr, frc, frr, best_s, best_n, la, lr, lu);
+            if (need & 4u) score_node_exact(n0 + 2, g.cv.z, g.r23.x, rr, frc, frr, best_s, best_n, la, lr, lu);
+            if (need & 8u) score_node_exact(n0 + 3, g.cv.w, g.r23.y, rr, frc, frr, best_s, best_n, la, lr, lu);
+        }
+        if (__ballot(need != 0)) {
+            const float thr = __builtin_bit_cast(float, uniform_u32(__builtin_bit_cast(uint32_t, wave_min_f32(lu))));
+            T = thr + K10S_SCREEN_EPS;
+        }
+    };
+    // K10S_SCAN_STEPS2 (packed node cache, no load pipeline): the loads of two 256-node steps (32 B
+    // per lane each) are issued together, so a 4,096-node scan waits 8 memory round trips, not 16;
+    // a lane still visits its nodes in ascending order
+    if (PK && K10S_SCAN_STEPS2 && PIPE == 0) {
+        for (uint32_t base = 0; base < n_nodes; base += 512) {
+            const ScanGrp g0 = SCREEN_LOAD(s_cpu, s_ram, present, n_nodes, base + l4);
+            const ScanGrp g1 = SCREEN_LOAD(s_cpu, s_ram, present, n_nodes, base + 256u + l4);
+            step(g0, base + l4);
+            step(g1, base + 256u + l4);
+        }
+        return;
+    }
+#endif
     ScanGrp g[PIPE + 1];
 #pragma unroll
     for (int i = 0; i < PIPE; i++) g[i] = SCREEN_LOAD(s_cpu, s_ram, present, n_nodes, 256u * i + l4);
@@ -3303,7 +3339,10 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
                 e = h->heap_top;
                 uniform_event(e);
 #endif
-                if (e.kind == K10S_EV_N_POD_FINISHED && c.V().pod(e.a).finish_seq != e.seq) {  // canceled
+                // canceled (lazy cancel): only while some canceled finish is pending is the pod read
+                if (e.kind == K10S_EV_N_POD_FINISHED && uniform_u32(h->stale_fin) != 0 &&
+                    c.V().pod(e.a).finish_seq != e.seq) {
+                    h->stale_fin -= 1;
                     heap_pop(c);
                     sl_refresh(c, SRC_HEAP, ntr);
                     continue;

@@ -247,6 +247,9 @@ struct RepHdr {
     uint32_t unsched_missing;     // PS unscheduled-pod cache entries whose pod left storage (PF_UNSCHED
                                   // without PF_IN_PS): scale_up_info would panic on them
                                   // (persistent_storage.rs:137-145)
+    uint32_t stale_fin;           // canceled pod-finish events still in the heap (lazy cancel): while 0,
+                                  // a popped N_POD_FINISHED is live without reading its pod's line
+    uint32_t pad_h;
     HeapEv fq_win[K10S_NFQ * K10S_FQW];
     HeapEv heap_lds[K10S_HEAP_TOP];
 #if K10S_AQ_TOP
