@@ -26,9 +26,16 @@ namespace k10s {
 // working replica header — clock, id counter, queue sizes, counters, estimators — is staged in LDS
 // (k10s_hdr) for the whole launch: one workgroup = one replica.  Host (test-only check build): the
 // same code reads them through the pointers held in Ctx.
+// The replica region of this workgroup and its most used sections as absolute addresses
+// (k10s_sec, LDS), written by the kernels before anything else: an access reads its section's
+// address with one ds_read_b64 (CSE'd within a function: the array is never written afterwards)
+// instead of re-deriving it through the opaque constant block (replica index x stride + section
+// offset: ~10 SALU + 3 SMEM per access, repeated at every access by design, see K10S_DC below).
+enum : int { SEC_BASE = 0, SEC_POD, SEC_NODE, SEC_SLOT, SEC_FQ, SEC_HEAP, SEC_SNODE, SEC_PRES, SEC_AQ, SEC_UQ, K10S_NSEC };
 #if defined(__HIP__)
 __constant__ DevConst k10s_dc;
 __shared__ RepHdr k10s_hdr;
+__shared__ uint64_t k10s_sec[K10S_NSEC];
 // The launch's run arguments, staged in LDS by the run kernel (K10S_RUN_ARGS_LDS): read where the
 // loop tests them instead of held in SGPRs across the loop, where they are spilled around every
 // out-of-line handler call.
@@ -66,29 +73,36 @@ K10S_D DevConstPtr dc_ptr() {
 // layout at each use instead of being held live across the event loop.
 struct Rep {
 #if K10S_DEVICE
-    K10S_GB(uint8_t) b;
+    K10S_D static K10S_GB(uint8_t) sec(int i) { return (K10S_GB(uint8_t))uniform_u64(k10s_sec[i]); }
     K10S_D const Layout& L() const { return K10S_DC.L; }
+    template <typename T>
+    K10S_D T* at(uint64_t off) const { return (T*)(sec(SEC_BASE) + off); }
+    // a section with its own entry in k10s_sec (the offset argument is the host's)
+    template <typename T>
+    K10S_D T* hot(int i, uint64_t) const { return (T*)sec(i); }
 #else
     uint8_t* b;
     const Layout* Lp;
     const Layout& L() const { return *Lp; }
-#endif
     template <typename T>
-    K10S_HD T* at(uint64_t off) const { return (T*)(b + off); }
+    T* at(uint64_t off) const { return (T*)(b + off); }
+    template <typename T>
+    T* hot(int, uint64_t off) const { return at<T>(off); }
+#endif
     K10S_HD RepHdr* h() const { return at<RepHdr>(L().hdr); }
-    K10S_HD uint64_t* s_node() const { return at<uint64_t>(L().s_node); }
+    K10S_HD uint64_t* s_node() const { return hot<uint64_t>(SEC_SNODE, L().s_node); }
     K10S_HD uint32_t* s_cpu() const { return at<uint32_t>(L().s_cpu); }
     K10S_HD uint64_t* s_ram() const { return at<uint64_t>(L().s_ram); }
-    K10S_HD uint64_t* s_present() const { return at<uint64_t>(L().s_present); }
+    K10S_HD uint64_t* s_present() const { return hot<uint64_t>(SEC_PRES, L().s_present); }
     K10S_HD uint32_t* s_bcpu() const { return at<uint32_t>(L().s_bcpu); }
     K10S_HD uint32_t* s_ccpu() const { return at<uint32_t>(L().s_ccpu); }
     K10S_HD uint64_t* s_cram() const { return at<uint64_t>(L().s_cram); }
     K10S_HD uint64_t* s_bram() const { return at<uint64_t>(L().s_bram); }
-    K10S_HD NodeState& node(uint32_t n) const { return at<NodeState>(L().node)[n]; }
+    K10S_HD NodeState& node(uint32_t n) const { return hot<NodeState>(SEC_NODE, L().node)[n]; }
     K10S_HD uint64_t* pend_rm() const { return at<uint64_t>(L().pend_rm); }
-    K10S_HD PodState& pod(uint32_t p) const { return at<PodState>(L().pod)[p]; }
+    K10S_HD PodState& pod(uint32_t p) const { return hot<PodState>(SEC_POD, L().pod)[p]; }
     K10S_HD k10s_pod_record* prec() const { return L().rec_on ? at<k10s_pod_record>(L().prec) : nullptr; }
-    K10S_HD SlotState& slot(int32_t s) const { return at<SlotState>(L().slot)[s]; }
+    K10S_HD SlotState& slot(int32_t s) const { return hot<SlotState>(SEC_SLOT, L().slot)[s]; }
     K10S_HD uint32_t* pool_ring() const { return at<uint32_t>(L().pool_ring); }
     K10S_HD GroupState* grp() const { return at<GroupState>(L().grp); }
     K10S_HD uint64_t* grp_bits() const { return at<uint64_t>(L().grp_bits); }
@@ -102,10 +116,10 @@ struct Rep {
     K10S_HD int32_t* ps_head() const { return at<int32_t>(L().ps_head); }
     K10S_HD int32_t* ps_link() const { return at<int32_t>(L().ps_link); }   // [2p] prev, [2p + 1] next
     K10S_HD uint32_t* ca_list() const { return at<uint32_t>(L().ca_list); }
-    K10S_HD HeapEv* heap() const { return at<HeapEv>(L().heap); }
-    K10S_HD HeapEv* fq() const { return at<HeapEv>(L().fq); }
-    K10S_HD QInfo* aq() const { return at<QInfo>(L().aq); }
-    K10S_HD QInfo* uq() const { return at<QInfo>(L().uq); }
+    K10S_HD HeapEv* heap() const { return hot<HeapEv>(SEC_HEAP, L().heap); }
+    K10S_HD HeapEv* fq() const { return hot<HeapEv>(SEC_FQ, L().fq); }
+    K10S_HD QInfo* aq() const { return hot<QInfo>(SEC_AQ, L().aq); }
+    K10S_HD QInfo* uq() const { return hot<QInfo>(SEC_UQ, L().uq); }
     K10S_HD k10s_log_entry* log() const { return L().cap_log ? at<k10s_log_entry>(L().log) : nullptr; }
     K10S_HD k10s_placement* place() const { return L().cap_place ? at<k10s_placement>(L().place) : nullptr; }
     K10S_HD k10s_gauge_row* gauge() const { return at<k10s_gauge_row>(L().gauge); }
@@ -130,11 +144,7 @@ struct Ctx {
     K10S_D const Params& P() const { return *(const Params*)(K10S_DC.params + blockIdx.x); }
     K10S_D const Layout& Ly() const { return K10S_DC.L; }
     K10S_D RepHdr& H() const { return k10s_hdr; }
-    K10S_D Rep V() const {
-        Rep v;
-        v.b = K10S_DC.base + (uint64_t)blockIdx.x * K10S_DC.L.stride;
-        return v;
-    }
+    K10S_D Rep V() const { return Rep(); }
 #else
     const Scenario* sc;
     const Params* pr;
@@ -358,7 +368,7 @@ static_assert(K10S_HEAP_D == 8 || K10S_HEAP_TOP == 1 + K10S_HEAP_D, "heap top = 
 // HBM part through a raw buffer descriptor (scalar base, 32-bit offsets): distinct instructions
 // from the LDS path, so the two are never merged into one generic (FLAT) access.
 K10S_D __amdgpu_buffer_rsrc_t heap_rsrc(Ctx& c) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(c.V().b + K10S_DC.L.heap), (short)0,
+    return __builtin_amdgcn_make_buffer_rsrc((void*)c.V().heap(), (short)0,
                                              (int)(K10S_DC.L.cap_heap * (uint32_t)sizeof(HeapEv)), 0x00020000);
 }
 K10S_D HeapEv heap_get(Ctx& c, uint32_t i) {

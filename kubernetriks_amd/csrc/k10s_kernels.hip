@@ -55,9 +55,28 @@ __device__ __forceinline__ uint32_t* hdr_global(uint32_t r) {
 #endif
 }
 
+// The replica's region and hot sections as absolute addresses in LDS (k10s_engine.h k10s_sec).
+__device__ __forceinline__ void sec_setup(uint32_t r) {
+#if K10S_DEVICE
+    const uint32_t l = threadIdx.x;
+    if (l < (uint32_t)K10S_NSEC) {
+        const Layout& L = K10S_DC.L;
+        const uint64_t b = (uint64_t)(K10S_DC.base + (uint64_t)r * L.stride);
+        const uint64_t off = l == SEC_POD ? L.pod : l == SEC_NODE ? L.node : l == SEC_SLOT ? L.slot : l == SEC_FQ ? L.fq
+                           : l == SEC_HEAP ? L.heap : l == SEC_SNODE ? L.s_node : l == SEC_PRES ? L.s_present
+                           : l == SEC_AQ ? L.aq : l == SEC_UQ ? L.uq : 0;
+        k10s_sec[l] = b + off;
+    }
+    __syncthreads();
+#else
+    (void)r;
+#endif
+}
+
 __global__ __launch_bounds__(64) void k10s_init_kernel(uint32_t n_replicas) {
     uint32_t r = blockIdx.x;
     if (r >= n_replicas) return;
+    sec_setup(r);
     Ctx c;
     init_replica(c);
     __syncthreads();
@@ -80,6 +99,7 @@ __global__ K10S_RUN_BOUNDS void k10s_run_kernel(uint32_t n_replicas, int mode, d
         k10s_run.until_mode = mode == K10S_RUN_UNTIL_TIME ? 1u : 0u;
     }
 #endif
+    sec_setup(r);
     hdr_copy((uint32_t*)&k10s_hdr, hdr_global(r));
     Ctx c;
     int more = run_replica(c, mode, until_time, max_time, budget);

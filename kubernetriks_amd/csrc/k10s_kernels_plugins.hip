@@ -13,6 +13,7 @@
 #define K10S_PLUGINS_TU 1
 #define k10s_dc k10s_dc_plugins
 #define k10s_hdr k10s_hdr_plugins
+#define k10s_sec k10s_sec_plugins
 #define k10s_fair_board k10s_fair_board_plugins
 #define k10s_run k10s_run_plugins
 #define k10s_init_kernel k10s_init_kernel_plugins
