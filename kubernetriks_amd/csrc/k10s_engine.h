@@ -31,7 +31,8 @@ namespace k10s {
 // address with one ds_read_b64 (CSE'd within a function: the array is never written afterwards)
 // instead of re-deriving it through the opaque constant block (replica index x stride + section
 // offset: ~10 SALU + 3 SMEM per access, repeated at every access by design, see K10S_DC below).
-enum : int { SEC_BASE = 0, SEC_POD, SEC_NODE, SEC_SLOT, SEC_FQ, SEC_HEAP, SEC_SNODE, SEC_PRES, SEC_AQ, SEC_UQ, K10S_NSEC };
+enum : int { SEC_BASE = 0, SEC_POD, SEC_NODE, SEC_SLOT, SEC_FQ, SEC_HEAP, SEC_SNODE, SEC_PRES, SEC_AQ, SEC_UQ,
+             SEC_PARAMS, K10S_NSEC };   // SEC_PARAMS: this replica's k10s_replica_params (read-only)
 #if defined(__HIP__)
 __constant__ DevConst k10s_dc;
 __shared__ RepHdr k10s_hdr;
@@ -141,7 +142,7 @@ inline Rep make_rep(uint8_t* base, const Layout& L, uint32_t r) {
 struct Ctx {
 #if K10S_DEVICE
     K10S_D const Scenario& S() const { return K10S_DC.sc; }
-    K10S_D const Params& P() const { return *(const Params*)(K10S_DC.params + blockIdx.x); }
+    K10S_D const Params& P() const { return *(K10S_RO(Params))uniform_u64(k10s_sec[SEC_PARAMS]); }
     K10S_D const Layout& Ly() const { return K10S_DC.L; }
     K10S_D RepHdr& H() const { return k10s_hdr; }
     K10S_D Rep V() const { return Rep(); }

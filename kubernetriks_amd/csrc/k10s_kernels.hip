@@ -65,7 +65,7 @@ __device__ __forceinline__ void sec_setup(uint32_t r) {
         const uint64_t off = l == SEC_POD ? L.pod : l == SEC_NODE ? L.node : l == SEC_SLOT ? L.slot : l == SEC_FQ ? L.fq
                            : l == SEC_HEAP ? L.heap : l == SEC_SNODE ? L.s_node : l == SEC_PRES ? L.s_present
                            : l == SEC_AQ ? L.aq : l == SEC_UQ ? L.uq : 0;
-        k10s_sec[l] = b + off;
+        k10s_sec[l] = l == SEC_PARAMS ? (uint64_t)(K10S_DC.params + r) : b + off;
     }
     __syncthreads();
 #else

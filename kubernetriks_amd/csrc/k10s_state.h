@@ -197,8 +197,9 @@ struct QInfo {              // QueuedPodInfo (queue.rs:13-27), 24 B
 #endif
 
 struct RepHdr {
-    double clock;
+    double clock;            // clock, next_seq and error_code: one 16-B LDS read in emit
     uint32_t next_seq;
+    uint32_t error_code;
     uint32_t trace_cursor;
     uint32_t heap_size;
     uint32_t aq_size;
@@ -209,7 +210,6 @@ struct RepHdr {
     uint32_t pool_head;
     uint32_t pool_count;
     uint32_t status;
-    uint32_t error_code;
     uint32_t error_kind;
     uint32_t error_seq;
     double error_time;
