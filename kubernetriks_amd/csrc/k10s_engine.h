@@ -425,10 +425,10 @@ K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uin
     uint32_t hd = 0, tl = 0, we = 0;
     double last = 0.0;
     if (cls >= 0) {
-        hd = H.fq_head[cls];
-        tl = H.fq_tail[cls];
-        we = H.fq_wend[cls];
-        last = H.fq_last[cls];
+        hd = H.fq[cls].head;
+        tl = H.fq[cls].tail;
+        we = H.fq[cls].wend;
+        last = H.fq[cls].last;
     }
     if (err) return 0;
     if (seq == 0xFFFFFFFFu) {
@@ -448,13 +448,13 @@ K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uin
         if (tl - hd < cap && (tl == hd || k >= total_key(last))) {
             if (we == tl && tl - hd < K10S_FQW) {  // the window holds the whole ring: append
                 H.fq_win[(uint32_t)cls * K10S_FQW + (tl & (K10S_FQW - 1))] = e;
-                H.fq_wend[cls] = tl + 1;
+                H.fq[cls].wend = tl + 1;
             } else {
                 c.V().fq()[(uint32_t)cls * cap + (tl & (cap - 1))] = e;
             }
             if (tl == hd) sl_mark(H, (uint32_t)cls);  // the ring was empty: a new head (source list)
-            H.fq_tail[cls] = tl + 1;
-            H.fq_last[cls] = e.time;
+            H.fq[cls].tail = tl + 1;
+            H.fq[cls].last = e.time;
             H.next_seq = e.seq + 1;
             return e.seq;
         }
@@ -2994,7 +2994,7 @@ K10S_HD bool sl_less(int64_t ka, uint32_t sa, int64_t kb, uint32_t sb) { return 
 K10S_HD bool src_head(Ctx& c, uint32_t q, uint32_t ntr, int64_t& k, uint32_t& s) {
     const RepHdr& H = c.H();
     if (q < (uint32_t)K10S_NFQ) {
-        const uint32_t hd = H.fq_head[q], tl = H.fq_tail[q];
+        const uint32_t hd = H.fq[q].head, tl = H.fq[q].tail;
         const HeapEv& t = H.fq_win[q * K10S_FQW + (hd & (K10S_FQW - 1))];
         k = total_key(t.time);
         s = t.seq;
@@ -3087,12 +3087,12 @@ K10S_HD void sl_rebuild(Ctx& c, uint32_t ntr) {
 K10S_HD void fq_refill(Ctx& c, int cls, uint32_t hd) {
     RepHdr& H = c.H();
     const uint32_t cap = c.Ly().cap_fq;
-    const uint32_t avail = H.fq_tail[cls] - hd;
+    const uint32_t avail = H.fq[cls].tail - hd;
     const uint32_t n = avail < K10S_FQW ? avail : K10S_FQW;
     const HeapEv* ring = c.V().fq() + (uint32_t)cls * cap;
     for (uint32_t i = (uint32_t)lane_id(); i < n; i += K10S_LANES)
         H.fq_win[(uint32_t)cls * K10S_FQW + ((hd + i) & (K10S_FQW - 1))] = ring[(hd + i) & (cap - 1)];
-    H.fq_wend[cls] = hd + n;
+    H.fq[cls].wend = hd + n;
 }
 
 // Remove the head event of source src (sl[0]) and move the source's entry in the source list to
@@ -3120,8 +3120,8 @@ K10S_HD void consume_source(Ctx& c, int src, uint32_t ntr) {
         K10S_PROF_COUNT(c, PROF_NHEAPPOP);
         has = src_head(c, SRC_HEAP, ntr, key, seq);
     } else {
-        const uint32_t hd = H.fq_head[src] + 1, tl = H.fq_tail[src], we = H.fq_wend[src];
-        H.fq_head[src] = hd;
+        const uint32_t hd = H.fq[src].head + 1, tl = H.fq[src].tail, we = H.fq[src].wend;
+        H.fq[src].head = hd;
         has = hd != tl;
         if (has) {
             if (hd == we) fq_refill(c, src, hd);
@@ -3135,9 +3135,12 @@ K10S_HD void consume_source(Ctx& c, int src, uint32_t ntr) {
     // src is sl[0]: while its new head still precedes the second source (47 % of the events at C3,
     // profiles/r03_selection_policy_sim.json) only sl[0]'s key changes — no lane-parallel update
     if (K10S_SL_FAST && has) {
+        // sl[1] is read whether or not it is live (LDS; ignored when n <= 1), so the three reads
+        // issue together
+        const int64_t k1 = (int64_t)uniform_u64((uint64_t)H.sl[1].key);
+        const uint32_t s1 = uniform_u32(H.sl[1].seq);
         const uint32_t n = uniform_u32(H.sl_n);
-        bool stays = n <= 1;
-        if (!stays) stays = sl_less(key, seq, (int64_t)uniform_u64((uint64_t)H.sl[1].key), uniform_u32(H.sl[1].seq));
+        const bool stays = n <= 1 || sl_less(key, seq, k1, s1);
         if (stays) {
             H.sl[0].key = key;
             H.sl[0].seq = seq;
@@ -3182,7 +3185,7 @@ K10S_HD bool replica_stalled(Ctx& c) {
     if (H.trace_cursor < c.S().n_trace || H.heap_size != 4 || H.aq_size != 0) return false;
     if (c.S().ca_enabled || c.S().hpa_enabled) return false;
     for (int q = 0; q < K10S_NFQ; q++)
-        if (H.fq_head[q] != H.fq_tail[q]) return false;
+        if (H.fq[q].head != H.fq[q].tail) return false;
     const QInfo* d = c.V().uq();
     const uint32_t n = uniform_u32(H.uq_size);
     for (uint32_t i = 0; i < n; i++) {
@@ -3363,12 +3366,12 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
 #endif
             } else {
 #if K10S_EV_BYREF
-                ep = K10S_EVREF(&h->fq_win[(uint32_t)src * K10S_FQW + (uniform_u32(h->fq_head[src]) & (K10S_FQW - 1))]);
+                ep = K10S_EVREF(&h->fq_win[(uint32_t)src * K10S_FQW + (uniform_u32(h->fq[src].head) & (K10S_FQW - 1))]);
                 e.time = uniform_f64(ep->time);
                 e.seq = uniform_u32(ep->seq);
                 e.kind = (uint16_t)uniform_u32(ep->kind);
 #else
-                e = h->fq_win[(uint32_t)src * K10S_FQW + (h->fq_head[src] & (K10S_FQW - 1))];
+                e = h->fq_win[(uint32_t)src * K10S_FQW + (h->fq[src].head & (K10S_FQW - 1))];
                 uniform_event(e);
 #endif
             }

@@ -152,7 +152,7 @@ struct SrcEnt {
     uint32_t src;
 };
 // The head of every delay-class ring lives in the working header (LDS on the device): ring
-// positions [fq_head, fq_wend) are held in a K10S_FQW-entry window, the rest in the HBM ring, and a
+// positions [fq.head, fq.wend) are held in a K10S_FQW-entry window, the rest in the HBM ring, and a
 // drained window is refilled K10S_FQW entries at a time by one lane-parallel load.
 #ifndef K10S_FQW
 #define K10S_FQW 4
@@ -196,6 +196,16 @@ struct QInfo {              // QueuedPodInfo (queue.rs:13-27), 24 B
 #define K10S_PROF_SLOTS 8
 #endif
 
+// One delay-class ring's counters, read together (one 16-B LDS read for head / tail / window end).
+struct alignas(16) FqRing {
+    uint32_t head, tail;   // ring positions (wrapping counters)
+    uint32_t wend;         // the LDS window holds positions [head, wend)
+    uint32_t pad;
+    double last;           // time of the newest entry (the run stays sorted)
+    double pad2;
+};
+static_assert(sizeof(FqRing) == 32, "FqRing must be 32 B");
+
 struct RepHdr {
     double clock;            // clock, next_seq and error_code: one 16-B LDS read in emit
     uint32_t next_seq;
@@ -225,11 +235,9 @@ struct RepHdr {
     uint32_t gauge_n;             // gauge rows recorded
     uint64_t g_cur_nodes, g_cur_pods, g_pods_q;   // GaugeMetrics counters (collector.rs:169-190)
     // event queue: delay-class FIFO rings (head/tail counters, newest time; a non-empty ring's head
-    // entry is fq_win[ring * K10S_FQW + (fq_head & (K10S_FQW - 1))]) and the cached root of the
+    // entry is fq_win[ring * K10S_FQW + (fq[ring].head & (K10S_FQW - 1))]) and the cached root of the
     // heap (valid while heap_size > 0)
-    uint32_t fq_head[K10S_NFQ], fq_tail[K10S_NFQ];
-    uint32_t fq_wend[K10S_NFQ];   // the window holds ring positions [fq_head, fq_wend)
-    double fq_last[K10S_NFQ];
+    FqRing fq[K10S_NFQ];
     HeapEv heap_top;
     HeapEv cur_ev;                // a trace event being handled (k10s_engine.h K10S_EV_BYREF)
     double tr_time;               // cached head of the shared trace stream (valid while
