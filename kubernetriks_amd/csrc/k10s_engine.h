@@ -987,6 +987,15 @@ K10S_HD bool scan_screen(uint32_t ac, uint64_t ar, float fa, float fr, float T) 
     const float fR = __builtin_fmaf((float)(uint32_t)(ar >> 32), 4294967296.0f, (float)(uint32_t)ar);
     return __builtin_fmaf(fa, fR, fr * fA) > fA * fR * T;
 }
+// The packed node cache's form of the screen (scan_lanes_screen_pk, which evaluates the same
+// operations two nodes per packed f32 instruction): entry x = cpu << 40 | ram, hi = x >> 32, lo =
+// (uint32_t)x; H = hi with the ram byte cleared = cpu·2^8 exactly (cpu < 2^24), and the test is
+// scan_screen's scaled by 2^8 (exact): the same decision as scan_screen on (cpu, ram).
+K10S_HD bool pk_screen_out(uint32_t hi, uint32_t lo, float fa256, float fr, float T) {
+    const float H = (float)(hi & 0xFFFFFF00u);
+    const float R = __builtin_fmaf((float)(hi & 0xFFu), 4294967296.0f, (float)lo);
+    return __builtin_fmaf(fa256, R, fr * H) > (H * R) * T;
+}
 // u of a scored node from its exact score: (100 − s)/50, rounded to f32.
 K10S_HD float screen_u(double s) { return (float)((100.0 - s) * 0.02); }
 
@@ -1108,6 +1117,104 @@ K10S_D float wave_min_f32(float v) {
 #ifndef K10S_UNIT_SCREEN
 #define K10S_UNIT_SCREEN 1
 #endif
+// The packed node cache's screened scan (event loop; K10S_SCAN_PK_SCREEN, default 1).  Same
+// decisions as scan_lanes_screen over the decoded entries, with fewer instructions per node:
+//  * Fit on the packed word: cpu >= rc  <=>  hi >= rc << 8 (hi = the entry's high word, cpu << 8 |
+//    ram >> 32; rc < 2^24, else nothing fits), ram >= rr on the low 40 bits;
+//  * the screen converts hi with its ram byte cleared, cpu·2^8 exactly, and evaluates scan_screen's
+//    test scaled by 2^8 (exact), as  fa·2^8·R + fr·H > H·R·T: the same decisions as scan_screen
+//    (pk_screen_out; tests/test_scan_screen.py test_packed_screen_*), and every node it keeps is
+//    scored exactly as before;
+//  * per-node decisions stay lane masks (SGPR pairs) instead of a per-lane 4-bit VGPR mask, and
+//    the valid-node mask is only built for the last, partial 512-node block.
+#ifndef K10S_SCAN_PK_SCREEN
+#define K10S_SCAN_PK_SCREEN 1
+#endif
+K10S_D float cvt_f32_ubyte0(uint32_t v) {   // (float)(v & 0xFF) as the one instruction
+    float f;
+    asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(f) : "v"(v));
+    return f;
+}
+// A node the screen kept (need): scored exactly.
+K10S_D void pk_score_node(bool need, uint64_t x, uint32_t n, double frc, double frr, double& best_s, int32_t& best_n,
+                          float& lu, bool& scored) {
+    if (need) {
+        // scored exactly (a node with the lane best's allocatables gets the same score and, being
+        // later, the index: "score >= best")
+        scored = true;
+        const uint32_t ac = (uint32_t)(x >> 40);
+        const uint64_t ar = x & K10S_PK_RAM;
+        const double fac = (double)ac;
+        const double cs = div_rn((fac - frc) * 100.0, fac);
+        const double s = (cs + div_rn((u64_f64(ar) - frr) * 100.0, u64_f64(ar))) * 0.5;   // ar < 2^40: exact
+        best_n = s >= best_s ? (int32_t)n : best_n;
+        best_s = s >= best_s ? s : best_s;
+        const float u = screen_u(s);
+        lu = u < lu ? u : lu;
+    }
+}
+K10S_D void scan_lanes_screen_pk(const uint64_t* s_node, uint32_t n_nodes, uint32_t rc, uint64_t rr, double& best_s,
+                                 int32_t& best_n) {
+    const uint32_t l4 = 4u * (uint32_t)lane_id();
+    rc = uniform_u32(rc);
+    rr = uniform_u64(rr);
+    if (n_nodes == 0 || rc > K10S_PK_CPU || rr > K10S_PK_RAM) return;   // no packed entry can hold them
+    const double frc = uniform_f64((double)rc), frr = uniform_f64(u64_f64(rr));
+    const float fa256 = (float)rc * 256.0f;
+    const float fr = __builtin_fmaf((float)(uint32_t)(rr >> 32), 4294967296.0f, (float)(uint32_t)rr);
+    const uint32_t rc8 = rc << 8;
+    float lu = __builtin_inff();
+    float T = __builtin_inff();
+    const f32x2 two32 = {4294967296.0f, 4294967296.0f}, va = {fa256, fa256}, vr = {fr, fr};
+    auto step = [&](ulonglong2 x01, ulonglong2 x23, uint32_t n0, auto mask) {
+        constexpr bool M = decltype(mask)::value;
+        const uint32_t h0 = (uint32_t)(x01.x >> 32), h1 = (uint32_t)(x01.y >> 32), h2 = (uint32_t)(x23.x >> 32),
+                       h3 = (uint32_t)(x23.y >> 32);
+        // the screen of the 4 nodes, 2 per packed f32 op
+        const f32x2 H01 = {cvt_f32_u32(h0 & 0xFFFFFF00u), cvt_f32_u32(h1 & 0xFFFFFF00u)};
+        const f32x2 H23 = {cvt_f32_u32(h2 & 0xFFFFFF00u), cvt_f32_u32(h3 & 0xFFFFFF00u)};
+        const f32x2 B01 = {cvt_f32_ubyte0(h0), cvt_f32_ubyte0(h1)}, B23 = {cvt_f32_ubyte0(h2), cvt_f32_ubyte0(h3)};
+        const f32x2 L01 = {cvt_f32_u32((uint32_t)x01.x), cvt_f32_u32((uint32_t)x01.y)};
+        const f32x2 L23 = {cvt_f32_u32((uint32_t)x23.x), cvt_f32_u32((uint32_t)x23.y)};
+        const f32x2 R01 = __builtin_elementwise_fma(B01, two32, L01), R23 = __builtin_elementwise_fma(B23, two32, L23);
+        const f32x2 vT = {T, T};
+        const f32x2 l01 = __builtin_elementwise_fma(va, R01, vr * H01), l23 = __builtin_elementwise_fma(va, R23, vr * H23);
+        const f32x2 r01 = (H01 * R01) * vT, r23 = (H23 * R23) * vT;
+        const bool n0k = rc8 <= h0 && rr <= (x01.x & K10S_PK_RAM) && !(l01.x > r01.x) && (!M || n0 < n_nodes);
+        const bool n1k = rc8 <= h1 && rr <= (x01.y & K10S_PK_RAM) && !(l01.y > r01.y) && (!M || n0 + 1 < n_nodes);
+        const bool n2k = rc8 <= h2 && rr <= (x23.x & K10S_PK_RAM) && !(l23.x > r23.x) && (!M || n0 + 2 < n_nodes);
+        const bool n3k = rc8 <= h3 && rr <= (x23.y & K10S_PK_RAM) && !(l23.y > r23.y) && (!M || n0 + 3 < n_nodes);
+        bool scored = false;
+        pk_score_node(n0k, x01.x, n0, frc, frr, best_s, best_n, lu, scored);
+        pk_score_node(n1k, x01.y, n0 + 1, frc, frr, best_s, best_n, lu, scored);
+        pk_score_node(n2k, x23.x, n0 + 2, frc, frr, best_s, best_n, lu, scored);
+        pk_score_node(n3k, x23.y, n0 + 3, frc, frr, best_s, best_n, lu, scored);
+        if (__ballot(scored)) {   // thr moves only when some lane scored a node exactly
+            const float thr = __builtin_bit_cast(float, uniform_u32(__builtin_bit_cast(uint32_t, wave_min_f32(lu))));
+            T = thr + K10S_SCREEN_EPS;
+        }
+    };
+    // whole 512-node blocks: the four 16-B loads of a lane from one address (offsets 0, 16, 2048,
+    // 2064 B), issued before any of them is used
+    uint32_t base = 0;
+    for (; base + 512u <= n_nodes; base += 512) {
+        const ulonglong2* p = reinterpret_cast<const ulonglong2*>(s_node + base + l4);
+        const ulonglong2 x0 = p[0], x1 = p[1], x2 = p[128], x3 = p[129];
+        step(x0, x1, base + l4, std::false_type());
+        step(x2, x3, base + 256u + l4, std::false_type());
+    }
+    if (base < n_nodes) {   // the partial last block: clamped addresses, masked nodes
+        const uint32_t a0 = base + l4, a1 = base + 256u + l4;
+        const uint32_t b0 = a0 < n_nodes ? a0 : 0u, b1 = a1 < n_nodes ? a1 : 0u;   // past the end: re-read 0..3
+        const ulonglong2 x0 = *reinterpret_cast<const ulonglong2*>(s_node + b0);
+        const ulonglong2 x1 = *reinterpret_cast<const ulonglong2*>(s_node + b0 + 2);
+        const ulonglong2 x2 = *reinterpret_cast<const ulonglong2*>(s_node + b1);
+        const ulonglong2 x3 = *reinterpret_cast<const ulonglong2*>(s_node + b1 + 2);
+        step(x0, x1, a0, std::true_type());
+        step(x2, x3, a1, std::true_type());
+    }
+}
+
 template <int PIPE, bool NP = true, bool PK = false>
 K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
                               uint32_t rc, uint64_t rr, double& best_s, int32_t& best_n) {
@@ -1204,7 +1311,9 @@ K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const ui
         // A fitting node has alloc >= request > 0 in both resources, so neither term is 0/0 and every
         // score is a finite number >= 0: filtered[0] is never NaN, "some node fits" <=> best_n >= 0,
         // and neither filtered[0] nor its re-scored value is needed (kube_scheduler.rs:140-148).
-        if (LOOP && K10S_SCAN_SCREEN)
+        if (LOOP && K10S_SCAN_SCREEN && PK && K10S_SCAN_PK_SCREEN)
+            scan_lanes_screen_pk(s_ram, n_nodes, rc, rr, best_s, best_n);
+        else if (LOOP && K10S_SCAN_SCREEN)
             scan_lanes_screen<K10S_LOOP_SCAN_PIPE, true, PK>(s_cpu, s_ram, present, n_nodes, rc, rr, best_s, best_n);
         else if (!LOOP && K10S_UNIT_SCREEN)
             scan_lanes_screen<K10S_SCAN_PIPE, false, PK>(s_cpu, s_ram, present, n_nodes, rc, rr, best_s, best_n);

@@ -202,3 +202,9 @@ extern "C" int hc_scan_screen(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr
     return scan_screen(ac, ar, fa, fr, thr + K10S_SCREEN_EPS) ? 1 : 0;
 }
 extern "C" float hc_screen_u(double s) { return screen_u(s); }
+// The packed-entry screen (k10s_engine.h pk_screen_out, as scan_lanes_screen_pk forms its operands).
+extern "C" int hc_scan_screen_pk(uint64_t x, uint32_t rc, uint64_t rr, float thr) {
+    const float fa256 = (float)rc * 256.0f;
+    const float fr = __builtin_fmaf((float)(uint32_t)(rr >> 32), 4294967296.0f, (float)(uint32_t)rr);
+    return pk_screen_out((uint32_t)(x >> 32), (uint32_t)x, fa256, fr, thr + K10S_SCREEN_EPS) ? 1 : 0;
+}
