@@ -31,7 +31,8 @@ GPU, and exits with their status; under torch.distributed.run WORLD_SIZE must eq
 Prints ONE JSON line (rank 0).  `value` = placements of all ranks / max-over-ranks wall time of
 the timed steps.  `roofline`: the dominant kernel is k10s_run_kernel (the whole event loop incl. the
 scheduling scans); algorithmic bytes per launch = Σ_attempts (12·|node cache| + 12) + 12·placements
-(SURVEY.md §8(d)), divided by the launch's HIP-event time, against the 8 TB/s HBM3E peak.
+(SURVEY.md §8(d)), divided by the launch's HIP-event time, against the 8 TB/s HBM3E peak.  The packed
+node cache reads 8 B per node for the same work; that rate is `achieved_physical` / `frac_physical`.
 `cpu_baseline`: the repo's CPU oracle (a string-keyed restatement of the reference, kind "port";
 the Rust reference cannot be built here), one process per usable host core, each running one
 replica of the same workload to completion.
@@ -360,12 +361,18 @@ def main():
     # per scanned node: the node-cache entry (8 B packed cpu << 40 | ram, 12 B wide u32 + u64;
     # k10s_capacities.node_cache); MostAllocated also reads the node's capacity (12 B, wide only).
     # Per attempt the pod's request (12 B); per placement the entry's reservation write.
+    # `achieved` is priced as SURVEY.md §8(d) prices the algorithm: 12 B per scanned node (u32 cpu + u64
+    # ram of the reference's node cache), 12 B per attempt (the request), 12 B per placement; + 12 B of
+    # capacity per node for MostAllocated.  The packed node cache (8 B per node, cpu << 40 | ram) moves
+    # fewer bytes for the same work: that physical rate is reported beside it (`*_physical`).
     entry_b = float(eng.node_entry_bytes)
-    node_b = entry_b + (0.0 if args.score_plugins == "least" else 12.0)
-    per_launch_bytes = (node_b * scanned + 12.0 * attempts + entry_b * placements) / (args.steps * world)
+    extra_b = 0.0 if args.score_plugins == "least" else 12.0
+    per_launch_bytes = ((12.0 + extra_b) * scanned + 12.0 * attempts + 12.0 * placements) / (args.steps * world)
     achieved = per_launch_bytes / (mean_kernel_ms * 1e-3) if mean_kernel_ms > 0 else 0.0
+    phys_bytes = ((entry_b + extra_b) * scanned + 12.0 * attempts + entry_b * placements) / (args.steps * world)
+    achieved_phys = phys_bytes / (mean_kernel_ms * 1e-3) if mean_kernel_ms > 0 else 0.0
     # what the scans actually read (pruned scan: block bounds + scanned blocks + bound upkeep)
-    touched_bytes = (node_b * nread + 12.0 * attempts + entry_b * placements) / (args.steps * world)
+    touched_bytes = ((entry_b + extra_b) * nread + 12.0 * attempts + entry_b * placements) / (args.steps * world)
     traffic = None if args.selftest_host else pmc_traffic(args.workload, R, args.nodes, args.pods, args.pruned_scan,
                                                             args.score_plugins, version())
     out = {
@@ -390,6 +397,9 @@ def main():
                      "frac": achieved / HBM_PEAK, "traffic": traffic,
                      "kernel": "k10s_run_kernel", "kernel_ms_per_launch": mean_kernel_ms,
                      "algorithmic_bytes_per_launch": per_launch_bytes,
+                     "pricing": "SURVEY.md 8(d): 12 B per scanned node + 12 B per attempt + 12 B per placement",
+                     "node_entry_bytes": int(entry_b), "physical_bytes_per_launch": phys_bytes,
+                     "achieved_physical": achieved_phys / 1e9, "frac_physical": achieved_phys / HBM_PEAK,
                      "scan_mode": "pruned" if args.pruned_scan else "full",
                      "touched_bytes_per_launch": touched_bytes,
                      "touched_GBps": touched_bytes / (mean_kernel_ms * 1e-3) / 1e9 if mean_kernel_ms > 0 else 0.0},
@@ -472,14 +482,17 @@ def backlog_line(args, cfg, make_engine, caps, ensemble, num_counters, version):
     c = eng.counter_matrix().sum(axis=0, dtype=np.uint64).astype(np.int64)
     placements, attempts, scanned = int(c[12]), int(c[13]), int(c[15])
     entry_b = float(eng.node_entry_bytes)
-    per_launch = entry_b * scanned + 12.0 * attempts + entry_b * placements
+    per_launch = 12.0 * scanned + 12.0 * attempts + 12.0 * placements   # SURVEY.md 8(d) pricing, as the headline
     achieved = per_launch / (ms * 1e-3) if ms > 0 else 0.0
+    phys = entry_b * scanned + 12.0 * attempts + entry_b * placements
     log(f"backlog: {placements / elapsed / 1e6:.2f} M placements/s, run {ms:.1f} ms")
     return {"workload": desc, "workload_name": "c3_backlog", "steps": 1, "warmup": 0,
             "placements_per_s": placements / elapsed, "attempts_per_s": attempts / elapsed,
             "ms_per_step": elapsed * 1e3, "kernel_ms_per_launch": ms,
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK, "algorithmic_bytes_per_launch": per_launch,
+                         "node_entry_bytes": int(entry_b), "physical_bytes_per_launch": phys,
+                         "frac_physical": (phys / (ms * 1e-3) if ms > 0 else 0.0) / HBM_PEAK,
                          "traffic": pmc_traffic("c3_backlog", args.replicas, args.nodes, args.pods, args.pruned_scan,
                                                 "least", version())},
             "totals": {"placements": placements, "attempts": attempts, "requeued": int(c[17]), "flushed": int(c[18])},

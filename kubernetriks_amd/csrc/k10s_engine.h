@@ -1117,7 +1117,8 @@ K10S_D float wave_min_f32(float v) {
 #ifndef K10S_UNIT_SCREEN
 #define K10S_UNIT_SCREEN 1
 #endif
-// The packed node cache's screened scan (event loop; K10S_SCAN_PK_SCREEN, default 1).  Same
+// The packed node cache's screened scan (event loop; K10S_SCAN_PK_SCREEN, default 0: measured slower,
+// profiles/r03_g1_pk_screen_ab.json — C3 1,341 vs 1,296 ms, backlog 4,089 vs 3,871 ms).  Same
 // decisions as scan_lanes_screen over the decoded entries, with fewer instructions per node:
 //  * Fit on the packed word: cpu >= rc  <=>  hi >= rc << 8 (hi = the entry's high word, cpu << 8 |
 //    ram >> 32; rc < 2^24, else nothing fits), ram >= rr on the low 40 bits;
@@ -1128,7 +1129,7 @@ K10S_D float wave_min_f32(float v) {
 //  * per-node decisions stay lane masks (SGPR pairs) instead of a per-lane 4-bit VGPR mask, and
 //    the valid-node mask is only built for the last, partial 512-node block.
 #ifndef K10S_SCAN_PK_SCREEN
-#define K10S_SCAN_PK_SCREEN 1
+#define K10S_SCAN_PK_SCREEN 0
 #endif
 K10S_D float cvt_f32_ubyte0(uint32_t v) {   // (float)(v & 0xFF) as the one instruction
     float f;
