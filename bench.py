@@ -445,7 +445,7 @@ def main():
                                                                          "cycles_per_event": kc[k] / max(kn[k], 1)}
                                          for k in range(len(kc)) if kn[k]}
     if rank == 0 and world == 1 and args.workload == "c3" and args.score_plugins == "least" and not args.no_backlog_line and not args.selftest_host:
-        # the same replicas under load (failed attempts, unschedulable map, move-all, flush): one launch
+        # the same replicas under load (failed attempts, unschedulable map, move-all on every finish): one launch
         try:
             del eng
             out["backlog"] = backlog_line(args, cfg, make_engine, caps, ensemble, NUM_COUNTERS, version)
