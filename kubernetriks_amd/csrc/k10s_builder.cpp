@@ -579,7 +579,7 @@ bool build_scenario(const std::string& text, uint32_t group_bound_in, uint32_t c
         for (size_t i = 0; i < cluster.size(); i++) {
             const BTrace& t = cluster[i];
             TraceEv e;
-            e.time = t.ts;
+            e.time = 0.0 + t.ts;  // dslab: time = clock (0 at initialize) + delay, so -0.0 -> +0.0
             e.seq = seq++;
             e.kind = (uint32_t)t.kind;
             e.wpos = K10S_TRACE_CLUSTER;
@@ -600,7 +600,7 @@ bool build_scenario(const std::string& text, uint32_t group_bound_in, uint32_t c
         for (uint32_t x : is_pod) hs.wl_pods_upto.push_back(hs.wl_pods_upto.back() + x);
         for (const BTrace& t : workload) {
             TraceEv e;
-            e.time = t.ts;
+            e.time = 0.0 + t.ts;  // (as above)
             e.seq = seq++;
             e.kind = (uint32_t)t.kind;
             e.wpos = t.pos;
@@ -745,6 +745,26 @@ std::string params_error(const Params& p, const HostScenario& hs) {
 bool nodes_packable(const HostScenario& hs) {
     for (size_t d = 0; d < hs.def_cpu.size(); d++)
         if (hs.def_cpu[d] >= (1u << 24) || hs.def_ram[d] >= (1ull << 40)) return false;
+    return true;
+}
+
+// A value with the sign bit set other than -0.0 (negative numbers, -inf, negative NaNs).
+static bool signed_time(double x) { return std::signbit(x) && x != 0.0; }
+
+bool times_nonneg(const HostScenario& hs, const Params* params, uint32_t n_params) {
+    for (const TraceEv& t : hs.trace)
+        if (signed_time(t.time)) return false;
+    for (double d : hs.pod_dur)
+        if (signed_time(d)) return false;
+    for (double d : hs.unit_dur)
+        if (signed_time(d)) return false;
+    for (uint32_t r = 0; r < n_params; r++) {
+        const Params& p = params[r];
+        for (double d : {p.scheduling_cycle_interval, p.as_to_ps_network_delay, p.ps_to_sched_network_delay,
+                         p.sched_to_as_network_delay, p.as_to_node_network_delay, p.as_to_ca_network_delay,
+                         p.as_to_hpa_network_delay, p.ca_scan_interval, p.hpa_scan_interval})
+            if (signed_time(d)) return false;
+    }
     return true;
 }
 

@@ -71,8 +71,13 @@ std::vector<uint8_t> pack_scenario(const HostScenario& hs, Scenario& view_offset
 Scenario rebase_scenario(const Scenario& view_offsets, const uint8_t* base);
 
 // allow_packed: false when some replica needs the wide node cache (a score plugin beyond
-// LeastAllocated: the plugin kernel reads capacities from the wide SoA).
+// LeastAllocated: the plugin kernel reads capacities from the wide SoA) or the general event-time
+// key (!times_nonneg): the packed layout runs in the default kernel, which keys times by their bits.
 Layout make_layout(const HostScenario& hs, const k10s_capacities& caps, bool allow_packed);
+// Every event time of the scenario under these replica parameters carries no sign bit (trace
+// timestamps, pod and usage-unit durations, network delays, tick intervals; -0.0 allowed), so the
+// default kernel's bit-pattern time key orders them like total_cmp (k10s_common.h total_key).
+bool times_nonneg(const HostScenario& hs, const Params* params, uint32_t n_params);
 // Every node definition fits the packed node-cache entry (cpu < 2^24, ram < 2^40).
 bool nodes_packable(const HostScenario& hs);
 

@@ -81,9 +81,23 @@ K10S_HD double u2f(uint64_t u) {
 K10S_HD bool is_nan(double x) { return x != x; }
 
 // Rust f64::total_cmp key: monotone in the IEEE total order (core/num/f64.rs).
+// K10S_TIME_KEY_ID = 1: the key is the value's bit pattern itself.  For every value without the
+// sign bit (+0.0 ... +inf, positive NaNs) total_cmp's transform is the identity, and -0.0 maps to
+// INT64_MIN, still below all of them; only two distinct negative values (or negative NaNs) would
+// compare the wrong way round.  The default event-loop kernel (k10s_kernels.hip) is compiled with 1
+// and runs only scenarios whose every event time is such a value: trace timestamps, durations,
+// network delays and tick intervals carry no sign (times_nonneg, k10s_builder.cpp), so every
+// clock + delay is one too; any other scenario runs the second kernel copy, compiled with 0 (the
+// full transform).  Saves the transform's five VALU instructions on every key (emit, consume, the
+// heap's sift steps, the source list): C3 1,297 -> 1,280 ms, profiles/r03_k1_time_key_ab.json.
+#ifndef K10S_TIME_KEY_ID
+#define K10S_TIME_KEY_ID 0
+#endif
 K10S_HD int64_t total_key(double x) {
     int64_t b = (int64_t)f2u(x);
+#if !K10S_TIME_KEY_ID
     b ^= (int64_t)(((uint64_t)(b >> 63)) >> 1);
+#endif
     return b;
 }
 // Unsigned key, monotone for non-NaN scores (argmax of LeastAllocated scores).  Never 0 for a

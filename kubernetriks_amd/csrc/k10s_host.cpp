@@ -289,7 +289,7 @@ k10s_engine* k10s_engine_create_bulk(const char* scenario_text, const void* pods
         }
     }
     // the node cache is packed unless some replica needs the wide SoA (k10s_capacities.node_cache)
-    e->L = make_layout(e->hs, c, !e->plugins);
+    e->L = make_layout(e->hs, c, !e->plugins && times_nonneg(e->hs, e->params.data(), n_replicas));
     e->wide = e->plugins || !e->L.packed;
     auto fail = [&](const std::string& m) -> k10s_engine* {
         set_err(K10S_E_HIP, m);

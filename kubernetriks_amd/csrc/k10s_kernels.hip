@@ -22,6 +22,12 @@
 #ifndef K10S_SCORE_PLUGINS
 #define K10S_SCORE_PLUGINS 0
 #endif
+// Event-time keys as the raw bit pattern (k10s_common.h total_key): this copy runs only scenarios
+// whose event times carry no sign bit (make_layout: packed only when times_nonneg); the plugins
+// copy keeps the full total_cmp transform.
+#ifndef K10S_TIME_KEY_ID
+#define K10S_TIME_KEY_ID 1
+#endif
 #include "k10s_engine.h"
 
 using namespace k10s;

@@ -11,6 +11,7 @@
 #define K10S_PACKED 0   // the wide node cache (u32 cpu + u64 ram SoA): plugin replicas read the capacity
                         // SoA beside it, and scenarios whose nodes do not fit the packed entry run here
 #define K10S_PLUGINS_TU 1
+#define K10S_TIME_KEY_ID 0   // the general total_cmp key: scenarios with signed event times run here
 #define k10s_dc k10s_dc_plugins
 #define k10s_hdr k10s_hdr_plugins
 #define k10s_sec k10s_sec_plugins

@@ -79,7 +79,7 @@ void* hc_create_bulk(const char* text, const void* blob, uint64_t blob_len, cons
     }
     bool plugins = false;
     for (uint32_t r = 0; r < R; r++) plugins |= h->params[r].score_plugins != K10S_SCORE_LEAST_ALLOCATED;
-    h->L = make_layout(h->hs, c, !plugins);
+    h->L = make_layout(h->hs, c, !plugins && times_nonneg(h->hs, h->params.data(), R));
     h->state.assign((size_t)h->L.stride * R, 0);
     for (uint32_t r = 0; r < R; r++) {
         RepHdr work;

@@ -84,3 +84,35 @@ def test_layout_choice(backend):
     params[1].most_allocated_weight = 1.0
     assert E(scn, 2, params=params).node_entry_bytes == 12
     assert E(scn, 2).replica_bytes < E(scn, 2, caps=caps).replica_bytes   # 8 B/node and no capacity SoA
+
+
+def signed_time_scenario(t0: float) -> str:
+    """Pods created at t0 (and a little after), so the trace holds timestamps of t0's sign."""
+    c = GenericClusterTrace()
+    for k in range(4):
+        c.create_node(0.0, Node(f"node_{k}", 8000, 16 << 30))
+    w = GenericWorkloadTrace()
+    for i in range(40):
+        w.create_pod(t0 + (i % 5) * 0.5 if t0 else t0, Pod(f"pod_{i:03d}", 500 + 100 * (i % 7), (1 + i % 5) << 28,
+                                                           float(10 + 7 * (i % 9))))
+    return scenario_text(SimulationConfig(), c, w)
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_signed_event_times_take_the_general_key(backend):
+    """The default kernel keys event times by their bit pattern (k10s_common.h total_key), exact only
+    for values without the sign bit: a scenario with negative trace timestamps (or a negative network
+    delay) runs on the wide layout, i.e. the second kernel copy with total_cmp's full transform, and
+    matches the oracle; -0.0 timestamps keep the packed layout."""
+    E = engine_cls(backend)
+    od, eng = parity.run_pair(E, signed_time_scenario(-7.25), max_time=1e6)
+    assert eng.node_entry_bytes == 12
+    assert parity.compare(od, eng) == []
+    od, eng = parity.run_pair(E, signed_time_scenario(-0.0), max_time=1e6)
+    assert eng.node_entry_bytes == 8
+    assert parity.compare(od, eng) == []
+    scn = signed_time_scenario(3.0)
+    params = wl.replica_params(E(scn, 1).default_params(), 2)
+    assert E(scn, 2, params=params).node_entry_bytes == 8
+    params[1].as_to_ps_network_delay = -0.001
+    assert E(scn, 2, params=params).node_entry_bytes == 12
