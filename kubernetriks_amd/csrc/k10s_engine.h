@@ -848,6 +848,25 @@ K10S_D ScanGrp scan_load_pk(const uint64_t* s_node, const uint64_t* present, uin
     g.r23.y = x23.y & K10S_PK_RAM;
     return g;
 }
+// A whole group inside the node range (no clamp, no presence word).
+K10S_D ScanGrp scan_load_pk_full(const uint64_t* s_node, uint32_t n0) {
+    ScanGrp g;
+    g.pw = ~0ull;
+    const ulonglong2 x01 = *reinterpret_cast<const ulonglong2*>(s_node + n0);
+    const ulonglong2 x23 = *reinterpret_cast<const ulonglong2*>(s_node + n0 + 2);
+    g.cv.x = (uint32_t)(x01.x >> K10S_PK_SHIFT);
+    g.cv.y = (uint32_t)(x01.y >> K10S_PK_SHIFT);
+    g.cv.z = (uint32_t)(x23.x >> K10S_PK_SHIFT);
+    g.cv.w = (uint32_t)(x23.y >> K10S_PK_SHIFT);
+    g.r01.x = x01.x & K10S_PK_RAM;
+    g.r01.y = x01.y & K10S_PK_RAM;
+    g.r23.x = x23.x & K10S_PK_RAM;
+    g.r23.y = x23.y & K10S_PK_RAM;
+    return g;
+}
+#ifndef K10S_SCAN_FULLBLK
+#define K10S_SCAN_FULLBLK 1
+#endif
 // PK: s_ram is the packed node array (s_cpu unused)
 template <bool PK>
 K10S_D ScanGrp scan_load_x(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
@@ -1232,8 +1251,8 @@ K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, cons
     float T = __builtin_inff();  // thr + eps: +inf screens nothing out (the first step)
 #if K10S_SCREEN_PACKED
     // one 256-node step of a lane's group g at n0 (screen, exact scores, threshold)
-    auto step = [&](const ScanGrp& g, uint32_t n0) {
-        const uint32_t bits = grp_bits(g, n0, n_nodes);
+    auto step = [&](const ScanGrp& g, uint32_t n0, auto full) {
+        const uint32_t bits = decltype(full)::value ? 0xFu : grp_bits(g, n0, n_nodes);
         const uint32_t need = screen_grp(g, bits, rc, rr, fa, fr, T);
         if (need) {
             if (need & 1u) score_node_exact(n0, g.cv.x, g.r01.x, rr, frc, frr, best_s, best_n, la, lr, lu);
@@ -1249,12 +1268,24 @@ K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, cons
     // K10S_SCAN_STEPS2 (packed node cache, no load pipeline): the loads of two 256-node steps (32 B
     // per lane each) are issued together, so a 4,096-node scan waits 8 memory round trips, not 16;
     // a lane still visits its nodes in ascending order
+    // K10S_SCAN_FULLBLK (event loop, packed, no presence words): whole 512-node blocks load from
+    // unclamped addresses and screen all 4 nodes of a lane group without a validity mask; only the
+    // last, partial block builds one
     if (PK && K10S_SCAN_STEPS2 && PIPE == 0) {
-        for (uint32_t base = 0; base < n_nodes; base += 512) {
+        uint32_t base = 0;
+        if (K10S_SCAN_FULLBLK && NP && K10S_SCREEN_NO_PRESENCE) {
+            for (; base + 512u <= n_nodes; base += 512) {
+                const ScanGrp g0 = scan_load_pk_full(s_ram, base + l4);
+                const ScanGrp g1 = scan_load_pk_full(s_ram, base + 256u + l4);
+                step(g0, base + l4, std::true_type());
+                step(g1, base + 256u + l4, std::true_type());
+            }
+        }
+        for (; base < n_nodes; base += 512) {
             const ScanGrp g0 = SCREEN_LOAD(s_cpu, s_ram, present, n_nodes, base + l4);
             const ScanGrp g1 = SCREEN_LOAD(s_cpu, s_ram, present, n_nodes, base + 256u + l4);
-            step(g0, base + l4);
-            step(g1, base + 256u + l4);
+            step(g0, base + l4, std::false_type());
+            step(g1, base + 256u + l4, std::false_type());
         }
         return;
     }
