@@ -410,6 +410,16 @@ K10S_HD void heap_put(Ctx& c, uint32_t i, const HeapEv& e) {
 }
 #endif
 
+// Host-only event statistics (tooling: tools/host_stats.py builds the host engine with
+// -DK10S_HOST_STATS and reads k10s_host_stats); compiled out everywhere else.
+#if !K10S_DEVICE && defined(K10S_HOST_STATS)
+extern "C" uint64_t k10s_host_stats[32];
+#define K10S_HSTAT(i) (k10s_host_stats[i] += 1)
+#else
+#define K10S_HSTAT(i) ((void)0)
+#endif
+enum { HS_EVENTS, HS_FIFO_POP, HS_REFILL, HS_HEAP_POP, HS_TRACE_POP, HS_SL_FAST, HS_SL_UPDATE, HS_EMIT_WIN,
+       HS_EMIT_RING, HS_EMIT_HEAP, HS_SL_DIRTY, HS_SCANS, HS_REFILL_CLS0 = 12, HS_POP_CLS0 = 20 };
 // An emission changed source q's head: mark it for the source list.
 K10S_HD void sl_mark(RepHdr& H, uint32_t q) { H.sl_dirty |= 1u << q; }
 
@@ -449,8 +459,10 @@ K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uin
             if (we == tl && tl - hd < K10S_FQW) {  // the window holds the whole ring: append
                 H.fq_win[(uint32_t)cls * K10S_FQW + (tl & (K10S_FQW - 1))] = e;
                 H.fq[cls].wend = tl + 1;
+                K10S_HSTAT(HS_EMIT_WIN);
             } else {
                 c.V().fq()[(uint32_t)cls * cap + (tl & (cap - 1))] = e;
+                K10S_HSTAT(HS_EMIT_RING);
             }
             if (tl == hd) sl_mark(H, (uint32_t)cls);  // the ring was empty: a new head (source list)
             H.fq[cls].tail = tl + 1;
@@ -464,6 +476,7 @@ K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uin
         return 0;
     }
     H.next_seq = e.seq + 1;
+    K10S_HSTAT(HS_EMIT_HEAP);
     uint32_t pos = uniform_u32(hsize);
     H.heap_size = pos + 1;
     while (pos > 0) {
@@ -723,37 +736,30 @@ K10S_HD void s_move_after_free(Ctx& c, uint32_t cpu, uint64_t ram) {
     else s_move(c, 0, 0.0, 0, 0);
 }
 
-// ---- running-pod lists of node components ----------------------------------------------------
-K10S_HD void run_insert(Ctx& c, int32_t slot, uint32_t p) {
-    int32_t h = c.V().slot(slot).head;
-    c.V().pod(p).run_prev = -1;
-    c.V().pod(p).run_next = h;
-    if (h >= 0) c.V().pod(h).run_prev = (int32_t)p;
-    c.V().slot(slot).head = (int32_t)p;
-    c.V().pod(p).run_slot = slot;
-    if (c.Ly().cap_gauge) {  // allocate_pod_requests (node_component.rs:83-86): gauge recorder only
-        c.V().g_cpu()[slot] -= c.V().pod(p).req_cpu;
-        c.V().g_ram()[slot] -= c.V().pod(p).req_ram;
-    }
-}
-K10S_HD void run_remove(Ctx& c, uint32_t p) {
-    int32_t slot = c.V().pod(p).run_slot;
-    int32_t pr = c.V().pod(p).run_prev, nx = c.V().pod(p).run_next;
-    if (pr >= 0) c.V().pod(pr).run_next = nx;
-    else c.V().slot(slot).head = nx;
-    if (nx >= 0) c.V().pod(nx).run_prev = pr;
+// ---- running pods of node components -----------------------------------------------------------
+// A component's running_pods map (node_component.rs:33-47) is the set of pods whose run_slot is the
+// component; only cancel_all_running_pods (95-112, node removal) iterates it, and nothing it does per
+// pod depends on the order, so it is a lane-parallel sweep over run_slot (N_REMOVE_NODE) and a bind
+// or finish touches only the pod's own line and the component's count.
+// Remove running pod p (run_slot == slot, finish_seq == fs already loaded by the caller).
+K10S_HD void run_remove_at(Ctx& c, uint32_t p, int32_t slot, uint32_t fs) {
+    PodState& P = c.V().pod(p);
+    c.V().slot(slot).running -= 1;
     if (c.Ly().cap_gauge) {  // free_pod_requests (node_component.rs:88-91)
-        c.V().g_cpu()[slot] += c.V().pod(p).req_cpu;
-        c.V().g_ram()[slot] += c.V().pod(p).req_ram;
+        c.V().g_cpu()[slot] += P.req_cpu;
+        c.V().g_ram()[slot] += P.req_ram;
     }
-    c.V().pod(p).run_slot = -1;
+    P.run_slot = -1;
     // cancels a pending finish event (dslab cancel_event) unless it is the one being handled: the
     // canceled event stays in the heap until popped (counted in stale_fin)
-    const uint32_t fs = c.V().pod(p).finish_seq;
     if (fs != 0 && !(c.H().cur_kind == K10S_EV_N_POD_FINISHED && c.H().cur_seq == fs)) c.H().stale_fin += 1;
-    c.V().pod(p).finish_seq = 0;
+    P.finish_seq = 0;
     int32_t g = c.S().pod_group[p];
     if (g >= 0) c.V().grp()[g].running -= 1;
+}
+K10S_HD void run_remove(Ctx& c, uint32_t p) {
+    const PodState& P = c.V().pod(p);
+    run_remove_at(c, p, P.run_slot, P.finish_seq);
 }
 
 // ---- schedule_one: Fit filter + LeastAllocated score + argmax (the hot scan) -------------------
@@ -2208,24 +2214,41 @@ K10S_HD void ps_list_remove(Ctx& c, uint32_t n, uint32_t p) {
     if (nx >= 0) link[2 * nx] = pr;
 }
 
+// The node line's storage fields, loaded in one batch.
+struct PsNode {
+    uint8_t flags;
+    uint32_t cpu, epoch;
+    uint64_t ram;
+};
+K10S_HD PsNode ps_node_load(Ctx& c, uint32_t n) {
+    const NodeState& N = c.V().node(n);
+    PsNode v;
+    v.flags = N.flags;
+    v.cpu = N.ps_cpu;
+    v.epoch = N.ps_epoch;
+    v.ram = N.ps_ram;
+    return v;
+}
+// clean_up_pod (173-182) with the pod's fields loaded (n = ps_assigned) and node n's fields v.
+K10S_HD void ps_clean_up_at(Ctx& c, uint32_t p, int32_t n, uint32_t rc, uint64_t rr, uint32_t pae, const PsNode& v) {
+    if (n < 0) return;
+    if (v.flags & NF_PS_PRESENT) {
+        NodeState& N = c.V().node(n);
+        N.ps_cpu = v.cpu + rc;
+        N.ps_ram = v.ram + rr;
+        if (pae == v.epoch) {
+            c.V().pod(p).ps_aepoch = 0;
+            if (v.flags & NF_CA_ORIGIN) ps_list_remove(c, (uint32_t)n, p);
+        }
+    }
+}
 K10S_HD void ps_clean_up(Ctx& c, uint32_t p) {  // 173-182
     PodState& P = c.V().pod(p);
     const int32_t n = P.ps_assigned;
     const uint32_t rc = P.req_cpu, pae = P.ps_aepoch;
     const uint64_t rr = P.req_ram;
     if (n < 0) return;
-    NodeState& N = c.V().node(n);
-    const uint8_t nf = N.flags;  // one batch of loads from the node line
-    const uint32_t ncpu = N.ps_cpu, nep = N.ps_epoch;
-    const uint64_t nram = N.ps_ram;
-    if (nf & NF_PS_PRESENT) {
-        N.ps_cpu = ncpu + rc;
-        N.ps_ram = nram + rr;
-        if (pae == nep) {
-            P.ps_aepoch = 0;
-            if (nf & NF_CA_ORIGIN) ps_list_remove(c, (uint32_t)n, p);
-        }
-    }
+    ps_clean_up_at(c, p, n, rc, rr, pae, ps_node_load(c, (uint32_t)n));
 }
 
 K10S_WARM void on_ps(Ctx& c, K10S_EVARG) {
@@ -2331,12 +2354,19 @@ K10S_WARM void on_ps(Ctx& c, K10S_EVARG) {
     case K10S_EV_PS_POD_FINISHED: {
         uint32_t p = e.a;
         PodState& P = c.V().pod(p);
-        const uint8_t pf = P.flags, sflags = c.S().pod_flags[p];  // one batch of loads
+        // one batch of loads: the pod line, and the line of the node the pod ran on (e.b), which is
+        // its storage assignment unless the assignment changed meanwhile (then reloaded below)
+        const uint32_t hn = e.b < c.S().n_nodes ? e.b : 0u;
+        const PsNode hv = ps_node_load(c, hn);
+        const uint8_t pf = P.flags, sflags = c.S().pod_flags[p];
         const double dur = P.dur;
+        const int32_t pn = P.ps_assigned;
+        const uint32_t prc = P.req_cpu, pae = P.ps_aepoch;
+        const uint64_t prr = P.req_ram;
         if (pf & PF_IN_PS) {
             P.flags = (uint8_t)(pf & ~PF_IN_PS);
             if (pf & PF_UNSCHED) h->unsched_missing += 1;
-            ps_clean_up(c, p);
+            if (pn >= 0) ps_clean_up_at(c, p, pn, prc, prr, pae, (uint32_t)pn == hn ? hv : ps_node_load(c, (uint32_t)pn));
             if (!(sflags & POD_HAS_DUR)) {
                 fail(c, K10S_PANIC_MISSING_POD);
                 return;
@@ -2508,7 +2538,7 @@ K10S_WARM void on_api_server(Ctx& c, K10S_EVARG) {
         c.V().slot(slot).removed = 0;
         c.V().slot(slot).rtime = 0.0;
         c.V().slot(slot).gen += 1;
-        c.V().slot(slot).head = -1;
+        c.V().slot(slot).running = 0;
         uint32_t tail = (h->pool_head + h->pool_count) % sc->n_slots;
         c.V().pool_ring()[tail] = (uint32_t)slot;
         h->pool_count += 1;
@@ -2587,7 +2617,7 @@ K10S_WARM void on_node(Ctx& c, K10S_EVARG) {
         SlotState& SL = c.V().slot(slot);
         PodState& P = c.V().pod(p);
         const uint32_t removed = SL.removed;
-        const int32_t snode = SL.node, shead = SL.head;
+        const int32_t snode = SL.node, srun = SL.running;
         const int32_t prs = P.run_slot;
         const double dur = P.dur;
         const uint8_t sflags = c.S().pod_flags[p];
@@ -2607,11 +2637,7 @@ K10S_WARM void on_node(Ctx& c, K10S_EVARG) {
         uint32_t fseq = 0;
         if (sflags & POD_HAS_DUR)  // simulate_pod_runtime (114-175)
             fseq = emit(c, K10S_EV_N_POD_FINISHED, dur + pr->as_to_node_network_delay, slot, p, n, e.time + dur);
-        // run_insert with the head loaded above (emit touches only the event queue)
-        P.run_prev = -1;
-        P.run_next = shead;
-        if (shead >= 0) c.V().pod(shead).run_prev = (int32_t)p;
-        SL.head = (int32_t)p;
+        SL.running = srun + 1;   // the count loaded above (emit touches only the event queue)
         P.run_slot = slot;
         P.finish_seq = fseq;
         if (c.Ly().cap_gauge) {  // allocate_pod_requests (node_component.rs:83-86, called at 164)
@@ -2624,11 +2650,13 @@ K10S_WARM void on_node(Ctx& c, K10S_EVARG) {
     }
     case K10S_EV_N_POD_FINISHED: {
         uint32_t p = e.a;
-        if (c.V().pod(p).run_slot != slot) {
+        const int32_t rs = c.V().pod(p).run_slot;   // one batch of loads from the pod line
+        const uint32_t fs = c.V().pod(p).finish_seq;
+        if (rs != slot) {
             fail(c, K10S_PANIC_MISSING_POD);
             return;
         }
-        run_remove(c, p);
+        run_remove_at(c, p, slot, fs);
         emit(c, K10S_EV_AS_POD_FINISHED, 0.0, -1, p, e.b, e.x, FQ_NOW);  // emit_now
         break;
     }
@@ -2638,16 +2666,17 @@ K10S_WARM void on_node(Ctx& c, K10S_EVARG) {
             fail(c, K10S_PANIC_REMOVE_OTHER_NODE);
             return;
         }
-        // cancel_all_running_pods (95-112)
-        int32_t p = c.V().slot(slot).head;
-        uint32_t gen = c.V().slot(slot).gen;
-        while (p >= 0) {
-            int32_t nx = c.V().pod(p).run_next;
-            c.V().pod(p).cancel_slot = slot;
-            c.V().pod(p).cancel_gen = gen;
-            run_remove(c, (uint32_t)p);
-            p = nx;
-        }
+        // cancel_all_running_pods (95-112): the pods whose run_slot is this component, in index order
+        // (the per-pod work is order-independent)
+        const uint32_t gen = c.V().slot(slot).gen;
+        if (c.V().slot(slot).running > 0)
+            for_each_pod_in_order(
+                c, [&](uint32_t p) { return c.V().pod(p).run_slot == slot; },
+                [&](uint32_t p) {
+                    c.V().pod(p).cancel_slot = slot;
+                    c.V().pod(p).cancel_gen = gen;
+                    run_remove(c, p);
+                });
         emit(c, K10S_EV_AS_NODE_REMOVED, pr->as_to_node_network_delay, -1, n, 0, e.time, FQ_AS_TO_NODE);
         c.V().slot(slot).removed = 1;
         c.V().slot(slot).rtime = e.time;
@@ -3017,8 +3046,6 @@ K10S_HD void init_replica(Ctx& c) {
         ps.s_assigned = -1;
         ps.ps_assigned = -1;
         ps.run_slot = -1;
-        ps.run_prev = -1;
-        ps.run_next = -1;
         ps.cancel_slot = -1;
         v.pod(p) = ps;
         if (prec) {
@@ -3032,7 +3059,6 @@ K10S_HD void init_replica(Ctx& c) {
     SlotState ss;
     memset(&ss, 0, sizeof ss);
     ss.node = -1;
-    ss.head = -1;
     for (uint32_t s = lane; s < S; s += K10S_LANES) {
         v.slot((int32_t)s) = ss;
         v.pool_ring()[s] = s;  // pool contexts first (FIFO), default-node components after
@@ -3213,6 +3239,7 @@ K10S_HD void sl_apply_dirty(Ctx& c, uint32_t ntr) {
     do {
         const uint32_t q = (uint32_t)__builtin_ctz(d);
         d &= d - 1;
+        K10S_HSTAT(HS_SL_DIRTY);
         sl_refresh(c, q, ntr);
     } while (d);
 }
@@ -3247,7 +3274,9 @@ K10S_HD void consume_source(Ctx& c, int src, uint32_t ntr) {
     bool has;
     int64_t key = 0;
     uint32_t seq = 0;
+    K10S_HSTAT(HS_EVENTS);
     if (src == SRC_TRACE) {
+        K10S_HSTAT(HS_TRACE_POP);
         const uint32_t cur = trace_head_load(c, H.trace_cursor + 1);
         has = cur < ntr;
         if (has) {
@@ -3257,15 +3286,22 @@ K10S_HD void consume_source(Ctx& c, int src, uint32_t ntr) {
     } else if (src == SRC_HEAP) {
         const uint64_t t_hp = prof_now();
         heap_pop(c);
+        K10S_HSTAT(HS_HEAP_POP);
         K10S_PROF_ADD(c, PROF_HEAPPOP, t_hp);
         K10S_PROF_COUNT(c, PROF_NHEAPPOP);
         has = src_head(c, SRC_HEAP, ntr, key, seq);
     } else {
         const uint32_t hd = H.fq[src].head + 1, tl = H.fq[src].tail, we = H.fq[src].wend;
+        K10S_HSTAT(HS_POP_CLS0 + src);
         H.fq[src].head = hd;
         has = hd != tl;
+        K10S_HSTAT(HS_FIFO_POP);
         if (has) {
-            if (hd == we) fq_refill(c, src, hd);
+            if (hd == we) {
+                fq_refill(c, src, hd);
+                K10S_HSTAT(HS_REFILL);
+                K10S_HSTAT(HS_REFILL_CLS0 + src);
+            }
             const HeapEv& t = H.fq_win[(uint32_t)src * K10S_FQW + (hd & (K10S_FQW - 1))];
             key = total_key(t.time);
             seq = t.seq;
@@ -3285,9 +3321,11 @@ K10S_HD void consume_source(Ctx& c, int src, uint32_t ntr) {
         if (stays) {
             H.sl[0].key = key;
             H.sl[0].seq = seq;
+            K10S_HSTAT(HS_SL_FAST);
             return;
         }
     }
+    K10S_HSTAT(HS_SL_UPDATE);
     sl_update(c, (uint32_t)src, has, key, seq);
 }
 

@@ -302,7 +302,7 @@ struct PodState {
     int32_t ps_assigned;    // storage pod.status.assigned_node
     uint32_t ps_aepoch;     // member of PS assignments[ps_assigned] iff == that node's epoch
     int32_t run_slot;       // node component running it (running_pods), or -1
-    int32_t run_prev, run_next;   // intrusive list of running pods per component
+    uint32_t spare0, spare1;  // unused (round 2 kept a per-component running list here)
     uint32_t finish_seq;    // id of its pending PodFinishedRunning self-event (0 = none/canceled)
     int32_t cancel_slot;    // canceled_pods membership: (slot, slot generation)
     uint32_t cancel_gen;
@@ -328,7 +328,7 @@ struct SlotState {
     int32_t node;           // runtime node idx, -1 when back in the pool
     uint32_t def;
     uint32_t gen;           // bumped on reclaim (clears canceled_pods)
-    int32_t head;           // running-pod list head
+    int32_t running;        // pods running on the component (node removal sweeps only if > 0)
     double rtime;           // removal_time
     uint32_t removed;
     uint32_t pad;
