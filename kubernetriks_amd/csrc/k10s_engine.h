@@ -419,7 +419,7 @@ extern "C" uint64_t k10s_host_stats[32];
 #define K10S_HSTAT(i) ((void)0)
 #endif
 enum { HS_EVENTS, HS_FIFO_POP, HS_REFILL, HS_HEAP_POP, HS_TRACE_POP, HS_SL_FAST, HS_SL_UPDATE, HS_EMIT_WIN,
-       HS_EMIT_RING, HS_EMIT_HEAP, HS_SL_DIRTY, HS_SCANS, HS_REFILL_CLS0 = 12, HS_POP_CLS0 = 20 };
+       HS_EMIT_RING, HS_EMIT_HEAP, HS_SL_DIRTY, HS_SCANS, HS_REFILL_CLS0 = 12, HS_POP_CLS0 = 20, HS_AQ_HBM_GET = 28, HS_AQ_POP = 29 };
 // An emission changed source q's head: mark it for the source list.
 K10S_HD void sl_mark(RepHdr& H, uint32_t q) { H.sl_dirty |= 1u << q; }
 
@@ -586,7 +586,10 @@ K10S_HD QInfo aq_get(Ctx& c, uint32_t i) {
     if (i < K10S_AQ_TOP) q = c.H().aq_lds[i];
     else
 #endif
+    {
         q = c.V().aq()[i];
+        K10S_HSTAT(HS_AQ_HBM_GET);
+    }
 #if K10S_DEVICE
     q.timestamp = uniform_f64(q.timestamp);
     q.initial = uniform_f64(q.initial);
@@ -624,7 +627,11 @@ K10S_HELPER void aq_push(Ctx& c, const QInfo& q) {
     uint32_t old = c.H().aq_size++;
     aq_sift_up(c, 0, old, q);
 }
+// (Round 3 tried reading the 3-level subtree under the walk's position in one round trip below the
+// LDS levels: C3 +0.6 %, backlog -2 to -4 % from the extra SGPRs live in the scheduling cycle,
+// profiles/r03_k4_sflag_subtree_ab.json; not kept.)
 K10S_HELPER QInfo aq_pop(Ctx& c) {
+    K10S_HSTAT(HS_AQ_POP);
     const uint32_t end = --c.H().aq_size;
     QInfo item = aq_get(c, end);
     if (end == 0) return item;
@@ -680,7 +687,7 @@ K10S_HELPER void uq_insert(Ctx& c, const QInfo& q) {
     d[pos] = q;
 }
 
-K10S_HD bool pod_in_s(const Ctx& c, uint32_t p) { return (c.V().pod(p).flags & PF_IN_S) != 0; }
+K10S_HD bool pod_in_s(const Ctx& c, uint32_t p) { return c.V().pod(p).sflag != 0; }
 
 // move_pods_to_active_queue over a selection, in key order (scheduler.rs:174-185)
 // mode 0: all (move_all_to_active_queue, 235-244); 1: flush (188-203, stay > 300 s);
@@ -1823,7 +1830,7 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
     }
     case K10S_EV_S_POD_SCHEDULE_REQ: {
         uint32_t p = e.a;
-        c.V().pod(p).flags |= PF_IN_S;
+        c.V().pod(p).sflag = PF_IN_S;   // a store: no read of the pod line on this event
         c.V().pod(p).s_assigned = -1;
         QInfo q;
         q.timestamp = e.time;
@@ -1838,7 +1845,7 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
         // one batch of loads: the pod's fields, the event node's flags, and the scheduler-cache entry
         // of the event node (the pod's assigned node in every run so far; re-read if it is not)
         PodState& P = c.V().pod(p);
-        const uint8_t pf = P.flags;
+        const uint8_t pf = P.sflag;
         const int32_t sa = P.s_assigned;
         const uint32_t rc = P.req_cpu;
         const uint64_t rr = P.req_ram;
@@ -1849,7 +1856,7 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
             fail(c, K10S_PANIC_MISSING_POD);
             return;
         }
-        P.flags = (uint8_t)(pf & ~PF_IN_S);
+        P.sflag = 0;
         if (!(nf & NF_S_ASSIGN)) {
             fail(c, K10S_PANIC_MISSING_ASSIGNMENTS);
             return;
@@ -1898,7 +1905,7 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
     case K10S_EV_S_REMOVE_POD: {
         uint32_t p = e.a;
         if (!pod_in_s(c, p)) return;
-        c.V().pod(p).flags &= (uint8_t)~PF_IN_S;
+        c.V().pod(p).sflag = 0;
         int32_t n = c.V().pod(p).s_assigned;
         if (n >= 0) {
             s_release(c, p);

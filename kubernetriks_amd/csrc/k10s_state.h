@@ -294,8 +294,10 @@ enum : uint8_t { PF_IN_S = 1, PF_IN_PS = 2, PF_UNSCHED = 4 };
 // Per-pod state: every field an event handler touches for one pod, in one 64-B line.
 struct PodState {
     uint32_t req_cpu;       // requests (seed-perturbed per replica)
-    uint8_t flags;          // PF_*: in scheduler cache / in storage / in PS unscheduled cache
-    uint8_t pad0[3];
+    uint8_t flags;          // PF_IN_PS / PF_UNSCHED: in storage / in the PS unscheduled cache
+    uint8_t sflag;          // PF_IN_S: in the scheduler's cache (its own byte, so that
+                            // S_POD_SCHEDULE_REQ sets it with a store, no read of the line)
+    uint8_t pad0[2];
     uint64_t req_ram;
     double dur;
     int32_t s_assigned;     // scheduler cache pod.status.assigned_node (node idx or -1)

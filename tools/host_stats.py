@@ -50,7 +50,7 @@ def main():
     print(json.dumps({"workload": wl_name, "nodes": nodes, "pods": pods, "counts": v,
                       "per_event": {n: round(v[n] / ev, 4) for n in NAMES if n != "events"},
                       "refills_per_fifo_pop": round(v["refill"] / max(v["fifo_pop"], 1), 4),
-                      "rings": per_ring}, indent=1))
+                      "rings": per_ring, "aq_pops": int(st[29]), "aq_hbm_reads": int(st[28])}, indent=1))
 
 
 if __name__ == "__main__":
