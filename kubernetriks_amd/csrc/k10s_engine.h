@@ -3270,6 +3270,10 @@ K10S_HD void fq_refill(Ctx& c, int cls, uint32_t hd) {
     H.fq[cls].wend = hd + n;
 }
 
+// (Round 3 measured an asynchronous window refill — an LDS-DMA copy of the next ring entries into
+// freed window slots, waited for when the head reaches them — and did not keep it: C3 1,242 ->
+// 1,272 ms, the vmcnt(0) wait at the first copied entry also waits for the previous handler's
+// stores; profiles/r03_k5_fq_prefetch_ab.json.)
 // Remove the head event of source src (sl[0]) and move the source's entry in the source list to
 // its new head; a FIFO takes its next head from its window.  K10S_SL_FAST (default 1): when the new
 // head still precedes sl[1], only sl[0]'s key is rewritten (tuning knob, semantics-neutral).
