@@ -549,6 +549,9 @@ K10S_HD uint32_t heap_min_child(Ctx& c, uint32_t first, uint32_t n, int64_t& kmi
 #endif
 }
 
+// (Round 3 measured a heap_pop that takes the moved-up HBM entry from the lane that loaded it and
+// waits for the last entry only after the first level: C3 1,240 -> 1,259 ms, not kept;
+// profiles/r03_k6_heap_pop_ab.json.)
 K10S_HELPER void heap_pop(Ctx& c) {
     uint32_t n = uniform_u32(c.H().heap_size) - 1;
     c.H().heap_size = n;
