@@ -196,8 +196,11 @@ typedef struct k10s_capacities {
                                             K10S_NODE_CACHE_AUTO (0) = packed, one u64 per node (cpu in
                                             bits 40-63, ram in bits 0-39: 8 B per node and scan), when
                                             every node definition has cpu < 2^24 and ram < 2^40, no
-                                            replica uses a score plugin beyond LeastAllocated and
-                                            pruned_scan is off; otherwise wide.  K10S_NODE_CACHE_WIDE (1)
+                                            replica uses a score plugin beyond LeastAllocated,
+                                            pruned_scan is off and no event time carries a sign bit
+                                            (trace timestamps, durations, delays, tick intervals: the
+                                            packed kernel keys times by their bit pattern); otherwise
+                                            wide.  K10S_NODE_CACHE_WIDE (1)
                                             = always the u32 cpu + u64 ram SoA (12 B per node).  Results
                                             are identical either way. */
 } k10s_capacities;
