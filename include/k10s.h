@@ -86,6 +86,8 @@ extern "C" {
 #define K10S_ERR_NODE_CACHE_RANGE 105      /* engine capacity: a packed node-cache entry would exceed its
                                               field (allocatable cpu >= 2^24 or ram >= 2^40 after a
                                               release; cannot happen while allocatable <= capacity) */
+#define K10S_ERR_INVARIANT 106             /* host check build only: an invariant a device shortcut relies
+                                              on was violated (never expected) */
 
 /* ---- counters (printer.rs:90-101 + engine throughput counters) ---------------------------- */
 enum k10s_counter {

@@ -257,7 +257,11 @@ struct RepHdr {
                                   // (persistent_storage.rs:137-145)
     uint32_t stale_fin;           // canceled pod-finish events still in the heap (lazy cancel): while 0,
                                   // a popped N_POD_FINISHED is live without reading its pod's line
-    uint32_t pad_h;
+    uint32_t pend_rm_n;           // bits set in the api server's removal set (pend_rm): while 0, an
+                                  // assignment request needs no read of it
+    uint32_t ps_rm_n;             // pods storage dropped on a removal request (PS_REMOVE_POD_REQ): while
+                                  // 0, every PodStartedRunning finds its pod in storage (below)
+    uint32_t pad_h2;
     HeapEv fq_win[K10S_NFQ * K10S_FQW];
     HeapEv heap_lds[K10S_HEAP_TOP];
 #if K10S_AQ_TOP
