@@ -751,10 +751,11 @@ K10S_HD void s_move_after_free(Ctx& c, uint32_t cpu, uint64_t ram) {
 // component; only cancel_all_running_pods (95-112, node removal) iterates it, and nothing it does per
 // pod depends on the order, so it is a lane-parallel sweep over run_slot (N_REMOVE_NODE) and a bind
 // or finish touches only the pod's own line and the component's count.
-// Remove running pod p (run_slot == slot, finish_seq == fs already loaded by the caller).
-K10S_HD void run_remove_at(Ctx& c, uint32_t p, int32_t slot, uint32_t fs) {
+// Remove running pod p (run_slot == slot, finish_seq == fs, the component's count srun and the
+// pod's group g already loaded by the caller).
+K10S_HD void run_remove_at(Ctx& c, uint32_t p, int32_t slot, uint32_t fs, int32_t srun, int32_t g) {
     PodState& P = c.V().pod(p);
-    c.V().slot(slot).running -= 1;
+    c.V().slot(slot).running = srun - 1;
     if (c.Ly().cap_gauge) {  // free_pod_requests (node_component.rs:88-91)
         c.V().g_cpu()[slot] += P.req_cpu;
         c.V().g_ram()[slot] += P.req_ram;
@@ -764,12 +765,12 @@ K10S_HD void run_remove_at(Ctx& c, uint32_t p, int32_t slot, uint32_t fs) {
     // canceled event stays in the heap until popped (counted in stale_fin)
     if (fs != 0 && !(c.H().cur_kind == K10S_EV_N_POD_FINISHED && c.H().cur_seq == fs)) c.H().stale_fin += 1;
     P.finish_seq = 0;
-    int32_t g = c.S().pod_group[p];
     if (g >= 0) c.V().grp()[g].running -= 1;
 }
 K10S_HD void run_remove(Ctx& c, uint32_t p) {
     const PodState& P = c.V().pod(p);
-    run_remove_at(c, p, P.run_slot, P.finish_seq);
+    const int32_t slot = P.run_slot;
+    run_remove_at(c, p, slot, P.finish_seq, c.V().slot(slot).running, c.S().pod_group[p]);
 }
 
 // ---- schedule_one: Fit filter + LeastAllocated score + argmax (the hot scan) -------------------
@@ -2689,13 +2690,17 @@ K10S_WARM void on_node(Ctx& c, K10S_EVARG) {
     }
     case K10S_EV_N_POD_FINISHED: {
         uint32_t p = e.a;
-        const int32_t rs = c.V().pod(p).run_slot;   // one batch of loads from the pod line
+        // one batch of loads: the pod line, the component's count (the event names the component)
+        // and the pod's group (scenario)
+        const int32_t rs = c.V().pod(p).run_slot;
         const uint32_t fs = c.V().pod(p).finish_seq;
+        const int32_t srun = c.V().slot(slot).running;
+        const int32_t g = c.S().pod_group[p];
         if (rs != slot) {
             fail(c, K10S_PANIC_MISSING_POD);
             return;
         }
-        run_remove_at(c, p, slot, fs);
+        run_remove_at(c, p, slot, fs, srun, g);
         emit(c, K10S_EV_AS_POD_FINISHED, 0.0, -1, p, e.b, e.x, FQ_NOW);  // emit_now
         break;
     }
