@@ -413,13 +413,13 @@ K10S_HD void heap_put(Ctx& c, uint32_t i, const HeapEv& e) {
 // Host-only event statistics (tooling: tools/host_stats.py builds the host engine with
 // -DK10S_HOST_STATS and reads k10s_host_stats); compiled out everywhere else.
 #if !K10S_DEVICE && defined(K10S_HOST_STATS)
-extern "C" uint64_t k10s_host_stats[32];
+extern "C" uint64_t k10s_host_stats[48];
 #define K10S_HSTAT(i) (k10s_host_stats[i] += 1)
 #else
 #define K10S_HSTAT(i) ((void)0)
 #endif
 enum { HS_EVENTS, HS_FIFO_POP, HS_REFILL, HS_HEAP_POP, HS_TRACE_POP, HS_SL_FAST, HS_SL_UPDATE, HS_EMIT_WIN,
-       HS_EMIT_RING, HS_EMIT_HEAP, HS_SL_DIRTY, HS_SCANS, HS_REFILL_CLS0 = 12, HS_POP_CLS0 = 20, HS_AQ_HBM_GET = 28, HS_AQ_POP = 29 };
+       HS_EMIT_RING, HS_EMIT_HEAP, HS_SL_DIRTY, HS_SCANS, HS_REFILL_CLS0 = 12, HS_POP_CLS0 = 20, HS_AQ_HBM_GET = 28, HS_AQ_POP = 29, HS_SLPOS0 = 32 };
 // An emission changed source q's head: mark it for the source list.
 K10S_HD void sl_mark(RepHdr& H, uint32_t q) { H.sl_dirty |= 1u << q; }
 
@@ -3261,6 +3261,7 @@ K10S_HD void sl_update(Ctx& c, uint32_t q, bool has, int64_t key, uint32_t seq) 
             H.sl[i] = H.sl[i - 1];
             i--;
         }
+        K10S_HSTAT(HS_SLPOS0 + (i < 3 ? i : 3));
         H.sl[i].key = key;
         H.sl[i].seq = seq;
         H.sl[i].src = q;

@@ -26,7 +26,7 @@ def main():
     defs = os.path.join(REPO, "build", "hoststats_defs.cpp")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     with open(defs, "w") as f:
-        f.write('#include <cstdint>\nextern "C" uint64_t k10s_host_stats[32];\nuint64_t k10s_host_stats[32];\n')
+        f.write('#include <cstdint>\nextern "C" uint64_t k10s_host_stats[48];\nuint64_t k10s_host_stats[48];\n')
     hc = os.path.join(REPO, "tests", "hostcheck")
     subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-ffp-contract=off", "-DK10S_HOST_STATS", "-shared",
                            "-o", out, os.path.join(hc, "hostcheck.cpp"),
@@ -42,7 +42,7 @@ def main():
         cluster, workload = wl.c3_traces(n_nodes=nodes, n_pods=pods, arrival_window=1200.0, seed=123)
     eng = hb.HostEngine(scenario_text(SimulationConfig(), cluster, workload), 1)
     eng.run_until_all_finished(max_time=1e7)
-    st = (ctypes.c_uint64 * 32).in_dll(hb.lib(), "k10s_host_stats")
+    st = (ctypes.c_uint64 * 48).in_dll(hb.lib(), "k10s_host_stats")
     v = {n: int(st[i]) for i, n in enumerate(NAMES)}
     ev = max(v["events"], 1)
     rings = ["as_to_ps", "ps_to_sched", "sched_to_as", "assign", "as_to_node", "as_to_ca", "as_to_hpa", "now"]
@@ -50,7 +50,8 @@ def main():
     print(json.dumps({"workload": wl_name, "nodes": nodes, "pods": pods, "counts": v,
                       "per_event": {n: round(v[n] / ev, 4) for n in NAMES if n != "events"},
                       "refills_per_fifo_pop": round(v["refill"] / max(v["fifo_pop"], 1), 4),
-                      "rings": per_ring, "aq_pops": int(st[29]), "aq_hbm_reads": int(st[28])}, indent=1))
+                      "rings": per_ring, "aq_pops": int(st[29]), "aq_hbm_reads": int(st[28]),
+                      "sl_insert_pos_0_1_2_3plus": [int(st[32 + i]) for i in range(4)]}, indent=1))
 
 
 if __name__ == "__main__":
