@@ -420,6 +420,23 @@ extern "C" uint64_t k10s_host_stats[48];
 #endif
 enum { HS_EVENTS, HS_FIFO_POP, HS_REFILL, HS_HEAP_POP, HS_TRACE_POP, HS_SL_FAST, HS_SL_UPDATE, HS_EMIT_WIN,
        HS_EMIT_RING, HS_EMIT_HEAP, HS_SL_DIRTY, HS_SCANS, HS_REFILL_CLS0 = 12, HS_POP_CLS0 = 20, HS_AQ_HBM_GET = 28, HS_AQ_POP = 29, HS_SLPOS0 = 32 };
+// Out-of-line helpers (device; tuning knobs, semantics-neutral): a helper called from the event loop
+// or the scheduling cycle gets its own register allocation instead of widening the caller's live
+// set (round 3: heap_pop out of line, +1.3 % at C3, profiles/r03_k11_heap_pop_call_ab.json).
+#if K10S_DEVICE
+#define K10S_CALL_IF(knob) __host__ __device__ __attribute__((noinline))
+#else
+#define K10S_CALL_IF(knob) inline
+#endif
+#ifndef K10S_FQREFILL_CALL
+#define K10S_FQREFILL_CALL 0
+#endif
+#ifndef K10S_SLUPD_CALL
+#define K10S_SLUPD_CALL 0
+#endif
+#ifndef K10S_AQPOP_CALL
+#define K10S_AQPOP_CALL 0
+#endif
 // An emission changed source q's head: mark it for the source list.
 K10S_HD void sl_mark(RepHdr& H, uint32_t q) { H.sl_dirty |= 1u << q; }
 
@@ -549,30 +566,111 @@ K10S_HD uint32_t heap_min_child(Ctx& c, uint32_t first, uint32_t n, int64_t& kmi
 #endif
 }
 
-// (Round 3 measured a heap_pop that takes the moved-up HBM entry from the lane that loaded it and
-// waits for the last entry only after the first level: C3 1,240 -> 1,259 ms, not kept;
-// profiles/r03_k6_heap_pop_ab.json.)
+#if K10S_DEVICE
+// K10S_HEAP_POP2: heap_pop with (a) the moved-up entry of a level in HBM taken from the lane that
+// loaded it (heap_min_child_ev loads the whole 32-B entries, so the chosen child needs no second
+// load), and (b) the last entry's load awaited only after the first level's minimum (LDS) is known.
+// Same comparisons and moves.  Inlined into the event loop it lost 1.5 % to register pressure
+// (profiles/r03_k6_heap_pop_ab.json); K10S_HEAP_POP_CALL keeps the whole pop out of line.
+#ifndef K10S_HEAP_POP2
+#define K10S_HEAP_POP2 1
+#endif
+#ifndef K10S_HEAP_POP_CALL
+#define K10S_HEAP_POP_CALL 1
+#endif
+K10S_D uint32_t heap_min_child_ev(Ctx& c, uint32_t first, uint32_t n, int64_t& kmin, uint32_t& smin, HeapEv& ev) {
+    if (first < K10S_HEAP_TOP) {
+        const uint32_t m = heap_min_child(c, first, n, kmin, smin);
+        ev = heap_get(c, m);
+        uniform_event(ev);
+        return m;
+    }
+    const int lane = lane_id();
+    uint32_t i = first + (uint32_t)(lane & (K10S_HEAP_D - 1));
+    int64_t k = 0x7FFFFFFFFFFFFFFFll;
+    uint32_t sq = 0xFFFFFFFFu;
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    v4u lo = {0u, 0u, 0u, 0u}, hi = {0u, 0u, 0u, 0u};
+    if (lane < K10S_HEAP_D && i < n) {
+        const __amdgpu_buffer_rsrc_t rs = heap_rsrc(c);
+        lo = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * (uint32_t)sizeof(HeapEv)), 0, 0);
+        hi = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * (uint32_t)sizeof(HeapEv)) + 16, 0, 0);
+        k = total_key(u2f(((uint64_t)lo[1] << 32) | lo[0]));
+        sq = lo[2];
+    }
+    keymin_step<0>(k, sq, i);
+    keymin_step<1>(k, sq, i);
+    keymin_step<2>(k, sq, i);
+    if constexpr (K10S_HEAP_D >= 16) keymin_step<3>(k, sq, i);
+    if constexpr (K10S_HEAP_D >= 32) keymin_step<4>(k, sq, i);
+    if constexpr (K10S_HEAP_D >= 64) keymin_step<5>(k, sq, i);
+    const uint64_t klo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)k);
+    const uint64_t khi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)k >> 32));
+    kmin = (int64_t)(klo | (khi << 32));
+    smin = (uint32_t)__builtin_amdgcn_readfirstlane((int)sq);
+    const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
+    const int src = (int)(m - first);   // the lane that loaded entry m
+    auto rl = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, src); };
+    ev.time = u2f(((uint64_t)rl(lo[1]) << 32) | rl(lo[0]));
+    ev.seq = rl(lo[2]);
+    const uint32_t ks = rl(lo[3]);
+    ev.kind = (uint16_t)ks;
+    ev.slot = (int16_t)(ks >> 16);
+    ev.a = rl(hi[0]);
+    ev.b = rl(hi[1]);
+    ev.x = u2f(((uint64_t)rl(hi[3]) << 32) | rl(hi[2]));
+    return m;
+}
+#define K10S_HEAP_POP_ATTR __attribute__((noinline))
+#else
+#define K10S_HEAP_POP2 0
+#define K10S_HEAP_POP_CALL 0
+#define K10S_HEAP_POP_ATTR
+#endif
+#if K10S_HEAP_POP_CALL
+K10S_HD K10S_HEAP_POP_ATTR void heap_pop(Ctx& c) {
+#else
 K10S_HELPER void heap_pop(Ctx& c) {
+#endif
     uint32_t n = uniform_u32(c.H().heap_size) - 1;
     c.H().heap_size = n;
     if (n == 0) return;
     HeapEv last = heap_get(c, n);
+#if K10S_HEAP_POP2
+    bool have_last = false;
+    int64_t kl = 0;
+#else
     uniform_event(last);
     int64_t kl = total_key(last.time);
+#endif
     uint32_t pos = 0;
     for (;;) {
         uint32_t first = K10S_HEAP_D * pos + 1;
         if (first >= n) break;
         int64_t km;
         uint32_t sm;
+#if K10S_HEAP_POP2
+        HeapEv child;
+        uint32_t m = heap_min_child_ev(c, first, n, km, sm, child);
+        if (!have_last) {
+            uniform_event(last);
+            kl = total_key(last.time);
+            have_last = true;
+        }
+        if (!(km < kl || (km == kl && sm < last.seq))) break;
+#else
         uint32_t m = heap_min_child(c, first, n, km, sm);
         if (!(km < kl || (km == kl && sm < last.seq))) break;
         HeapEv child = heap_get(c, m);
         uniform_event(child);
+#endif
         heap_put(c, pos, child);
         if (pos == 0) c.H().heap_top = child;
         pos = m;
     }
+#if K10S_HEAP_POP2
+    if (!have_last) uniform_event(last);
+#endif
     heap_put(c, pos, last);
     if (pos == 0) c.H().heap_top = last;
 }
@@ -633,7 +731,11 @@ K10S_HELPER void aq_push(Ctx& c, const QInfo& q) {
 // (Round 3 tried reading the 3-level subtree under the walk's position in one round trip below the
 // LDS levels: C3 +0.6 %, backlog -2 to -4 % from the extra SGPRs live in the scheduling cycle,
 // profiles/r03_k4_sflag_subtree_ab.json; not kept.)
+#if K10S_AQPOP_CALL
+K10S_CALL_IF(K10S_AQPOP_CALL) QInfo aq_pop(Ctx& c) {
+#else
 K10S_HELPER QInfo aq_pop(Ctx& c) {
+#endif
     K10S_HSTAT(HS_AQ_POP);
     const uint32_t end = --c.H().aq_size;
     QInfo item = aq_get(c, end);
@@ -3224,7 +3326,11 @@ K10S_HD bool src_head(Ctx& c, uint32_t q, uint32_t ntr, int64_t& k, uint32_t& s)
 // Replace source q's entry by its new head (key, seq), or drop it (has == false).  Device: one
 // 16-B LDS read per lane (lane i = entry i), the new positions from two ballots, one scattered
 // 16-B write per kept entry and one for the new entry: no serial walk.
+#if K10S_SLUPD_CALL
+K10S_CALL_IF(K10S_SLUPD_CALL) void sl_update(Ctx& c, uint32_t q, bool has, int64_t key, uint32_t seq) {
+#else
 K10S_HD void sl_update(Ctx& c, uint32_t q, bool has, int64_t key, uint32_t seq) {
+#endif
     RepHdr& H = c.H();
 #if K10S_DEVICE
     const uint32_t n = uniform_u32(H.sl_n);
@@ -3297,7 +3403,11 @@ K10S_HD void sl_rebuild(Ctx& c, uint32_t ntr) {
 
 // Refill a drained delay-class window from the HBM ring: positions [hd, hd + min(W, tail - hd)),
 // one 32-B entry per lane, so a burst of FIFO events costs one memory round trip per K10S_FQW pops.
+#if K10S_FQREFILL_CALL
+K10S_CALL_IF(K10S_FQREFILL_CALL) void fq_refill(Ctx& c, int cls, uint32_t hd) {
+#else
 K10S_HD void fq_refill(Ctx& c, int cls, uint32_t hd) {
+#endif
     RepHdr& H = c.H();
     const uint32_t cap = c.Ly().cap_fq;
     const uint32_t avail = H.fq[cls].tail - hd;
