@@ -61,7 +61,7 @@ def test_hpa_checkpoints(backend):
         assert eng.group_sizes(0)["pod_group_1"][0] == size, t
 
 
-FUZZ_SEEDS_HOST = list(range(0, 120))
+FUZZ_SEEDS_HOST = list(range(0, 240))
 # K10S_FUZZ_GPU_SEEDS=N widens the GPU sweep to seeds 0..N-1 (an extended run, e.g. after kernel
 # changes; the default keeps the round-end suite short)
 FUZZ_SEEDS_GPU = list(range(0, int(os.environ.get("K10S_FUZZ_GPU_SEEDS", "60"))))
