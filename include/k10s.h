@@ -78,6 +78,9 @@ extern "C" {
 #define K10S_PANIC_MISSING_PENDING 12      /* api_server.rs:98-101 */
 #define K10S_PANIC_REMOVE_OTHER_NODE 13    /* node_component.rs:248-254 */
 #define K10S_PANIC_UNKNOWN_PROFILE 14      /* kube_scheduler.rs:95 */
+#define K10S_PANIC_NEGATIVE_DELAY 15       /* dslab-core add_event: an event emitted with a negative (or NaN)
+                                              delay, i.e. into the past (a negative pod duration, network
+                                              delay or tick interval reaching an emission) */
 #define K10S_ERR_HEAP_FULL 100             /* engine capacity: event heap */
 #define K10S_ERR_QUEUE_FULL 101            /* engine capacity: scheduler queues */
 #define K10S_ERR_NAME_BOUND 102            /* engine capacity: generated-name universe bound */
@@ -88,6 +91,9 @@ extern "C" {
                                               release; cannot happen while allocatable <= capacity) */
 #define K10S_ERR_INVARIANT 106             /* host check build only: an invariant a device shortcut relies
                                               on was violated (never expected) */
+#define K10S_ERR_EXEC_GUARD 107            /* K10S_EXEC_CHECK tooling builds only: a lane-parallel helper
+                                              was entered without the whole wave live, or a bounded
+                                              loop exceeded its bound; error_kind = site id */
 
 /* ---- counters (printer.rs:90-101 + engine throughput counters) ---------------------------- */
 enum k10s_counter {
@@ -185,7 +191,10 @@ typedef struct k10s_capacities {
     uint32_t event_log, placement_log;   /* parity mode logs; 0 = off */
     uint32_t pod_records;                /* 1 = keep per-pod start/finish/removal times */
     uint32_t delay_fifo;                 /* entries per delay-class event ring: 0 = default (the node
-                                            count rounded up to a power of two, within [512, 8192]),
+                                            count rounded up to a power of two, within [512, 8192]:
+                                            8 rings x 32 B x that many entries per replica, up to 2 MiB;
+                                            when the replicas' state would not fit the free device
+                                            memory, the default falls back to 512 entries),
                                             K10S_FIFO_OFF = every event in the heap */
     uint32_t pruned_scan;                /* 0 = every attempt scans every node (default);
                                             1 = exact block-bound pruned scan where it applies

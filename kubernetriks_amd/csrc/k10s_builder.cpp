@@ -609,6 +609,13 @@ bool build_scenario(const std::string& text, uint32_t group_bound_in, uint32_t c
             if (t.kind == K10S_EV_AS_CREATE_POD_REQ) hs.total_pods_in_trace++;
             wt.push_back(e);
         }
+        // initialize emits every trace event at delay = its timestamp (simulator.rs:234-253): dslab-core
+        // refuses a negative (or NaN) delay with a panic, so such a trace never starts a simulation
+        for (const std::vector<TraceEv>* v : {&ct, &wt})
+            for (const TraceEv& t : *v)
+                if (!(t.time >= 0.0))
+                    throw std::runtime_error("trace event at a negative (or NaN) timestamp: the reference panics in "
+                                             "initialize (dslab-core refuses an event delay < 0)");
         hs.trace.resize(ct.size() + wt.size());
         std::merge(ct.begin(), ct.end(), wt.begin(), wt.end(), hs.trace.begin(), [](const TraceEv& a, const TraceEv& b) {
             int64_t ka = total_key(a.time), kb = total_key(b.time);
@@ -748,8 +755,8 @@ bool nodes_packable(const HostScenario& hs) {
     return true;
 }
 
-// A value with the sign bit set other than -0.0 (negative numbers, -inf, negative NaNs).
-static bool signed_time(double x) { return std::signbit(x) && x != 0.0; }
+// A delay dslab-core refuses (`delay >= 0.` false: negative numbers, -inf, NaNs); -0.0 is allowed.
+static bool signed_time(double x) { return !(x >= 0.0); }
 
 bool times_nonneg(const HostScenario& hs, const Params* params, uint32_t n_params) {
     for (const TraceEv& t : hs.trace)
@@ -768,9 +775,10 @@ bool times_nonneg(const HostScenario& hs, const Params* params, uint32_t n_param
     return true;
 }
 
-Layout make_layout(const HostScenario& hs, const k10s_capacities& caps, bool allow_packed) {
+Layout make_layout(const HostScenario& hs, const k10s_capacities& caps, bool allow_packed, bool tnonneg) {
     Layout L;
     std::memset(&L, 0, sizeof L);
+    L.tnonneg = tnonneg ? 1u : 0u;
     L.packed = (allow_packed && caps.node_cache == K10S_NODE_CACHE_AUTO && !caps.pruned_scan && nodes_packable(hs)) ? 1u : 0u;
     const uint64_t N = hs.n_nodes, P = hs.n_pods, S = hs.n_slots, G = hs.group_names.size(),
                    CG = hs.ca_group_names.size();

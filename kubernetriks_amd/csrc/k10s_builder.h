@@ -73,7 +73,7 @@ Scenario rebase_scenario(const Scenario& view_offsets, const uint8_t* base);
 // allow_packed: false when some replica needs the wide node cache (a score plugin beyond
 // LeastAllocated: the plugin kernel reads capacities from the wide SoA) or the general event-time
 // key (!times_nonneg): the packed layout runs in the default kernel, which keys times by their bits.
-Layout make_layout(const HostScenario& hs, const k10s_capacities& caps, bool allow_packed);
+Layout make_layout(const HostScenario& hs, const k10s_capacities& caps, bool allow_packed, bool tnonneg);
 // Every event time of the scenario under these replica parameters carries no sign bit (trace
 // timestamps, pod and usage-unit durations, network delays, tick intervals; -0.0 allowed), so the
 // default kernel's bit-pattern time key orders them like total_cmp (k10s_common.h total_key).

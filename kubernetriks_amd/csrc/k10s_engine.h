@@ -37,34 +37,100 @@ enum : int { SEC_BASE = 0, SEC_POD, SEC_NODE, SEC_SLOT, SEC_FQ, SEC_HEAP, SEC_SN
 __constant__ DevConst k10s_dc;
 __shared__ RepHdr k10s_hdr;
 __shared__ uint64_t k10s_sec[K10S_NSEC];
-// The launch's run arguments, staged in LDS by the run kernel (K10S_RUN_ARGS_LDS): read where the
-// loop tests them instead of held in SGPRs across the loop, where they are spilled around every
-// out-of-line handler call.
-struct RunArgs {
-    double limit;       // until_time (K10S_RUN_UNTIL_TIME) or max_time
-    uint64_t budget;    // events per launch, 0 = unbounded
-    uint32_t until_mode;
-    uint32_t pad;
-};
-__shared__ RunArgs k10s_run;
 #endif
-#ifndef K10S_RUN_ARGS_LDS
-#define K10S_RUN_ARGS_LDS 0   // 1: 8.6 % slower at C3 (LDS reads on every event's path), r02_v16
+
+// ---- progress beacon (K10S_BEACON tooling builds) --------------------------------------------------
+// Lane 0 of every replica writes the event it is about to handle (and the queue state) to host-mapped
+// memory with system-scope stores before each dispatch, so a host thread can see where a launch that
+// never returns stopped (tools/beacon_trace.py).  Product builds compile it out.
+#ifndef K10S_BEACON
+#define K10S_BEACON 0
+#endif
+#define K10S_BEACON_WORDS 16
+#if defined(__HIP__) && K10S_BEACON
+__device__ uint32_t* k10s_beacon;   // [replica][K10S_BEACON_WORDS], host-mapped (k10s_debug_beacon_alloc)
+#endif
+
+// ---- EXEC guard (K10S_EXEC_CHECK tooling builds) --------------------------------------------------
+// Every lane-parallel helper (DPP/permlane reductions, ballots, readlane of a computed lane) assumes
+// the whole wave is live: under a partial EXEC a DPP step reads the disabled partners' `old` value
+// (0), so a reduction returns garbage, and a helper entered with an empty EXEC runs only its scalar
+// control flow over stale vector values.  Check builds test EXEC at each such helper's entry (and
+// bound the queue/heap sift loops: K10S_EXEC_CHECK bit 1); a violation stops the replica with K10S_ERR_EXEC_GUARD, site id
+// in error_kind (| 0x100 when EXEC was empty).  The record is written with the whole wave switched on,
+// because a vector store under an empty EXEC writes nothing.  Product builds compile it out.
+#ifndef K10S_EXEC_CHECK
+#define K10S_EXEC_CHECK 0
+#endif
+enum : uint32_t {
+    XG_HEAP_POP = 1, XG_HEAP_MIN_CHILD, XG_HEAP_MIN_CHILD_EV, XG_SCHEDULE_SCAN, XG_SL_UPDATE, XG_FQ_REFILL,
+    XG_PODS_IN_ORDER, XG_FOR_EACH_BIT, XG_CA_FIRST_FIT, XG_CA_SORT, XG_DISPATCH, XG_CYCLE, XG_GAUGE, XG_CACHE_FITS,
+    XG_FAIR, XG_HANDLER, XG_EMIT, XG_SCAN_PLUGINS,
+    XG_LOOP_HEAP_POP = 0x40, XG_LOOP_EMIT, XG_LOOP_AQ_POP, XG_LOOP_AQ_UP, XG_LOOP_STALE,
+};
+#if K10S_DEVICE && K10S_EXEC_CHECK
+K10S_D bool exec_guard_fail(uint32_t site) {
+#if defined(K10S_PLUGINS_TU)
+    // (the plugins copy records with plain stores: the flat-address form below trips an instruction
+    // selection error in that translation unit; an empty EXEC goes unrecorded there)
+    k10s_hdr.error_code = K10S_ERR_EXEC_GUARD;
+    k10s_hdr.error_kind = site;
+    return false;
+#else
+    // generic (flat) addresses of the two header words: an LDS-aperture address works for flat stores
+    const uint64_t a_code = (uint64_t)(uintptr_t)&k10s_hdr.error_code;
+    const uint64_t a_kind = (uint64_t)(uintptr_t)&k10s_hdr.error_kind;
+    const uint32_t code = K10S_ERR_EXEC_GUARD;
+    uint64_t saved, va;
+    uint32_t vd;
+    asm volatile(
+        "s_or_saveexec_b64 %0, -1\n\t"
+        "v_mov_b32 %1, %3\n\t"
+        "v_mov_b64 %2, %4\n\t"
+        "flat_store_dword %2, %1\n\t"
+        "v_mov_b32 %1, %5\n\t"
+        "s_waitcnt vmcnt(0) lgkmcnt(0)\n\t"
+        "v_mov_b64 %2, %6\n\t"
+        "flat_store_dword %2, %1\n\t"
+        "s_waitcnt vmcnt(0) lgkmcnt(0)\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(saved), "=&v"(vd), "=&v"(va)
+        : "s"(code), "s"(a_code), "s"(site), "s"(a_kind)
+        : "memory");
+    return false;
+#endif
+}
+// true when the whole wave is live; otherwise records the site and returns false (the caller returns)
+K10S_D bool exec_guard(uint32_t site) {
+    const uint64_t ex = __builtin_amdgcn_read_exec();
+    if (__builtin_expect(ex == ~0ull, 1)) return true;
+    return exec_guard_fail(site | (ex == 0 ? 0x100u : 0u));
+}
+// K10S_EXEC_CHECK bit 0: the entry guards; bit 1: the loop bounds (each alone perturbs codegen less)
+#if K10S_EXEC_CHECK & 1
+#define K10S_FULL_WAVE(site) exec_guard(site)
+#else
+#define K10S_FULL_WAVE(site) true
+#endif
+#if K10S_EXEC_CHECK & 2
+// a bounded loop took more than `cap` iterations (it = the loop's counter)
+#define K10S_LOOP_CAP(it, cap, site) (++(it) > (cap) ? exec_guard_fail(site), true : false)
+#else
+#define K10S_LOOP_CAP(it, cap, site) false
+#endif
+#else
+#define K10S_FULL_WAVE(site) true
+#define K10S_LOOP_CAP(it, cap, site) false
 #endif
 // Every read of the launch constants goes through an opaque copy of the block's address (an empty
 // asm the compiler cannot see through): the scalar loads are then issued where a value is used
 // instead of being hoisted out of the event loop and kept live across it, which is what
 // exhausted the SGPRs (and spilled them into VGPR lanes) and raised the loop's VGPR count.
 #if K10S_DEVICE
-#ifndef K10S_DC_OPAQUE
-#define K10S_DC_OPAQUE 1
-#endif
 typedef const __attribute__((address_space(4))) DevConst* DevConstPtr;
 K10S_D DevConstPtr dc_ptr() {
     DevConstPtr p = (DevConstPtr)&k10s_dc;
-#if K10S_DC_OPAQUE
     asm volatile("" : "+s"(p));
-#endif
     return p;
 }
 #define K10S_DC (*dc_ptr())
@@ -262,14 +328,10 @@ K10S_HD void uniform_event(HeapEv& e) {
 #endif
 }
 
-// How an event reaches its out-of-line handler.  K10S_EV_BYREF=1 (default): as the address of its
-// LDS copy (the head entry of its source, which the loop consumes only after the handler ran; a
-// trace event is first written to the header's cur_ev slot), so a call passes one 32-bit VGPR and
-// the loop reads only the fields it tests.  0: by value in 8 VGPRs (the loop reads all 8 dwords to
-// SGPRs, writes them back into the argument VGPRs, the handler reads them to SGPRs again).
-#ifndef K10S_EV_BYREF
-#define K10S_EV_BYREF 1
-#endif
+// How an event reaches its out-of-line handler: as the address of its LDS copy (the head entry of
+// its source, which the loop consumes only after the handler ran; a trace event is first written to
+// the header's cur_ev slot), so a call passes one 32-bit VGPR and the loop reads only the fields it
+// tests (round 2 passed the event by value in 8 VGPRs, each handler reading them to SGPRs again).
 #if K10S_DEVICE
 typedef const __attribute__((address_space(3))) HeapEv* EvRef;
 #define K10S_EVREF(x) ((EvRef)(x))
@@ -277,15 +339,11 @@ typedef const __attribute__((address_space(3))) HeapEv* EvRef;
 typedef const HeapEv* EvRef;
 #define K10S_EVREF(x) ((EvRef)(x))
 #endif
-#if K10S_EV_BYREF
 #define K10S_EVARG EvRef ep
-#define K10S_EV_PROLOGUE \
-    HeapEv e = *ep;      \
+#define K10S_EV_PROLOGUE                     \
+    if (!K10S_FULL_WAVE(XG_HANDLER)) return; \
+    HeapEv e = *ep;                          \
     uniform_event(e)
-#else
-#define K10S_EVARG HeapEv e
-#define K10S_EV_PROLOGUE uniform_event(e)
-#endif
 
 // ---- cycle attribution (K10S_PROF builds: tooling only, semantics-neutral) ----------------------
 // s_memtime deltas per loop phase, accumulated in RepHdr::prof and read by k10s_engine_profile.
@@ -420,23 +478,6 @@ extern "C" uint64_t k10s_host_stats[48];
 #endif
 enum { HS_EVENTS, HS_FIFO_POP, HS_REFILL, HS_HEAP_POP, HS_TRACE_POP, HS_SL_FAST, HS_SL_UPDATE, HS_EMIT_WIN,
        HS_EMIT_RING, HS_EMIT_HEAP, HS_SL_DIRTY, HS_SCANS, HS_REFILL_CLS0 = 12, HS_POP_CLS0 = 20, HS_AQ_HBM_GET = 28, HS_AQ_POP = 29, HS_SLPOS0 = 32 };
-// Out-of-line helpers (device; tuning knobs, semantics-neutral): a helper called from the event loop
-// or the scheduling cycle gets its own register allocation instead of widening the caller's live
-// set (round 3: heap_pop out of line, +1.3 % at C3, profiles/r03_k11_heap_pop_call_ab.json).
-#if K10S_DEVICE
-#define K10S_CALL_IF(knob) __host__ __device__ __attribute__((noinline))
-#else
-#define K10S_CALL_IF(knob) inline
-#endif
-#ifndef K10S_FQREFILL_CALL
-#define K10S_FQREFILL_CALL 0
-#endif
-#ifndef K10S_SLUPD_CALL
-#define K10S_SLUPD_CALL 0
-#endif
-#ifndef K10S_AQPOP_CALL
-#define K10S_AQPOP_CALL 0
-#endif
 // An emission changed source q's head: mark it for the source list.
 K10S_HD void sl_mark(RepHdr& H, uint32_t q) { H.sl_dirty |= 1u << q; }
 
@@ -462,6 +503,16 @@ K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uin
         fail(c, K10S_ERR_SEQ_OVERFLOW);
         return 0;
     }
+#if !K10S_TIME_KEY_ID
+    // dslab-core add_event refuses an event in the past (a negative or NaN delay) with a panic.  Only
+    // the signed-time copies check: the default kernel copy runs scenarios whose every delay, interval,
+    // duration and trace time is >= 0 (times_nonneg, k10s_builder.cpp), where no emission can be.
+    // (This also keeps the events-by-reference rule: an emission never precedes the event handled.)
+    if (!(delay >= 0.0)) {
+        fail(c, K10S_PANIC_NEGATIVE_DELAY);
+        return 0;
+    }
+#endif
     HeapEv e;
     e.time = clock + delay;
     e.seq = seq;
@@ -496,7 +547,9 @@ K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uin
     K10S_HSTAT(HS_EMIT_HEAP);
     uint32_t pos = uniform_u32(hsize);
     H.heap_size = pos + 1;
+    [[maybe_unused]] uint32_t it = 0;
     while (pos > 0) {
+        if (K10S_LOOP_CAP(it, 12, XG_LOOP_EMIT)) break;
         uint32_t parent = (pos - 1) / K10S_HEAP_D;
         HeapEv p = heap_get(c, parent);
         uniform_event(p);  // wave-uniform by construction: keep the sift loop on the scalar unit
@@ -518,6 +571,11 @@ K10S_HD uint32_t emit0(Ctx& c, uint32_t kind, double delay) { return emit(c, kin
 // 0..D-1 load one child's key each (one contiguous read) and reduce with log2(D) DPP/permlane steps.
 K10S_HD uint32_t heap_min_child(Ctx& c, uint32_t first, uint32_t n, int64_t& kmin, uint32_t& smin) {
 #if K10S_DEVICE
+    if (!K10S_FULL_WAVE(XG_HEAP_MIN_CHILD)) {
+        kmin = 0x7FFFFFFFFFFFFFFFll;
+        smin = 0xFFFFFFFFu;
+        return first;
+    }
     const int lane = lane_id();
     uint32_t i = first + (uint32_t)(lane & (K10S_HEAP_D - 1));
     int64_t k = 0x7FFFFFFFFFFFFFFFll;
@@ -567,18 +625,18 @@ K10S_HD uint32_t heap_min_child(Ctx& c, uint32_t first, uint32_t n, int64_t& kmi
 }
 
 #if K10S_DEVICE
-// K10S_HEAP_POP2: heap_pop with (a) the moved-up entry of a level in HBM taken from the lane that
+// The device's heap_pop: (a) the moved-up entry of a level in HBM taken from the lane that
 // loaded it (heap_min_child_ev loads the whole 32-B entries, so the chosen child needs no second
 // load), and (b) the last entry's load awaited only after the first level's minimum (LDS) is known.
 // Same comparisons and moves.  Inlined into the event loop it lost 1.5 % to register pressure
-// (profiles/r03_k6_heap_pop_ab.json); K10S_HEAP_POP_CALL keeps the whole pop out of line.
-#ifndef K10S_HEAP_POP2
-#define K10S_HEAP_POP2 1
-#endif
-#ifndef K10S_HEAP_POP_CALL
-#define K10S_HEAP_POP_CALL 1
-#endif
+// (profiles/r03_k6_heap_pop_ab.json); the whole pop runs out of line on the device (+1.6 %,
+// profiles/r03_k11_heap_pop_call_ab.json).
 K10S_D uint32_t heap_min_child_ev(Ctx& c, uint32_t first, uint32_t n, int64_t& kmin, uint32_t& smin, HeapEv& ev) {
+    if (!K10S_FULL_WAVE(XG_HEAP_MIN_CHILD_EV)) {
+        kmin = 0x7FFFFFFFFFFFFFFFll;
+        smin = 0xFFFFFFFFu;
+        return first;
+    }
     if (first < K10S_HEAP_TOP) {
         const uint32_t m = heap_min_child(c, first, n, kmin, smin);
         ev = heap_get(c, m);
@@ -623,20 +681,16 @@ K10S_D uint32_t heap_min_child_ev(Ctx& c, uint32_t first, uint32_t n, int64_t& k
 }
 #define K10S_HEAP_POP_ATTR __attribute__((noinline))
 #else
-#define K10S_HEAP_POP2 0
-#define K10S_HEAP_POP_CALL 0
 #define K10S_HEAP_POP_ATTR
 #endif
-#if K10S_HEAP_POP_CALL
 K10S_HD K10S_HEAP_POP_ATTR void heap_pop(Ctx& c) {
-#else
-K10S_HELPER void heap_pop(Ctx& c) {
-#endif
+    if (!K10S_FULL_WAVE(XG_HEAP_POP)) return;
     uint32_t n = uniform_u32(c.H().heap_size) - 1;
     c.H().heap_size = n;
     if (n == 0) return;
     HeapEv last = heap_get(c, n);
-#if K10S_HEAP_POP2
+    [[maybe_unused]] uint32_t it = 0;
+#if K10S_DEVICE
     bool have_last = false;
     int64_t kl = 0;
 #else
@@ -647,9 +701,10 @@ K10S_HELPER void heap_pop(Ctx& c) {
     for (;;) {
         uint32_t first = K10S_HEAP_D * pos + 1;
         if (first >= n) break;
+        if (K10S_LOOP_CAP(it, 12, XG_LOOP_HEAP_POP)) break;
         int64_t km;
         uint32_t sm;
-#if K10S_HEAP_POP2
+#if K10S_DEVICE
         HeapEv child;
         uint32_t m = heap_min_child_ev(c, first, n, km, sm, child);
         if (!have_last) {
@@ -668,7 +723,7 @@ K10S_HELPER void heap_pop(Ctx& c) {
         if (pos == 0) c.H().heap_top = child;
         pos = m;
     }
-#if K10S_HEAP_POP2
+#if K10S_DEVICE
     if (!have_last) uniform_event(last);
 #endif
     heap_put(c, pos, last);
@@ -710,7 +765,9 @@ K10S_HD void aq_put(Ctx& c, uint32_t i, const QInfo& q) {
 }
 
 K10S_HD uint32_t aq_sift_up(Ctx& c, uint32_t start, uint32_t pos, const QInfo& elem) {
+    [[maybe_unused]] uint32_t it = 0;
     while (pos > start) {
+        if (K10S_LOOP_CAP(it, 40, XG_LOOP_AQ_UP)) break;
         uint32_t parent = (pos - 1) / 2;
         QInfo p = aq_get(c, parent);
         if (q_le(elem, p)) break;
@@ -731,11 +788,7 @@ K10S_HELPER void aq_push(Ctx& c, const QInfo& q) {
 // (Round 3 tried reading the 3-level subtree under the walk's position in one round trip below the
 // LDS levels: C3 +0.6 %, backlog -2 to -4 % from the extra SGPRs live in the scheduling cycle,
 // profiles/r03_k4_sflag_subtree_ab.json; not kept.)
-#if K10S_AQPOP_CALL
-K10S_CALL_IF(K10S_AQPOP_CALL) QInfo aq_pop(Ctx& c) {
-#else
 K10S_HELPER QInfo aq_pop(Ctx& c) {
-#endif
     K10S_HSTAT(HS_AQ_POP);
     const uint32_t end = --c.H().aq_size;
     QInfo item = aq_get(c, end);
@@ -744,7 +797,9 @@ K10S_HELPER QInfo aq_pop(Ctx& c) {
     // sift_down_to_bottom(0) with `item` in the hole, then sift_up(0, pos)
     uint32_t pos = 0;
     uint32_t child = 1;
+    [[maybe_unused]] uint32_t it = 0;
     while (end >= 2 && child <= end - 2) {
+        if (K10S_LOOP_CAP(it, 40, XG_LOOP_AQ_POP)) break;
         QInfo a = aq_get(c, child), b = aq_get(c, child + 1);
         if (q_le(a, b)) {
             child += 1;
@@ -899,11 +954,6 @@ K10S_HD double la_score(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr) {
 #ifndef K10S_SCAN_PIPE
 #define K10S_SCAN_PIPE 1
 #endif
-// K10S_SCAN_BF: 1 evaluates every node's score and selects (no exec-mask branches), 0 branches
-// on Fit per node.  Semantics-neutral tuning knob.
-#ifndef K10S_SCAN_BF
-#define K10S_SCAN_BF 0
-#endif
 K10S_HD void scan_node(uint32_t n, uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr, double weight, int32_t& first,
                        uint64_t& best_key, int32_t& best_n) {
     if (rc <= ac && rr <= ar) {
@@ -983,9 +1033,6 @@ K10S_D ScanGrp scan_load_pk_full(const uint64_t* s_node, uint32_t n0) {
     g.r23.y = x23.y & K10S_PK_RAM;
     return g;
 }
-#ifndef K10S_SCAN_FULLBLK
-#define K10S_SCAN_FULLBLK 1
-#endif
 // PK: s_ram is the packed node array (s_cpu unused)
 template <bool PK>
 K10S_D ScanGrp scan_load_x(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
@@ -1038,24 +1085,6 @@ K10S_D double la_score_d(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr) {
 template <bool W1, bool TF>
 K10S_D void scan_node_d(uint32_t n, bool present, uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr, double frc,
                         double frr, double weight, int32_t& first, double& best_s, int32_t& best_n) {
-#if K10S_SCAN_BF
-    // Branch-free: the score is evaluated for every node of the group and kept only if the node
-    // is present and fits (the wave runs all four nodes anyway unless every lane skips one).
-    const bool fit = present && rc <= ac && rr <= ar;
-    const double fac = (double)ac;
-    const double cs = div_rn((fac - frc) * 100.0, fac);  // = (double)(ac - rc): u32 values are exact
-    const uint2 w = __builtin_bit_cast(uint2, ar);
-    const double far = u64_f64(ar);
-    // (ar - rr) as f64: far - frr is exact while ar < 2^53 (then rr <= ar is exact too)
-    double dr = far - frr;
-    if (__builtin_expect(w.y >= (1u << 21), 0)) dr = u64_f64(ar - rr);
-    double s = (cs + div_rn(dr * 100.0, far)) * 0.5;
-    if (!W1) s = 0.0 + s * weight;
-    first = (fit && (int32_t)n < first) ? (int32_t)n : first;
-    const bool take = fit && s >= best_s;
-    best_s = take ? s : best_s;
-    best_n = take ? (int32_t)n : best_n;
-#else
     if (rc <= ac && rr <= ar && present) {
         if (TF) first = (int32_t)n < first ? (int32_t)n : first;
         const double fac = (double)ac;
@@ -1071,7 +1100,6 @@ K10S_D void scan_node_d(uint32_t n, bool present, uint32_t ac, uint64_t ar, uint
             best_n = (int32_t)n;
         }
     }
-#endif
 }
 template <bool W1, bool TF>
 K10S_D void scan_grp(const ScanGrp& g, uint32_t n0, uint32_t n_nodes, uint32_t rc, uint64_t rr, double frc,
@@ -1106,7 +1134,7 @@ K10S_D void scan_lanes(const uint32_t* s_cpu, const uint64_t* s_ram, const uint6
 }
 #endif
 
-// ---- screened scan (event loop, weight 1.0, rc > 0, rr > 0; K10S_SCAN_SCREEN) -----------------
+// ---- screened scan (weight 1.0, rc > 0, rr > 0: the event loop and the unit surface) -----------
 // With u = rc/A + rr/R, a fitting node's LeastAllocated score is 100 − 50·u (plugin.rs:52-63), so
 // the argmax is the u minimum.  Each lane keeps lu, the smallest u among the nodes it scored, and
 // after every 256-node step the wave takes thr = min lu: some scored node y has u(y) <= thr
@@ -1125,59 +1153,19 @@ K10S_HD bool scan_screen(uint32_t ac, uint64_t ar, float fa, float fr, float T) 
     const float fR = __builtin_fmaf((float)(uint32_t)(ar >> 32), 4294967296.0f, (float)(uint32_t)ar);
     return __builtin_fmaf(fa, fR, fr * fA) > fA * fR * T;
 }
-// The packed node cache's form of the screen (scan_lanes_screen_pk, which evaluates the same
-// operations two nodes per packed f32 instruction): entry x = cpu << 40 | ram, hi = x >> 32, lo =
-// (uint32_t)x; H = hi with the ram byte cleared = cpu·2^8 exactly (cpu < 2^24), and the test is
-// scan_screen's scaled by 2^8 (exact): the same decision as scan_screen on (cpu, ram).
-K10S_HD bool pk_screen_out(uint32_t hi, uint32_t lo, float fa256, float fr, float T) {
-    const float H = (float)(hi & 0xFFFFFF00u);
-    const float R = __builtin_fmaf((float)(hi & 0xFFu), 4294967296.0f, (float)lo);
-    return __builtin_fmaf(fa256, R, fr * H) > (H * R) * T;
-}
 // u of a scored node from its exact score: (100 − s)/50, rounded to f32.
 K10S_HD float screen_u(double s) { return (float)((100.0 - s) * 0.02); }
 
 #if K10S_DEVICE
-// 1 (default): the event loop's fast-path scans screen (+2.0 % at C3 once the scheduling cycle runs
-// out of line with its own registers, profiles/r02_v6_scan_screen_ab.json; inlined into the event
-// loop its state spilled inside the scan, r02_v3_scan_experiments_ab.json).  The unit-surface
-// kernel keeps the plain scan (it is HBM-bound).
-#ifndef K10S_SCAN_SCREEN
-#define K10S_SCAN_SCREEN 1
-#endif
-K10S_D void scan_node_screen(uint32_t n, bool present, uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr, double frc,
-                             double frr, float fa, float fr, float T, double& best_s, int32_t& best_n, uint32_t& la,
-                             uint64_t& lr, float& lu) {
-    if (rc <= ac && rr <= ar && present) {
-        if (ac == la && ar == lr) {
-            best_n = (int32_t)n;
-        } else if (!scan_screen(ac, ar, fa, fr, T)) {
-            const double fac = (double)ac;
-            const double cs = div_rn((fac - frc) * 100.0, fac);
-            const uint2 w = __builtin_bit_cast(uint2, ar);
-            const double far = u64_f64(ar);
-            double dr = far - frr;
-            if (__builtin_expect(w.y >= (1u << 21), 0)) dr = u64_f64(ar - rr);
-            const double s = (cs + div_rn(dr * 100.0, far)) * 0.5;
-            if (s >= best_s) {
-                best_s = s;
-                best_n = (int32_t)n;
-                la = ac;
-                lr = ar;
-            }
-            const float u = screen_u(s);
-            lu = u < lu ? u : lu;
-        }
-    }
-}
-// K10S_SCREEN_PACKED (default 1): scan_lanes_screen evaluates the screen of a lane's 4 nodes first
-// (screen_grp), then scores the remaining ones in order (score_node_exact); the same decisions and
-// the same f32 operations as scan_node_screen, so the same nodes are scored and the result is
-// identical, with fewer instructions: the conversions are single v_cvt_f32_u32 each, the products
-// run 2 nodes per v_pk_mul_f32 / v_pk_fma_f32, and no exec-mask branch separates the 4 nodes.
-#ifndef K10S_SCREEN_PACKED
-#define K10S_SCREEN_PACKED 1
-#endif
+// The event loop's fast-path scans screen (+2.0 % at C3 once the scheduling cycle runs out of line
+// with its own registers, profiles/r02_v6_scan_screen_ab.json; inlined into the event loop its state
+// spilled inside the scan, r02_v3_scan_experiments_ab.json), and so does the unit surface
+// (k10s_schedule_kernel: scoring every node exactly, two f64 divisions each, made it VALU-bound below
+// the HBM roofline, r02_v27_unit_screen.json).
+// scan_lanes_screen evaluates the screen of a lane's 4 nodes first (screen_grp), then scores the
+// remaining ones in order (score_node_exact): the conversions are single v_cvt_f32_u32 each, the
+// products run 2 nodes per v_pk_mul_f32 / v_pk_fma_f32, and no exec-mask branch separates the 4
+// nodes (round 2 tested and scored node by node: -59 VALU per event, +4.9 % at C3).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 K10S_D float cvt_f32_u32(uint32_t v) {   // (float)v, correctly rounded, as the one instruction
     float f;
@@ -1204,7 +1192,7 @@ K10S_D uint32_t screen_grp(const ScanGrp& g, uint32_t bits, uint32_t rc, uint64_
     return fit & ~out;
 }
 // A fitting node the screen did not rule out: the lane best's allocatables take the index (same
-// score), anything else is scored exactly (scan_node_screen's exact branch).
+// score), anything else is scored exactly (as scan_node_d).
 K10S_D void score_node_exact(uint32_t n, uint32_t ac, uint64_t ar, uint64_t rr, double frc, double frr, double& best_s,
                              int32_t& best_n, uint32_t& la, uint64_t& lr, float& lu) {
     if (ac == la && ar == lr) {
@@ -1239,121 +1227,11 @@ K10S_D float wave_min_f32(float v) {
     v = minf_step<3>(v); v = minf_step<4>(v); v = minf_step<5>(v);
     return v;
 }
-#ifndef K10S_SCREEN_NO_PRESENCE
-#define K10S_SCREEN_NO_PRESENCE 1
-#endif
-#ifndef K10S_SCAN_STEPS2
-#define K10S_SCAN_STEPS2 1
-#endif
-// NP: the event loop's own node cache (absent nodes hold (0, 0): no presence words read); the unit
-// surface's caller-owned buffers keep their presence bitmap.
-#define SCREEN_LOAD(c, r, p, n, n0)                                                                   \
-    (PK ? scan_load_pk(r, p, n, n0, !(NP && K10S_SCREEN_NO_PRESENCE))                                  \
-        : ((NP && K10S_SCREEN_NO_PRESENCE) ? scan_load_np(c, r, n, n0) : scan_load(c, r, p, n, n0)))
-// K10S_UNIT_SCREEN (default 1): the unit surface (k10s_schedule_kernel) screens too.  Scoring every
-// node exactly (two f64 divisions) made it VALU-bound below the HBM roofline.
-#ifndef K10S_UNIT_SCREEN
-#define K10S_UNIT_SCREEN 1
-#endif
-// The packed node cache's screened scan (event loop; K10S_SCAN_PK_SCREEN, default 0: measured slower,
-// profiles/r03_g1_pk_screen_ab.json — C3 1,341 vs 1,296 ms, backlog 4,089 vs 3,871 ms).  Same
-// decisions as scan_lanes_screen over the decoded entries, with fewer instructions per node:
-//  * Fit on the packed word: cpu >= rc  <=>  hi >= rc << 8 (hi = the entry's high word, cpu << 8 |
-//    ram >> 32; rc < 2^24, else nothing fits), ram >= rr on the low 40 bits;
-//  * the screen converts hi with its ram byte cleared, cpu·2^8 exactly, and evaluates scan_screen's
-//    test scaled by 2^8 (exact), as  fa·2^8·R + fr·H > H·R·T: the same decisions as scan_screen
-//    (pk_screen_out; tests/test_scan_screen.py test_packed_screen_*), and every node it keeps is
-//    scored exactly as before;
-//  * per-node decisions stay lane masks (SGPR pairs) instead of a per-lane 4-bit VGPR mask, and
-//    the valid-node mask is only built for the last, partial 512-node block.
-#ifndef K10S_SCAN_PK_SCREEN
-#define K10S_SCAN_PK_SCREEN 0
-#endif
-K10S_D float cvt_f32_ubyte0(uint32_t v) {   // (float)(v & 0xFF) as the one instruction
-    float f;
-    asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(f) : "v"(v));
-    return f;
-}
-// A node the screen kept (need): scored exactly.
-K10S_D void pk_score_node(bool need, uint64_t x, uint32_t n, double frc, double frr, double& best_s, int32_t& best_n,
-                          float& lu, bool& scored) {
-    if (need) {
-        // scored exactly (a node with the lane best's allocatables gets the same score and, being
-        // later, the index: "score >= best")
-        scored = true;
-        const uint32_t ac = (uint32_t)(x >> 40);
-        const uint64_t ar = x & K10S_PK_RAM;
-        const double fac = (double)ac;
-        const double cs = div_rn((fac - frc) * 100.0, fac);
-        const double s = (cs + div_rn((u64_f64(ar) - frr) * 100.0, u64_f64(ar))) * 0.5;   // ar < 2^40: exact
-        best_n = s >= best_s ? (int32_t)n : best_n;
-        best_s = s >= best_s ? s : best_s;
-        const float u = screen_u(s);
-        lu = u < lu ? u : lu;
-    }
-}
-K10S_D void scan_lanes_screen_pk(const uint64_t* s_node, uint32_t n_nodes, uint32_t rc, uint64_t rr, double& best_s,
-                                 int32_t& best_n) {
-    const uint32_t l4 = 4u * (uint32_t)lane_id();
-    rc = uniform_u32(rc);
-    rr = uniform_u64(rr);
-    if (n_nodes == 0 || rc > K10S_PK_CPU || rr > K10S_PK_RAM) return;   // no packed entry can hold them
-    const double frc = uniform_f64((double)rc), frr = uniform_f64(u64_f64(rr));
-    const float fa256 = (float)rc * 256.0f;
-    const float fr = __builtin_fmaf((float)(uint32_t)(rr >> 32), 4294967296.0f, (float)(uint32_t)rr);
-    const uint32_t rc8 = rc << 8;
-    float lu = __builtin_inff();
-    float T = __builtin_inff();
-    const f32x2 two32 = {4294967296.0f, 4294967296.0f}, va = {fa256, fa256}, vr = {fr, fr};
-    auto step = [&](ulonglong2 x01, ulonglong2 x23, uint32_t n0, auto mask) {
-        constexpr bool M = decltype(mask)::value;
-        const uint32_t h0 = (uint32_t)(x01.x >> 32), h1 = (uint32_t)(x01.y >> 32), h2 = (uint32_t)(x23.x >> 32),
-                       h3 = (uint32_t)(x23.y >> 32);
-        // the screen of the 4 nodes, 2 per packed f32 op
-        const f32x2 H01 = {cvt_f32_u32(h0 & 0xFFFFFF00u), cvt_f32_u32(h1 & 0xFFFFFF00u)};
-        const f32x2 H23 = {cvt_f32_u32(h2 & 0xFFFFFF00u), cvt_f32_u32(h3 & 0xFFFFFF00u)};
-        const f32x2 B01 = {cvt_f32_ubyte0(h0), cvt_f32_ubyte0(h1)}, B23 = {cvt_f32_ubyte0(h2), cvt_f32_ubyte0(h3)};
-        const f32x2 L01 = {cvt_f32_u32((uint32_t)x01.x), cvt_f32_u32((uint32_t)x01.y)};
-        const f32x2 L23 = {cvt_f32_u32((uint32_t)x23.x), cvt_f32_u32((uint32_t)x23.y)};
-        const f32x2 R01 = __builtin_elementwise_fma(B01, two32, L01), R23 = __builtin_elementwise_fma(B23, two32, L23);
-        const f32x2 vT = {T, T};
-        const f32x2 l01 = __builtin_elementwise_fma(va, R01, vr * H01), l23 = __builtin_elementwise_fma(va, R23, vr * H23);
-        const f32x2 r01 = (H01 * R01) * vT, r23 = (H23 * R23) * vT;
-        const bool n0k = rc8 <= h0 && rr <= (x01.x & K10S_PK_RAM) && !(l01.x > r01.x) && (!M || n0 < n_nodes);
-        const bool n1k = rc8 <= h1 && rr <= (x01.y & K10S_PK_RAM) && !(l01.y > r01.y) && (!M || n0 + 1 < n_nodes);
-        const bool n2k = rc8 <= h2 && rr <= (x23.x & K10S_PK_RAM) && !(l23.x > r23.x) && (!M || n0 + 2 < n_nodes);
-        const bool n3k = rc8 <= h3 && rr <= (x23.y & K10S_PK_RAM) && !(l23.y > r23.y) && (!M || n0 + 3 < n_nodes);
-        bool scored = false;
-        pk_score_node(n0k, x01.x, n0, frc, frr, best_s, best_n, lu, scored);
-        pk_score_node(n1k, x01.y, n0 + 1, frc, frr, best_s, best_n, lu, scored);
-        pk_score_node(n2k, x23.x, n0 + 2, frc, frr, best_s, best_n, lu, scored);
-        pk_score_node(n3k, x23.y, n0 + 3, frc, frr, best_s, best_n, lu, scored);
-        if (__ballot(scored)) {   // thr moves only when some lane scored a node exactly
-            const float thr = __builtin_bit_cast(float, uniform_u32(__builtin_bit_cast(uint32_t, wave_min_f32(lu))));
-            T = thr + K10S_SCREEN_EPS;
-        }
-    };
-    // whole 512-node blocks: the four 16-B loads of a lane from one address (offsets 0, 16, 2048,
-    // 2064 B), issued before any of them is used
-    uint32_t base = 0;
-    for (; base + 512u <= n_nodes; base += 512) {
-        const ulonglong2* p = reinterpret_cast<const ulonglong2*>(s_node + base + l4);
-        const ulonglong2 x0 = p[0], x1 = p[1], x2 = p[128], x3 = p[129];
-        step(x0, x1, base + l4, std::false_type());
-        step(x2, x3, base + 256u + l4, std::false_type());
-    }
-    if (base < n_nodes) {   // the partial last block: clamped addresses, masked nodes
-        const uint32_t a0 = base + l4, a1 = base + 256u + l4;
-        const uint32_t b0 = a0 < n_nodes ? a0 : 0u, b1 = a1 < n_nodes ? a1 : 0u;   // past the end: re-read 0..3
-        const ulonglong2 x0 = *reinterpret_cast<const ulonglong2*>(s_node + b0);
-        const ulonglong2 x1 = *reinterpret_cast<const ulonglong2*>(s_node + b0 + 2);
-        const ulonglong2 x2 = *reinterpret_cast<const ulonglong2*>(s_node + b1);
-        const ulonglong2 x3 = *reinterpret_cast<const ulonglong2*>(s_node + b1 + 2);
-        step(x0, x1, a0, std::true_type());
-        step(x2, x3, a1, std::true_type());
-    }
-}
-
+// NP: the event loop's own node cache (absent nodes hold (0, 0), so Fit alone excludes them with
+// rc > 0: no presence words read, r02_v10_presence_split_ab.json); the unit surface's caller-owned
+// buffers keep their presence bitmap.
+#define SCREEN_LOAD(c, r, p, n, n0) \
+    (PK ? scan_load_pk(r, p, n, n0, !NP) : (NP ? scan_load_np(c, r, n, n0) : scan_load(c, r, p, n, n0)))
 template <int PIPE, bool NP = true, bool PK = false>
 K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, const uint64_t* present, uint32_t n_nodes,
                               uint32_t rc, uint64_t rr, double& best_s, int32_t& best_n) {
@@ -1368,7 +1246,6 @@ K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, cons
     uint64_t lr = 0;
     float lu = __builtin_inff();
     float T = __builtin_inff();  // thr + eps: +inf screens nothing out (the first step)
-#if K10S_SCREEN_PACKED
     // one 256-node step of a lane's group g at n0 (screen, exact scores, threshold)
     auto step = [&](const ScanGrp& g, uint32_t n0, auto full) {
         const uint32_t bits = decltype(full)::value ? 0xFu : grp_bits(g, n0, n_nodes);
@@ -1384,15 +1261,14 @@ K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, cons
             T = thr + K10S_SCREEN_EPS;
         }
     };
-    // K10S_SCAN_STEPS2 (packed node cache, no load pipeline): the loads of two 256-node steps (32 B
-    // per lane each) are issued together, so a 4,096-node scan waits 8 memory round trips, not 16;
-    // a lane still visits its nodes in ascending order
-    // K10S_SCAN_FULLBLK (event loop, packed, no presence words): whole 512-node blocks load from
-    // unclamped addresses and screen all 4 nodes of a lane group without a validity mask; only the
-    // last, partial block builds one
-    if (PK && K10S_SCAN_STEPS2 && PIPE == 0) {
+    // Packed node cache, no load pipeline: the loads of two 256-node steps (32 B per lane each) are
+    // issued together, so a 4,096-node scan waits 8 memory round trips, not 16 (+2.4 %,
+    // r03_s4_knobs_ab.json); a lane still visits its nodes in ascending order.  In the event loop
+    // (no presence words) whole 512-node blocks load from unclamped addresses and screen all 4 nodes
+    // of a lane group without a validity mask; only the last, partial block builds one.
+    if (PK && PIPE == 0) {
         uint32_t base = 0;
-        if (K10S_SCAN_FULLBLK && NP && K10S_SCREEN_NO_PRESENCE) {
+        if (NP) {
             for (; base + 512u <= n_nodes; base += 512) {
                 const ScanGrp g0 = scan_load_pk_full(s_ram, base + l4);
                 const ScanGrp g1 = scan_load_pk_full(s_ram, base + 256u + l4);
@@ -1408,40 +1284,15 @@ K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, cons
         }
         return;
     }
-#endif
     ScanGrp g[PIPE + 1];
 #pragma unroll
     for (int i = 0; i < PIPE; i++) g[i] = SCREEN_LOAD(s_cpu, s_ram, present, n_nodes, 256u * i + l4);
     for (uint32_t base = 0; base < n_nodes; base += 256) {
         g[PIPE] = SCREEN_LOAD(s_cpu, s_ram, present, n_nodes, base + 256u * PIPE + l4);
         const uint32_t n0 = base + l4;
-        const uint32_t bits = grp_bits(g[0], n0, n_nodes);
-#if K10S_SCREEN_PACKED
-        // the screen of the lane's 4 nodes first, branch-free and 2 nodes per packed f32 op; only
-        // the nodes it cannot rule out take the sequential exact path below
-        const uint32_t need = screen_grp(g[0], bits, rc, rr, fa, fr, T);
-        if (need) {
-            if (need & 1u) score_node_exact(n0, g[0].cv.x, g[0].r01.x, rr, frc, frr, best_s, best_n, la, lr, lu);
-            if (need & 2u) score_node_exact(n0 + 1, g[0].cv.y, g[0].r01.y, rr, frc, frr, best_s, best_n, la, lr, lu);
-            if (need & 4u) score_node_exact(n0 + 2, g[0].cv.z, g[0].r23.x, rr, frc, frr, best_s, best_n, la, lr, lu);
-            if (need & 8u) score_node_exact(n0 + 3, g[0].cv.w, g[0].r23.y, rr, frc, frr, best_s, best_n, la, lr, lu);
-        }
-        // thr only moves when some lane scored a node exactly this step (lu changed): skip the
-        // 6-step wave reduction otherwise (T is then exactly what the reduction would give)
-        if (__ballot(need != 0)) {
-            const float thr = __builtin_bit_cast(float, uniform_u32(__builtin_bit_cast(uint32_t, wave_min_f32(lu))));
-            T = thr + K10S_SCREEN_EPS;
-        }
-#else
-        if (bits) {
-            scan_node_screen(n0, bits & 1u, g[0].cv.x, g[0].r01.x, rc, rr, frc, frr, fa, fr, T, best_s, best_n, la, lr, lu);
-            scan_node_screen(n0 + 1, bits & 2u, g[0].cv.y, g[0].r01.y, rc, rr, frc, frr, fa, fr, T, best_s, best_n, la, lr, lu);
-            scan_node_screen(n0 + 2, bits & 4u, g[0].cv.z, g[0].r23.x, rc, rr, frc, frr, fa, fr, T, best_s, best_n, la, lr, lu);
-            scan_node_screen(n0 + 3, bits & 8u, g[0].cv.w, g[0].r23.y, rc, rr, frc, frr, fa, fr, T, best_s, best_n, la, lr, lu);
-        }
-        const float thr = __builtin_bit_cast(float, uniform_u32(__builtin_bit_cast(uint32_t, wave_min_f32(lu))));
-        T = thr + K10S_SCREEN_EPS;
-#endif
+        // (thr only moves when some lane scored a node exactly this step: the 6-step wave reduction
+        // is skipped otherwise, T is then exactly what it would give)
+        step(g[0], n0, std::false_type());
 #pragma unroll
         for (int i = 0; i < PIPE; i++) g[i] = g[i + 1];
     }
@@ -1457,20 +1308,16 @@ K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const ui
     int32_t best_n = -1;
     int32_t first = 0x7fffffff;
 #if K10S_DEVICE
+    if (!K10S_FULL_WAVE(XG_SCHEDULE_SCAN)) return K10S_SCHED_NO_SUFFICIENT_RESOURCES;
     double best_s = -__builtin_inf();
     if (weight == 1.0 && rc > 0 && rr > 0) {
         // A fitting node has alloc >= request > 0 in both resources, so neither term is 0/0 and every
         // score is a finite number >= 0: filtered[0] is never NaN, "some node fits" <=> best_n >= 0,
         // and neither filtered[0] nor its re-scored value is needed (kube_scheduler.rs:140-148).
-        if (LOOP && K10S_SCAN_SCREEN && PK && K10S_SCAN_PK_SCREEN)
-            scan_lanes_screen_pk(s_ram, n_nodes, rc, rr, best_s, best_n);
-        else if (LOOP && K10S_SCAN_SCREEN)
+        if (LOOP)
             scan_lanes_screen<K10S_LOOP_SCAN_PIPE, true, PK>(s_cpu, s_ram, present, n_nodes, rc, rr, best_s, best_n);
-        else if (!LOOP && K10S_UNIT_SCREEN)
-            scan_lanes_screen<K10S_SCAN_PIPE, false, PK>(s_cpu, s_ram, present, n_nodes, rc, rr, best_s, best_n);
         else
-            scan_lanes<true, false, LOOP ? K10S_LOOP_SCAN_PIPE : K10S_SCAN_PIPE, PK>(s_cpu, s_ram, present, n_nodes, rc,
-                                                                                    rr, weight, first, best_s, best_n);
+            scan_lanes_screen<K10S_SCAN_PIPE, false, PK>(s_cpu, s_ram, present, n_nodes, rc, rr, best_s, best_n);
         best_key = best_n >= 0 ? score_key(best_s) : 0;
         wave_argmax(best_key, best_n);
         if (best_n < 0) return K10S_SCHED_NO_SUFFICIENT_RESOURCES;
@@ -1570,6 +1417,7 @@ K10S_HD int schedule_scan_plugins(Ctx& c, uint32_t rc, uint64_t rr, int32_t* cho
     int32_t best_n = -1;
     int32_t first = 0x7fffffff;
 #if K10S_DEVICE
+    if (!K10S_FULL_WAVE(XG_SCAN_PLUGINS)) return K10S_SCHED_NO_SUFFICIENT_RESOURCES;
     // each lane owns 4 consecutive nodes per 256-node step, as the LeastAllocated scan: one 16-B
     // load per u32 array and two per u64 array (sections 256-B aligned and padded; a lane past the
     // end re-reads nodes 0..3 and grp_bits masks them out); ascending per lane, then the cross-lane
@@ -1764,21 +1612,14 @@ K10S_HD int schedule_scan_pruned(Ctx& c, uint32_t rc, uint64_t rr, int32_t* chos
 }
 
 // ---- scheduling cycle (scheduler.rs:246-334) ----------------------------------------------------
-// K10S_CYCLE_INLINE=0 (default) keeps the cycle out of line on the device: a cycle runs once per
-// many events, and out of line its attempt loop (the node scans, the queue pops) gets its own
-// register allocation instead of sharing the event loop's.  With the action queue's top levels in
-// LDS (K10S_AQ_TOP=15) it measured +1.2 % on C3 and +16.7 % on the backlog workload, where cycles
-// run many attempts (profiles/r02_v5_knobs_ab.json).
-#ifndef K10S_CYCLE_INLINE
-#define K10S_CYCLE_INLINE 0
-#endif
-#if K10S_CYCLE_INLINE
-#define K10S_CYCLE_FN K10S_HD
-#else
-#define K10S_CYCLE_FN K10S_HD_NOINL
-#endif
+// The cycle runs out of line on the device: it runs once per many events, and out of line its
+// attempt loop (the node scans, the queue pops) gets its own register allocation instead of sharing
+// the event loop's.  With the action queue's top levels in LDS (K10S_AQ_TOP=15) that measured +1.2 %
+// on C3 and +16.7 % on the backlog workload, where cycles run many attempts
+// (profiles/r02_v5_knobs_ab.json).
 template <bool PLUG>
-K10S_CYCLE_FN void run_scheduling_cycle_t(Ctx& c, double t) {
+K10S_HD_NOINL void run_scheduling_cycle_t(Ctx& c, double t) {
+    if (!K10S_FULL_WAVE(XG_CYCLE)) return;
     double cycle_dur = 0.0;
     RepHdr* h = &c.H();
     h->g_pods_q = (uint64_t)h->aq_size + (uint64_t)h->uq_size;  // scheduler.rs:256-259
@@ -1861,6 +1702,7 @@ K10S_CYCLE_FN void run_scheduling_cycle_t(Ctx& c, double t) {
 // Calls f(p) for every pod p (ascending) with pred(p); stops early if c.H().error_code.
 template <typename Pred, typename F>
 K10S_HD void for_each_pod_in_order(Ctx& c, Pred pred, F f) {
+    if (!K10S_FULL_WAVE(XG_PODS_IN_ORDER)) return;
     const uint32_t P = c.S().n_pods;
     for (uint32_t base = 0; base < P; base += K10S_LANES) {
         uint32_t p = base + (uint32_t)lane_id();
@@ -2045,6 +1887,7 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
 // Calls f(i) for every set bit i of words[0, W) in ascending order; stops early on an error.
 template <typename F>
 K10S_HD void for_each_bit(Ctx& c, const uint64_t* words, uint32_t W, F f) {
+    if (!K10S_FULL_WAVE(XG_FOR_EACH_BIT)) return;
     for (uint32_t wb = 0; wb < W; wb += K10S_LANES) {
         const uint32_t w = wb + (uint32_t)lane_id();
         const uint64_t word = w < W ? words[w] : 0ull;
@@ -2081,6 +1924,7 @@ K10S_HD int32_t ca_first_fit(Ctx& c, uint32_t n, uint32_t skip, uint32_t rc, uin
     const uint32_t* cc = c.V().ca_cpu();
     const uint64_t* cr = c.V().ca_ram();
 #if K10S_DEVICE
+    if (!K10S_FULL_WAVE(XG_CA_FIRST_FIT)) return -1;
     // each lane tests 4 consecutive entries per 256-entry step (one 16-B cpu load, two 16-B ram
     // loads: the sections are 256-B aligned and padded, entries >= n are masked out)
     const uint32_t l4 = 4u * (uint32_t)lane_id();
@@ -2116,6 +1960,7 @@ K10S_HD int32_t ca_first_fit(Ctx& c, uint32_t n, uint32_t skip, uint32_t rc, uin
 // node's assignment set).  Device: rank sort, 64 elements per pass against all k.
 K10S_HD void ca_sort(const uint32_t* src, uint32_t* dst, uint32_t k) {
 #if K10S_DEVICE
+    if (!K10S_FULL_WAVE(XG_CA_SORT)) return;
     const uint32_t lane = (uint32_t)lane_id();
     for (uint32_t cb = 0; cb < k; cb += 64) {
         const uint32_t mine = cb + lane < k ? src[cb + lane] : 0xFFFFFFFFu;
@@ -2462,15 +2307,18 @@ K10S_WARM void on_ps(Ctx& c, K10S_EVARG) {
         // ring to storage, started first: N_BIND emits the finish self-event at t + dur + d and the
         // start at t + d, and at dur = 0 the finish, handled first, re-emits after the start), so
         // while no removal request has dropped a pod (ps_rm_n == 0) the membership check cannot fail
-        // and the pod line is not read.
+        // and the pod line is not read.  That needs durations >= 0 (a negative one can land the
+        // finish in storage before the start, persistent_storage.rs:313 then panics): the shortcut is
+        // taken only in the default kernel copy (K10S_TIME_KEY_ID: every duration >= 0 by routing).
 #if !K10S_DEVICE
-        // the host check build verifies the invariant the shortcut relies on at every such event
-        if (h->ps_rm_n == 0 && !(c.V().pod(p).flags & PF_IN_PS)) {
+        // the host check build verifies the invariant the shortcut relies on at every such event of
+        // a scenario the default copy would run
+        if (c.Ly().tnonneg && h->ps_rm_n == 0 && !(c.V().pod(p).flags & PF_IN_PS)) {
             fail(c, K10S_ERR_INVARIANT);
             return;
         }
 #endif
-        if (h->ps_rm_n != 0 && !(c.V().pod(p).flags & PF_IN_PS)) {
+        if ((!K10S_TIME_KEY_ID || h->ps_rm_n != 0) && !(c.V().pod(p).flags & PF_IN_PS)) {
             fail(c, K10S_PANIC_MISSING_POD);
             return;
         }
@@ -2984,6 +2832,7 @@ K10S_D uint64_t wave_sum_u64_cold(uint64_t v) {
 // node indices at a time; the f64 node averages are then summed serially over the created nodes in
 // name order (ascending index), the integer cluster sums in any order (exact).
 K10S_COLD void gauge_record(Ctx& c, double t) {
+    if (!K10S_FULL_WAVE(XG_GAUGE)) return;
     RepHdr* h = &c.H();
     if (h->gauge_n >= c.Ly().cap_gauge) {
         h->flags |= 4u;
@@ -3066,14 +2915,11 @@ K10S_COLD void on_metrics(Ctx& c, K10S_EVARG) {
     emit0(c, K10S_EV_M_POD_METRICS_TICK, 60.0);
 }
 
-// K10S_FAST_DISPATCH: the api server's pure forwarding cases for the per-pod message chain (the
-// same statements as in on_api_server) run inline in the event loop instead of through the
-// out-of-line handler call and its register save/restore.  Tuning knob, semantics-neutral.
-#ifndef K10S_FAST_DISPATCH
-#define K10S_FAST_DISPATCH 0
-#endif
-#if K10S_EV_BYREF
+// (Round 2 inlined the api server's forwarding cases here, K10S_FAST_DISPATCH: VGPR spills 20 -> 77,
+// -3 % at C3, profiles/r02_v14_fast_dispatch_ab.json; not kept.)
 K10S_HD void dispatch(Ctx& c, EvRef ep, uint32_t k) {
+    if (!K10S_FULL_WAVE(XG_DISPATCH)) return;
+    k = uniform_u32(k);   // wave-uniform by construction: scalar branches (see run_replica)
     if (k <= K10S_EV_M_GAUGE_TICK) on_metrics(c, ep);
     else if (k <= K10S_EV_AS_CREATE_GROUP_REQ) on_api_server(c, ep);
     else if (k <= K10S_EV_PS_POD_REMOVED) on_ps(c, ep);
@@ -3085,42 +2931,6 @@ K10S_HD void dispatch(Ctx& c, EvRef ep, uint32_t k) {
     else if (k <= K10S_EV_CA_RESP) on_ca(c, ep);
     else on_hpa(c, ep);
 }
-#else
-K10S_HD void dispatch(Ctx& c, const HeapEv& e) {
-    uint32_t k = e.kind;
-#if K10S_FAST_DISPATCH
-    switch (k) {
-    case K10S_EV_AS_CREATE_POD_REQ:   // api_server.rs:151-155
-        c.H().g_cur_pods += 1;
-        emit(c, K10S_EV_PS_CREATE_POD_REQ, c.P().as_to_ps_network_delay, -1, e.a, 0, 0.0, FQ_AS_TO_PS);
-        return;
-    case K10S_EV_AS_POD_STARTED:
-        emit(c, K10S_EV_PS_POD_STARTED, c.P().as_to_ps_network_delay, -1, e.a, 0, e.x, FQ_AS_TO_PS);
-        return;
-#if K10S_FAST_DISPATCH >= 2
-    case K10S_EV_AS_POD_FINISHED: {   // api_server.rs:262-265
-        RepHdr& H = c.H();
-        H.counters[K10S_C_TERMINATED_PODS] += 1;
-        H.pods_left -= 1;
-        H.counters[K10S_C_PODS_SUCCEEDED] += 1;
-        H.g_cur_pods -= 1;
-        emit(c, K10S_EV_PS_POD_FINISHED, c.P().as_to_ps_network_delay, -1, e.a, e.b, e.x, FQ_AS_TO_PS);
-        return;
-    }
-#endif
-    default:
-        break;
-    }
-#endif
-    if (k <= K10S_EV_M_GAUGE_TICK) on_metrics(c, e);
-    else if (k <= K10S_EV_AS_CREATE_GROUP_REQ) on_api_server(c, e);
-    else if (k <= K10S_EV_PS_POD_REMOVED) on_ps(c, e);
-    else if (k <= K10S_EV_S_REMOVE_POD) on_scheduler(c, e);
-    else if (k <= K10S_EV_N_REMOVE_POD) on_node(c, e);
-    else if (k <= K10S_EV_CA_RESP) on_ca(c, e);
-    else on_hpa(c, e);
-}
-#endif
 
 // Advance the trace cursor from `cur` past the workload events that are not in this replica's
 // trace (file position >= trace_prefix: k10s_replica_params.workload_prefix) and cache the head
@@ -3326,13 +3136,10 @@ K10S_HD bool src_head(Ctx& c, uint32_t q, uint32_t ntr, int64_t& k, uint32_t& s)
 // Replace source q's entry by its new head (key, seq), or drop it (has == false).  Device: one
 // 16-B LDS read per lane (lane i = entry i), the new positions from two ballots, one scattered
 // 16-B write per kept entry and one for the new entry: no serial walk.
-#if K10S_SLUPD_CALL
-K10S_CALL_IF(K10S_SLUPD_CALL) void sl_update(Ctx& c, uint32_t q, bool has, int64_t key, uint32_t seq) {
-#else
 K10S_HD void sl_update(Ctx& c, uint32_t q, bool has, int64_t key, uint32_t seq) {
-#endif
     RepHdr& H = c.H();
 #if K10S_DEVICE
+    if (!K10S_FULL_WAVE(XG_SL_UPDATE)) return;
     const uint32_t n = uniform_u32(H.sl_n);
     const uint32_t lane = (uint32_t)lane_id();
     SrcEnt E;
@@ -3403,11 +3210,8 @@ K10S_HD void sl_rebuild(Ctx& c, uint32_t ntr) {
 
 // Refill a drained delay-class window from the HBM ring: positions [hd, hd + min(W, tail - hd)),
 // one 32-B entry per lane, so a burst of FIFO events costs one memory round trip per K10S_FQW pops.
-#if K10S_FQREFILL_CALL
-K10S_CALL_IF(K10S_FQREFILL_CALL) void fq_refill(Ctx& c, int cls, uint32_t hd) {
-#else
 K10S_HD void fq_refill(Ctx& c, int cls, uint32_t hd) {
-#endif
+    if (!K10S_FULL_WAVE(XG_FQ_REFILL)) return;
     RepHdr& H = c.H();
     const uint32_t cap = c.Ly().cap_fq;
     const uint32_t avail = H.fq[cls].tail - hd;
@@ -3423,12 +3227,10 @@ K10S_HD void fq_refill(Ctx& c, int cls, uint32_t hd) {
 // 1,272 ms, the vmcnt(0) wait at the first copied entry also waits for the previous handler's
 // stores; profiles/r03_k5_fq_prefetch_ab.json.)
 // Remove the head event of source src (sl[0]) and move the source's entry in the source list to
-// its new head; a FIFO takes its next head from its window.  K10S_SL_FAST (default 1): when the new
+// its new head; a FIFO takes its next head from its window.  When the new
 // head still precedes sl[1], only sl[0]'s key is rewritten (tuning knob, semantics-neutral).
-#ifndef K10S_SL_FAST
-#define K10S_SL_FAST 1
-#endif
 K10S_HD void consume_source(Ctx& c, int src, uint32_t ntr) {
+    src = (int)uniform_u32((uint32_t)src);   // wave-uniform by construction: scalar branches (see run_replica)
     RepHdr& H = c.H();
     bool has;
     int64_t key = 0;
@@ -3470,7 +3272,7 @@ K10S_HD void consume_source(Ctx& c, int src, uint32_t ntr) {
     seq = uniform_u32(seq);
     // src is sl[0]: while its new head still precedes the second source (47 % of the events at C3,
     // profiles/r03_selection_policy_sim.json) only sl[0]'s key changes — no lane-parallel update
-    if (K10S_SL_FAST && has) {
+    if (has) {
         // sl[1] is read whether or not it is live (LDS; ignored when n <= 1), so the three reads
         // issue together
         const int64_t k1 = (int64_t)uniform_u64((uint64_t)H.sl[1].key);
@@ -3492,6 +3294,7 @@ K10S_HD void consume_source(Ctx& c, int src, uint32_t ntr) {
 // Lane-parallel over node indices with an early exit; a zero request never schedules
 // (RequestedResourcesAreZeros, kube_scheduler.rs:74-76).
 K10S_HD bool cache_fits(Ctx& c, uint32_t rc, uint64_t rr) {
+    if (!K10S_FULL_WAVE(XG_CACHE_FITS)) return true;
     if (rc == 0 && rr == 0) return false;
     const uint32_t N = c.S().n_nodes;
     const uint64_t* pres = c.V().s_present();
@@ -3539,19 +3342,12 @@ K10S_HD bool replica_stalled(Ctx& c) {
 // arbiter prefers the oldest wave among equal priorities, so with 8 identical replicas per SIMD the
 // oldest finished at 63 % of the launch and the youngest at 100 % (tools/wall_spread.py,
 // profiles/r02_v7_wall_spread_*.json): the SIMD ran the last third with fewer and fewer waves.
-// Every 2^K10S_FAIR_SHIFT events a wave picks a priority:
-//   1  random 0..3 from a hash of (replica, epoch)                       C3 2,089 -> 1,836 ms
-//   2  rotation by the wave's SIMD slot (2 waves per level)              1,871 ms
-//   3  rotation, one wave on top                                         1,913 ms
-//   4  least progress first (per-SIMD event board, 4 levels)             1,873 ms (all end together)
-//   5  (default) random 1..2 while within K10S_FAIR_BAND events of the SIMD's mean, 3 when behind
-//      by more, 0 when ahead by more                                     1,734 ms
-// Strict fairness (4) drains the SIMD together but lowers its throughput while all 8 waves run;
-// letting random waves lead inside a band keeps that throughput and still bounds the drift
-// (profiles/r02_v7_fair_ab.json).  Scheduling hints only: no effect on any result.
-#ifndef K10S_FAIR
-#define K10S_FAIR 5
-#endif
+// Every 2^K10S_FAIR_SHIFT events a wave adds its progress to a per-SIMD board and picks a priority:
+// random 1..2 while within K10S_FAIR_BAND events of its SIMD's mean, 3 when behind by more, 0 when
+// ahead by more.  Measured against the alternatives (profiles/r02_v7_fair_ab.json, C3 ms): none
+// 2,089; random 0..3 1,836; rotation by SIMD slot 1,871-1,913; strict least-progress-first 1,873
+// (every replica ends together but the SIMD issues less while 8 waves compete evenly); this banded
+// hybrid 1,734.  Scheduling hints only: no effect on any result.
 #ifndef K10S_FAIR_SHIFT
 #define K10S_FAIR_SHIFT 6
 #endif
@@ -3559,26 +3355,15 @@ K10S_HD bool replica_stalled(Ctx& c) {
 #define K10S_FAIR_BAND 512
 #endif
 #define K10S_FAIR_KEYS 4096   // XCC x SE x SH x CU x SIMD
-#if defined(__HIP__) && (K10S_FAIR == 4 || K10S_FAIR == 5)
+#if defined(__HIP__)
 __device__ uint32_t k10s_fair_board[2 * K10S_FAIR_KEYS];   // zeroed before every run launch
 #endif
 K10S_HD void fair_priority(uint64_t done) {
-#if K10S_DEVICE && K10S_FAIR
+#if K10S_DEVICE
     if ((done & ((1ull << K10S_FAIR_SHIFT) - 1)) != 0) return;
-#if K10S_FAIR == 2
-    // rotation by the wave's slot on its SIMD (HW_ID.WAVE_ID): over every 8 epochs each slot holds
-    // each priority for exactly 2 epochs, and the pairs that tie alternate
-    const uint32_t slot = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 4);
-    const uint32_t pr = ((slot + (uint32_t)(done >> K10S_FAIR_SHIFT)) & 7u) >> 1;
-#elif K10S_FAIR == 3
-    // rotation with a single wave on top: ranks 0..7 -> priorities 0,0,0,1,1,2,2,3
-    const uint32_t slot = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 4);
-    const uint32_t rk = (slot + (uint32_t)(done >> K10S_FAIR_SHIFT)) & 7u;
-    const uint32_t pr = (0xE940u >> (2u * rk)) & 3u;
-#elif K10S_FAIR == 4 || K10S_FAIR == 5
-    // least progress first: the waves of one SIMD (HW_ID + XCC_ID key) add their event counts to a
-    // per-SIMD board; a wave behind its SIMD's mean by more than one epoch runs at priority 3, one
-    // ahead by more than one epoch at 0 (vector atomics by lanes 0/1 on distinct words)
+    if (!K10S_FULL_WAVE(XG_FAIR)) return;
+    // the waves of one SIMD (HW_ID + XCC_ID key) add their event counts to a per-SIMD board (vector
+    // atomics by lanes 0/1 on distinct words)
     const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
     const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) & 7u;
     const uint32_t key = (((xcc * 4u + ((hw >> 13) & 3u)) * 2u + ((hw >> 12) & 1u)) * 16u + ((hw >> 8) & 15u)) * 4u +
@@ -3594,17 +3379,8 @@ K10S_HD void fair_priority(uint64_t done) {
     uint32_t nw = (uint32_t)__builtin_amdgcn_readlane((int)got, 1) + (done == 0 ? 1u : 0u);
     nw = nw ? nw : 1u;
     const int64_t lag = (int64_t)(tot / nw) - (int64_t)(done + inc);
-#if K10S_FAIR == 4
-    const uint32_t pr = lag > (int64_t)inc ? 3u : lag >= 0 ? 2u : lag >= -(int64_t)inc ? 1u : 0u;
-#else
-    // 5: random priority (as 1) while within K10S_FAIR_BAND events of the SIMD's mean; outside it the
-    // lagging wave is raised above every random draw and the leading one lowered below them
     const uint32_t rnd = 1u + (uint32_t)(splitmix64(((uint64_t)blockIdx.x << 32) ^ (done >> K10S_FAIR_SHIFT)) >> 63);
     const uint32_t pr = lag > (int64_t)K10S_FAIR_BAND ? 3u : lag < -(int64_t)K10S_FAIR_BAND ? 0u : rnd;
-#endif
-#else
-    const uint32_t pr = (uint32_t)(splitmix64(((uint64_t)blockIdx.x << 32) ^ (done >> K10S_FAIR_SHIFT)) >> 62);
-#endif
     switch (pr) {
     case 0: __builtin_amdgcn_s_setprio(0); break;
     case 1: __builtin_amdgcn_s_setprio(1); break;
@@ -3627,23 +3403,15 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
 #define ntr (c.S().n_trace)
 #define cap_log (c.Ly().cap_log)
     // one time limit per mode (until_time / max_time)
-#if K10S_DEVICE && K10S_RUN_ARGS_LDS
-    (void)mode; (void)until_time; (void)max_time; (void)budget;
-#define limit (k10s_run.limit)
-#define budget (k10s_run.budget)
-    auto until_mode = [&]() -> bool { return uniform_u32(k10s_run.until_mode) != 0; };
-#else
     const uint32_t until_mode0 = mode == K10S_RUN_UNTIL_TIME ? 1u : 0u;
     const double limit = until_mode0 ? until_time : max_time;
-    auto until_mode = [&]() -> bool {
-        return until_mode0 != 0;
-    };
-#endif
+    auto until_mode = [&]() -> bool { return until_mode0 != 0; };
     uint64_t done = 0;
     int more = 0;
     uint32_t status = K10S_REPLICA_RUNNING;
     const uint64_t t_loop = prof_now();
     sl_rebuild(c, ntr);  // the sorted source list, from the sources' heads
+    [[maybe_unused]] uint32_t it_stale = 0;
     while (!h->error_code) {
         if (!until_mode() && h->pods_left <= 0 && is_multiple_of_1000(h->clock)) {
             status = K10S_REPLICA_FINISHED;
@@ -3656,9 +3424,7 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
         bool have = false;
         const uint64_t t_sel = prof_now();
         sl_apply_dirty(c, ntr);
-#if K10S_EV_BYREF
         EvRef ep = K10S_EVREF(&h->heap_top);
-#endif
         for (;;) {
             if (uniform_u32(h->sl_n) == 0) break;
             src = (int)uniform_u32(h->sl[0].src);
@@ -3677,41 +3443,28 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
                     e.b = ta;
                 }
                 uniform_event(e);
-#if K10S_EV_BYREF
                 h->cur_ev = e;
                 ep = K10S_EVREF(&h->cur_ev);
-#endif
             } else if (src == SRC_HEAP) {
-#if K10S_EV_BYREF
                 e.kind = (uint16_t)uniform_u32(h->heap_top.kind);
                 e.a = uniform_u32(h->heap_top.a);
                 e.seq = uniform_u32(h->heap_top.seq);
                 e.time = uniform_f64(h->heap_top.time);
-#else
-                e = h->heap_top;
-                uniform_event(e);
-#endif
                 // canceled (lazy cancel): only while some canceled finish is pending is the pod read
                 if (e.kind == K10S_EV_N_POD_FINISHED && uniform_u32(h->stale_fin) != 0 &&
                     c.V().pod(e.a).finish_seq != e.seq) {
                     h->stale_fin -= 1;
                     heap_pop(c);
                     sl_refresh(c, SRC_HEAP, ntr);
+                    if (K10S_LOOP_CAP(it_stale, 1u << 24, XG_LOOP_STALE)) break;
                     continue;
                 }
-#if K10S_EV_BYREF
                 ep = K10S_EVREF(&h->heap_top);
-#endif
             } else {
-#if K10S_EV_BYREF
                 ep = K10S_EVREF(&h->fq_win[(uint32_t)src * K10S_FQW + (uniform_u32(h->fq[src].head) & (K10S_FQW - 1))]);
                 e.time = uniform_f64(ep->time);
                 e.seq = uniform_u32(ep->seq);
                 e.kind = (uint16_t)uniform_u32(ep->kind);
-#else
-                e = h->fq_win[(uint32_t)src * K10S_FQW + (h->fq[src].head & (K10S_FQW - 1))];
-                uniform_event(e);
-#endif
             }
             have = true;
             break;
@@ -3731,21 +3484,14 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
             more = 1;
             break;
         }
-#if !K10S_EV_BYREF
-        const uint64_t t_con = prof_now();
-        consume_source(c, src, ntr);
-        K10S_PROF_ADD(c, PROF_CONSUME, t_con);
-#endif
         h->clock = e.time;
         h->cur_kind = e.kind;
         h->cur_seq = e.seq;
         fair_priority(done);
         done++;  // counters[K10S_C_EVENTS] takes the launch's count once, at exit (no per-event LDS RMW)
         if (cap_log) {
-#if K10S_EV_BYREF
             e = *ep;   // parity logging: the whole event
             uniform_event(e);
-#endif
             uint32_t k = h->log_n;
             if (k < cap_log) {
                 k10s_log_entry le;
@@ -3789,29 +3535,16 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
                 h->flags |= 1u;
             }
         }
-#if K10S_DEVICE && defined(K10S_DBG_VALU)
-        // bottleneck probe (tooling builds only): K10S_DBG_VALU extra independent VALU ops per event
-        for (int i = 0; i < K10S_DBG_VALU; i++) asm volatile("v_mov_b32 v0, v0" ::: "v0");
-#endif
-#if K10S_DEVICE && defined(K10S_DBG_SALU)
-        // bottleneck probe (tooling builds only): K10S_DBG_SALU extra independent SALU ops per event
-        for (int i = 0; i < K10S_DBG_SALU; i++) asm volatile("s_add_u32 s0, s0, 0" ::: "s0", "scc");
-#endif
-#if K10S_DEVICE && defined(K10S_DBG_STORE)
-        // bottleneck probe: one extra HBM store per event just before the handler call (to the HBM
-        // copy of the header, which the launch's copy-out overwrites)
-        if (lane_id() == 0) ((volatile uint32_t*)&c.V().h()->tr_pad)[0] = (uint32_t)done;
-#endif
-#if K10S_DEVICE && defined(K10S_DBG_LAT)
-        // bottleneck probe: K10S_DBG_LAT extra dependent LDS round trips per event
-        {
-            uint32_t x = 0;
-            for (int i = 0; i < K10S_DBG_LAT; i++) x = uniform_u32(((volatile uint32_t*)&k10s_hdr.tr_pad)[x & 0]);
-            if (x == 0xDEADBEEFu) h->flags |= 0x100u;
+#if K10S_DEVICE && K10S_BEACON
+        if (lane_id() == 0) {
+            uint32_t* b = k10s_beacon + (uint64_t)blockIdx.x * K10S_BEACON_WORDS;
+            const uint32_t w[12] = {(uint32_t)done, e.kind, e.seq, (uint32_t)f2u(e.time), (uint32_t)(f2u(e.time) >> 32),
+                                    h->heap_size, h->stale_fin, h->sl_n, (uint32_t)src, h->aq_size, h->uq_size, e.a};
+            for (int i = 11; i >= 0; i--)   // word 0 (the event count) last
+                __hip_atomic_store(b + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
 #endif
         const uint64_t t_dis = prof_now();
-#if K10S_EV_BYREF
         dispatch(c, ep, e.kind);
         {   // the event stayed at the head of its source during the handler (an emission lands after
             // it: larger id, time >= clock); remove it now
@@ -3819,9 +3552,6 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
             consume_source(c, src, ntr);
             K10S_PROF_ADD(c, PROF_CONSUME, t_con);
         }
-#else
-        dispatch(c, e);
-#endif
         K10S_PROF_ADD(c, PROF_DISPATCH, t_dis);
 #if K10S_PROF
         h->prof[K10S_PROF_KIND0 + e.kind] += prof_now() - t_dis;
@@ -3840,10 +3570,6 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
     return more;
 #undef ntr
 #undef cap_log
-#if K10S_DEVICE && K10S_RUN_ARGS_LDS
-#undef limit
-#undef budget
-#endif
 }
 
 }  // namespace k10s

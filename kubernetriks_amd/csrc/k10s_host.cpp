@@ -289,7 +289,8 @@ k10s_engine* k10s_engine_create_bulk(const char* scenario_text, const void* pods
         }
     }
     // the node cache is packed unless some replica needs the wide SoA (k10s_capacities.node_cache)
-    e->L = make_layout(e->hs, c, !e->plugins && times_nonneg(e->hs, e->params.data(), n_replicas));
+    const bool tnn = times_nonneg(e->hs, e->params.data(), n_replicas);
+    e->L = make_layout(e->hs, c, !e->plugins && tnn, tnn);
     e->wide = e->plugins || !e->L.packed;
     auto fail = [&](const std::string& m) -> k10s_engine* {
         set_err(K10S_E_HIP, m);
@@ -308,6 +309,14 @@ k10s_engine* k10s_engine_create_bulk(const char* scenario_text, const void* pods
     size_t bytes = (size_t)e->L.stride * n_replicas;
     size_t free_b = 0, total_b = 0;
     (void)hipMemGetInfo(&free_b, &total_b);
+    if (bytes + (64ull << 20) > free_b && c.delay_fifo == 0 && e->L.cap_fq > 512) {
+        // the default rings grow with the node count (up to 8 x 8,192 x 32 B = 2 MiB per replica): when
+        // that does not fit, fall back to 512-entry rings (a fuller ring only spills to the heap)
+        k10s_capacities c512 = c;
+        c512.delay_fifo = 512;
+        e->L = make_layout(e->hs, c512, !e->plugins && tnn, tnn);
+        bytes = (size_t)e->L.stride * n_replicas;
+    }
     if (bytes + (64ull << 20) > free_b) {
         set_err(K10S_E_CAPACITY, "replica state (" + std::to_string(bytes >> 20) + " MiB) exceeds free device memory");
         engine_free(e);

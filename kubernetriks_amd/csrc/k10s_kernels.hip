@@ -98,13 +98,6 @@ __global__ K10S_RUN_BOUNDS void k10s_run_kernel(uint32_t n_replicas, int mode, d
     // hardware ids) in the profile slots, for the finish-time spread of one resident round
     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
 #endif
-#if K10S_RUN_ARGS_LDS
-    if (threadIdx.x == 0) {   // staged before hdr_copy's barrier
-        k10s_run.limit = mode == K10S_RUN_UNTIL_TIME ? until_time : max_time;
-        k10s_run.budget = budget;
-        k10s_run.until_mode = mode == K10S_RUN_UNTIL_TIME ? 1u : 0u;
-    }
-#endif
     sec_setup(r);
     hdr_copy((uint32_t*)&k10s_hdr, hdr_global(r));
     Ctx c;
@@ -199,16 +192,28 @@ hipError_t k10s_launch_run(const void* h_dcv, uint32_t n_replicas, int mode, dou
     std::lock_guard<std::mutex> g(g_launch_mu);
     hipError_t e = upload(h_dc, s);
     if (e != hipSuccess) return e;
-#if K10S_FAIR == 4 || K10S_FAIR == 5
     void* board = nullptr;
     e = hipGetSymbolAddress(&board, HIP_SYMBOL(k10s_fair_board));
     if (e == hipSuccess) e = hipMemsetAsync(board, 0, sizeof(k10s_fair_board), s);
     if (e != hipSuccess) return e;
-#endif
     hipLaunchKernelGGL(k10s_run_kernel, dim3(n_replicas), dim3(64), 0, s, n_replicas, mode, until_time, max_time,
                        budget, d_active);
     return hipGetLastError();
 }
+
+#if K10S_BEACON && !defined(K10S_PLUGINS_TU)
+// tooling builds only: host-mapped beacon memory for n_replicas replicas; returns its host address
+extern "C" void* k10s_debug_beacon_alloc(uint32_t n_replicas) {
+    void* h = nullptr;
+    void* d = nullptr;
+    const size_t bytes = sizeof(uint32_t) * K10S_BEACON_WORDS * (size_t)n_replicas;
+    if (hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
+    memset(h, 0xFF, bytes);
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) return nullptr;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(k10s_beacon), &d, sizeof d) != hipSuccess) return nullptr;
+    return h;
+}
+#endif
 
 #ifndef K10S_PLUGINS_TU
 hipError_t k10s_launch_schedule(const uint32_t* alloc_cpu, const uint64_t* alloc_ram, const uint64_t* present,

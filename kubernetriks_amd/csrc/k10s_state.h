@@ -239,7 +239,7 @@ struct RepHdr {
     // heap (valid while heap_size > 0)
     FqRing fq[K10S_NFQ];
     HeapEv heap_top;
-    HeapEv cur_ev;                // a trace event being handled (k10s_engine.h K10S_EV_BYREF)
+    HeapEv cur_ev;                // a trace event being handled (passed to its handler by reference)
     double tr_time;               // cached head of the shared trace stream (valid while
     uint32_t tr_seq, tr_pad;      // trace_cursor < n_trace)
     uint32_t trace_prefix;        // workload events at file positions >= this are not in this
@@ -367,7 +367,8 @@ struct Layout {
     uint32_t cap_gauge;   // gauge rows per replica (0 = gauge recorder off)
     uint32_t stall;       // 1: stall guard on (k10s_capacities.stall_guard)
     uint32_t packed;      // 1: node cache packed in s_node (8 B per node); 0: wide SoA s_cpu / s_ram
-    uint32_t pad_l;
+    uint32_t tnonneg;     // 1: every event time of the scenario and its replicas' parameters is >= 0
+                          // (times_nonneg): no emission can precede the clock
 };
 
 // Everything a launch reads but never writes, as one block (device: __constant__ memory).

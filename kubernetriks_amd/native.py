@@ -43,6 +43,8 @@ RUN_UNTIL_ALL_FINISHED = 0
 RUN_UNTIL_TIME = 1
 
 STATUS = {0: "running", 1: "finished", 2: "error", 3: "time_limit", 4: "stalled"}
+K10S_PANIC_MISSING_POD = 4
+K10S_PANIC_NEGATIVE_DELAY = 15   # dslab-core add_event refuses an event in the past (include/k10s.h)
 
 
 HIST_BINS = 32  # K10S_HIST_BINS (include/k10s.h): log2 bins, 0: < 2^-10 s, k: [2^(k-11), 2^(k-10)), 31: >= 2^20 s

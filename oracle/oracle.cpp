@@ -504,7 +504,11 @@ public:
     double panic_time = 0.0;
 
     /* ------------------------------------------------------------------ */
+    /* dslab-core SimulationState::add_event (rev 4ea3b3a, not vendored; restated): an event with a
+       negative delay — one in the past — is refused with a panic ("Event delay is negative! It is not
+       allowed to add events from the past."); `delay >= 0.` is false for NaN too. */
     std::shared_ptr<Ev> emit(int kind, double delay) {
+        if (!(delay >= 0.0)) panic("Event delay is negative! It is not allowed to add events from the past.");
         auto e = std::make_shared<Ev>();
         e->kind = kind;
         e->id = next_id++;

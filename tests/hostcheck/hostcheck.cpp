@@ -79,7 +79,8 @@ void* hc_create_bulk(const char* text, const void* blob, uint64_t blob_len, cons
     }
     bool plugins = false;
     for (uint32_t r = 0; r < R; r++) plugins |= h->params[r].score_plugins != K10S_SCORE_LEAST_ALLOCATED;
-    h->L = make_layout(h->hs, c, !plugins && times_nonneg(h->hs, h->params.data(), R));
+    const bool tnn = times_nonneg(h->hs, h->params.data(), R);
+    h->L = make_layout(h->hs, c, !plugins && tnn, tnn);
     h->state.assign((size_t)h->L.stride * R, 0);
     for (uint32_t r = 0; r < R; r++) {
         RepHdr work;
@@ -202,9 +203,3 @@ extern "C" int hc_scan_screen(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr
     return scan_screen(ac, ar, fa, fr, thr + K10S_SCREEN_EPS) ? 1 : 0;
 }
 extern "C" float hc_screen_u(double s) { return screen_u(s); }
-// The packed-entry screen (k10s_engine.h pk_screen_out, as scan_lanes_screen_pk forms its operands).
-extern "C" int hc_scan_screen_pk(uint64_t x, uint32_t rc, uint64_t rr, float thr) {
-    const float fa256 = (float)rc * 256.0f;
-    const float fr = __builtin_fmaf((float)(uint32_t)(rr >> 32), 4294967296.0f, (float)(uint32_t)rr);
-    return pk_screen_out((uint32_t)(x >> 32), (uint32_t)x, fa256, fr, thr + K10S_SCREEN_EPS) ? 1 : 0;
-}

@@ -12,7 +12,9 @@ from kubernetriks_amd.native import (Capacities, EngineBase, ReplicaParams, RUN_
                                      RUN_UNTIL_TIME, _decl)
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(REPO, "build", "libk10s_hostcheck.so")
+# K10S_HOSTCHECK_LIB: a prebuilt variant of the host build (e.g. the sanitizer build of
+# tools/hang_hostcheck.py); it is loaded as is, not rebuilt
+LIB_PATH = os.environ.get("K10S_HOSTCHECK_LIB") or os.path.join(REPO, "build", "libk10s_hostcheck.so")
 _lib = None
 
 
@@ -23,7 +25,8 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        build()
+        if not os.environ.get("K10S_HOSTCHECK_LIB"):
+            build()
         L = ctypes.CDLL(LIB_PATH)
         L.hc_create.restype = ctypes.c_void_p
         L.hc_create.argtypes = [ctypes.c_char_p, ctypes.POINTER(ReplicaParams), ctypes.c_uint32,

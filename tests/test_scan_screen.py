@@ -146,53 +146,3 @@ def test_adversarial_clusters_in_the_event_loop(backend):
         scn = _cluster_scenario(cpu, ram, 240 if backend == "gpu" else 80, seed=k)
         od, eng = parity.run_pair(_engine(backend), scn, max_time=50000.0)
         assert parity.compare(od, eng) == [], k
-
-
-# ---- the packed node cache's screen (k10s_engine.h pk_screen_out / scan_lanes_screen_pk) -------
-PK_CPU, PK_RAM = (1 << 24) - 1, (1 << 40) - 1
-
-
-def test_packed_screen_sound_near_threshold():
-    """The packed-entry screen (scan_screen's test on cpu·2^8 and ram, scaled by 2^8): a node it
-    drops still scores strictly below the node the threshold came from (nodes built within a few eps
-    of the threshold, over the packed ranges cpu < 2^24, ram < 2^40); it drops nearly every node
-    clearly above the threshold; and it decides every node exactly as scan_screen does."""
-    L = _hc()
-    L.hc_scan_screen_pk.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float]
-    L.hc_scan_screen_pk.restype = ctypes.c_int
-    rng = random.Random(11)
-    dropped = far = far_dropped = 0
-    for _ in range(1500):
-        B = rng.choice([64000, 1000, rng.randint(1, PK_CPU), PK_CPU, rng.randint(1, 200)])
-        S = rng.choice([rng.randint(1, PK_RAM), PK_RAM, 137438953472, rng.randint(1, 5000), rng.randint(1 << 32, PK_RAM)])
-        rc, rr = _rand_req(rng, B, S)
-        sy = la(B, S, rc, rr)
-        thr = L.hc_screen_u(sy)
-        uy = rc / B + rr / S
-        for _ in range(12):
-            A = min(rng.choice([rng.randint(rc, max(rc, 2 * B)), B, rc]), PK_CPU)
-            rest = uy + rng.uniform(-1.0, 3.0) * EPS - rc / A
-            if rest <= 0:
-                continue
-            R = int(rr / rest)
-            for R2 in (R - 1, R, R + 1, rng.randint(rr, max(rr, 2 * S))):
-                if not (rr <= R2 <= PK_RAM) or R2 < 1:
-                    continue
-                x = (A << 40) | R2
-                if L.hc_scan_screen_pk(x, rc, rr, thr):
-                    dropped += 1
-                    assert la(A, R2, rc, rr) < sy, (A, R2, rc, rr, B, S)
-                assert L.hc_scan_screen_pk(x, rc, rr, thr) == L.hc_scan_screen(A, R2, rc, rr, thr), (A, R2, rc, rr)
-                if rc / A + rr / R2 > uy + 2.2 * EPS:
-                    far += 1
-                    far_dropped += L.hc_scan_screen_pk(x, rc, rr, thr)
-    assert dropped > 4000
-    assert far_dropped >= 0.98 * far, (far_dropped, far)
-
-
-def test_packed_screen_keeps_everything_before_the_first_threshold():
-    L = _hc()
-    L.hc_scan_screen_pk.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float]
-    L.hc_scan_screen_pk.restype = ctypes.c_int
-    assert not L.hc_scan_screen_pk((64000 << 40) | (1 << 37), 500, 1 << 30, float("inf"))
-    assert not L.hc_scan_screen_pk((PK_CPU << 40) | PK_RAM, 1, 1, float("inf"))

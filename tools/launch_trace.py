@@ -34,9 +34,19 @@ def main():
         running = [r for r in res if r.status == 0]
         ev = int(eng.counter_matrix().sum(axis=0)[14])
         clk = min((r.clock for r in running), default=None)
-        print(f"launch {i}: running {len(running)} events {ev} min_clock {clk} t={time.time() - t0:.1f}s", flush=True)
+        errs = {}
+        for r in res:
+            if r.status == 2:
+                k = (r.error_code, r.error_kind)
+                errs[k] = errs.get(k, 0) + 1
+        print(f"launch {i}: running {len(running)} events {ev} min_clock {clk} errors(code,kind) {errs} "
+              f"t={time.time() - t0:.1f}s", flush=True)
         if not running:
             break
+    st = {}
+    for r in eng.raw_results():
+        st[r.status] = st.get(r.status, 0) + 1
+    print("status counts", st, "events", int(eng.counter_matrix().sum(axis=0)[14]), flush=True)
 
 
 if __name__ == "__main__":

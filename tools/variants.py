@@ -1,14 +1,15 @@
 #!/usr/bin/env python3
 """Build semantics-neutral variant libraries for A/B runs on the GPU (load one with K10S_LIB=...).
 
-  prof   -DK10S_PROF=1: cycle attribution of the event loop (bench.py --profile)
-  wN     -DK10S_WAVES_PER_EU=N
-  sN     -DK10S_SPLIT=N
-  pN     -DK10S_SCAN_PIPE=N (scan loads N steps ahead)
-  qN     -DK10S_FQW=N (delay-class FIFO window entries in LDS)
-  bfN    -DK10S_SCAN_BF=N (branch-free node scan)
-  hN     -DK10S_HEAP_D=N (event-heap arity: 8, 16, 32, 64)
-  NAME=v -DK10S_NAME=v (any knob), parts joined by '+'
+Live knobs (round 4 removed the measured-and-not-kept alternatives; their A/B history is DESIGN §7c):
+  tooling   prof  -DK10S_PROF=1 (cycle attribution, bench.py --profile); EXEC_CHECK=1|2|3 (entry guards /
+            loop bounds, tools/launch_trace.py); BEACON=1 (host-mapped progress beacon,
+            tools/beacon_trace.py); WALL=1 (tools/wall_spread.py)
+  numeric   wN -DK10S_WAVES_PER_EU=N; sN -DK10S_SPLIT=N (out-of-line handlers); pN -DK10S_SCAN_PIPE=N
+            (unit-surface scan loads N steps ahead); LOOP_SCAN_PIPE=N; qN -DK10S_FQW=N (FIFO window
+            entries in LDS); hN -DK10S_HEAP_D=N (event-heap arity 8/16/32/64); AQ_TOP=N;
+            FAIR_SHIFT=N, FAIR_BAND=N (wave priorities)
+  NAME=v    -DK10S_NAME=v (any of the above by name), parts joined by '+'
 Usage: tools/variants.py prof w8 s1 WAVES_PER_EU=8+FQW=4 ..."""
 import os
 import sys
@@ -32,8 +33,6 @@ def flags(name):
             out.append(f"-DK10S_FQW={int(part[1:])}")
         elif part.startswith("h") and part[1:].isdigit():
             out.append(f"-DK10S_HEAP_D={int(part[1:])}")
-        elif part.startswith("bf"):
-            out.append(f"-DK10S_SCAN_BF={int(part[2:])}")
         elif part.startswith("s"):
             out.append(f"-DK10S_SPLIT={int(part[1:])}")
         else:
