@@ -50,6 +50,11 @@
 #endif
 
 #if defined(__HIP_DEVICE_COMPILE__)
+#define K10S_UNROLL _Pragma("unroll")
+#else
+#define K10S_UNROLL
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
 #define K10S_DEVICE 1
 #define K10S_LANES 64
 #else

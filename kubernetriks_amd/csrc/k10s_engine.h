@@ -1611,91 +1611,253 @@ K10S_HD int schedule_scan_pruned(Ctx& c, uint32_t rc, uint64_t rr, int32_t* chos
     return K10S_SCHED_OK;
 }
 
+// ---- batched fit pass of a cycle tile (exact early fail) -----------------------------------------
+// Nothing is pushed onto the action queue during a cycle (scheduler.rs:261-330: a failed pod goes to
+// the unschedulable map, every emission to the event queue), so the cycle's pod sequence is fixed
+// when it starts, and the only change the cycle makes to the node cache is reserve_node_resources
+// (scheduler.rs:118-123), which lowers one node's allocatable.  So a pod that fits no node of the
+// cache as it is when its tile is formed fits no node when its turn comes: its attempt fails with
+// NoSufficientResources (kube_scheduler.rs:89-97), exactly as the scan would find.  The fit pass
+// answers "fits some node?" for K10S_TILE pods with one read of the node cache (packed entries, two
+// 16-B loads per lane per 512 nodes as the screened scan; per node and pod one 32-bit and one 64-bit
+// compare into lane masks), and stops as soon as every pod of the tile has a fitting node.  Pods
+// that fit are then scheduled one at a time by the exact scan, in order, on the current cache.
+// Used only after a cycle with failed attempts (RepHdr::cyc_fails): in the light regime every pod
+// fits and the pass would only add reads; in the backlog regime most attempts fail and their node
+// scans become one shared read per tile.
+#ifndef K10S_TILE
+#define K10S_TILE 8
+#endif
+static_assert(K10S_TILE >= 1 && K10S_TILE <= 32, "K10S_TILE");
+// Bit j set: pod j of the tile (need bit j: request rc8[j] = cpu << 8, rr[j] = ram, both > 0 and cpu
+// < 2^24) fits some node of the packed cache (cpu field >= cpu, ram field >= ram).  Absent nodes hold
+// (0, 0) and fit nothing.  *nread: cache entries read.
+K10S_HD uint32_t fit_tile(const uint64_t* s_node, uint32_t n_nodes, const uint32_t* rc8, const uint64_t* rr,
+                          uint32_t need, uint32_t* nread) {
+    uint32_t found = 0;
+#if K10S_DEVICE
+    const uint32_t l4 = 4u * (uint32_t)lane_id();
+    uint32_t base = 0;
+    for (; base < n_nodes && (found & need) != need; base += 512) {
+        // a lane's 8 nodes of this 512-node block (past the end: entries 0..3 re-read, then zeroed)
+        const uint32_t a0 = base + l4, a1 = base + 256u + l4;
+        const uint32_t b0 = a0 < n_nodes ? a0 : 0u, b1 = a1 < n_nodes ? a1 : 0u;
+        const ulonglong2 p0 = *reinterpret_cast<const ulonglong2*>(s_node + b0);
+        const ulonglong2 p1 = *reinterpret_cast<const ulonglong2*>(s_node + b0 + 2);
+        const ulonglong2 p2 = *reinterpret_cast<const ulonglong2*>(s_node + b1);
+        const ulonglong2 p3 = *reinterpret_cast<const ulonglong2*>(s_node + b1 + 2);
+        uint64_t x[8] = {p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y};
+        if (base + 512u > n_nodes) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t n = (k < 4 ? a0 : a1) + (uint32_t)(k & 3);
+                x[k] = n < n_nodes ? x[k] : 0ull;
+            }
+        }
+        uint32_t hi[8];
+        uint64_t ram[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            hi[k] = (uint32_t)(x[k] >> 32);      // cpu << 8 | ram >> 32
+            ram[k] = x[k] & K10S_PK_RAM;
+        }
+#pragma unroll
+        for (int j = 0; j < K10S_TILE; j++) {
+            if (!((need & ~found) >> j & 1u)) continue;   // wave-uniform
+            bool f = false;
+#pragma unroll
+            for (int k = 0; k < 8; k++) f |= hi[k] >= rc8[j] && ram[k] >= rr[j];
+            if (__ballot(f)) found |= 1u << j;
+        }
+    }
+    *nread = base < n_nodes ? base : n_nodes;
+#else
+    uint32_t n = 0;
+    for (; n < n_nodes && (found & need) != need; n++) {
+        const uint64_t x = s_node[n];
+        for (int j = 0; j < K10S_TILE; j++)
+            if ((need >> j & 1u) && (uint32_t)(x >> 32) >= rc8[j] && (x & K10S_PK_RAM) >= rr[j]) found |= 1u << j;
+    }
+    *nread = n;
+#endif
+    return found;
+}
+
 // ---- scheduling cycle (scheduler.rs:246-334) ----------------------------------------------------
 // The cycle runs out of line on the device: it runs once per many events, and out of line its
 // attempt loop (the node scans, the queue pops) gets its own register allocation instead of sharing
 // the event loop's.  With the action queue's top levels in LDS (K10S_AQ_TOP=15) that measured +1.2 %
 // on C3 and +16.7 % on the backlog workload, where cycles run many attempts
 // (profiles/r02_v5_knobs_ab.json).
+// One iteration of the cycle's loop (scheduler.rs:270-329) for a live pod q at cycle time t, with the
+// cycle's running duration and failure count; nofit: a tile's fit pass found no node for the pod
+// (its attempt then fails exactly as the scan would).
+template <bool PLUG>
+K10S_HD void cycle_attempt(Ctx& c, double t, QInfo q, bool nofit, double& cycle_dur, uint32_t& fails) {
+    RepHdr* h = &c.H();
+    const double w = c.P().score_weight;
+    const uint32_t p = q.pod;
+    const double queue_t = t - q.initial + cycle_dur;
+    const uint32_t nn = h->s_node_count;
+    const double sched_time = 0.000001 * (double)nn;  // ConstantTimePerNodeModel (model.rs:24-26)
+    cycle_dur += sched_time;
+    const uint32_t rc = c.V().pod(p).req_cpu;
+    const uint64_t rr = c.V().pod(p).req_ram;
+    int st;
+    int32_t chosen = -1;
+    if (rc == 0 && rr == 0) {
+        st = K10S_SCHED_REQUESTED_RESOURCES_ARE_ZEROS;
+    } else if (nn == 0) {
+        st = K10S_SCHED_NO_NODES_IN_CLUSTER;
+    } else {
+        h->counters[K10S_C_ATTEMPTS] += 1;
+        h->counters[K10S_C_NODES_SCANNED] += nn;
+        st = -1;
+        uint32_t nread = 0;
+        const uint64_t t_scan = prof_now();
+        if (nofit) {
+            st = K10S_SCHED_NO_SUFFICIENT_RESOURCES;   // (the tile's fit pass counted its reads)
+        } else if (PLUG) {
+            st = schedule_scan_plugins(c, rc, rr, &chosen);
+            nread = c.S().n_nodes;
+        } else if (!nc_packed(c) && c.Ly().pruned && w == 1.0 && rc > 0 && rr > 0) {
+            st = schedule_scan_pruned(c, rc, rr, &chosen, &nread);
+        }
+        if (st < 0) {
+            if (nc_packed(c))
+                st = schedule_scan<true, true>(nullptr, c.V().s_node(), c.V().s_present(), c.S().n_nodes, rc, rr, w,
+                                               &chosen);
+            else
+                st = schedule_scan<true, false>(c.V().s_cpu(), c.V().s_ram(), c.V().s_present(), c.S().n_nodes, rc, rr,
+                                                w, &chosen);
+            nread = c.S().n_nodes;
+        }
+        h->counters[K10S_C_NODES_READ] += nread;
+        K10S_PROF_ADD(c, PROF_SCAN, t_scan);
+        K10S_PROF_COUNT(c, PROF_NSCAN);
+    }
+    if (st != K10S_SCHED_OK) {
+        fails += 1;
+        q.timestamp = t + cycle_dur;
+        uq_insert(c, q);
+        emit(c, K10S_EV_AS_POD_NOT_SCHEDULED, c.P().sched_to_as_network_delay, -1, p, 0, t + cycle_dur, FQ_SCHED_TO_AS);
+        return;
+    }
+    const uint32_t n = (uint32_t)chosen;
+    nc_reserve(c, n, rc, rr);  // reserve_node_resources (118-123)
+    node_bound_changed(c, n);
+    c.V().node(n).flags |= NF_S_ASSIGN;  // assign_node_to_pod (125-151)
+    c.V().pod(p).s_assigned = (int32_t)n;
+    emit(c, K10S_EV_AS_ASSIGN_REQ, cycle_dur + c.P().sched_to_as_network_delay, -1, p, n, t + cycle_dur, FQ_ASSIGN);
+    h->counters[K10S_C_PLACEMENTS] += 1;
+    if (c.V().place()) {
+        const uint32_t k = h->place_n;
+        if (k < c.Ly().cap_place) {
+            c.V().place()[k].assign_time = t + cycle_dur;
+            c.V().place()[k].pod = (int32_t)p;
+            c.V().place()[k].node = (int32_t)n;
+            h->place_n = k + 1;
+        } else {
+            h->flags |= 2u;
+        }
+    }
+    est_add(h->est[K10S_EST_POD_SCHEDULE_TIME], sched_time);
+    est_add(h->est[K10S_EST_POD_QUEUE_TIME], queue_t);
+}
+// The end of a cycle: the next one after max(its duration, the interval) (scheduler.rs:331-333).
+K10S_HD void cycle_end(Ctx& c, double cycle_dur, uint32_t fails) {
+    c.H().cyc_fails = fails;
+    emit0(c, K10S_EV_S_RUN_CYCLE, fmax_rs(cycle_dur, c.P().scheduling_cycle_interval));
+}
+
 template <bool PLUG>
 K10S_HD_NOINL void run_scheduling_cycle_t(Ctx& c, double t) {
     if (!K10S_FULL_WAVE(XG_CYCLE)) return;
     double cycle_dur = 0.0;
+    uint32_t fails = 0;
     RepHdr* h = &c.H();
     h->g_pods_q = (uint64_t)h->aq_size + (uint64_t)h->uq_size;  // scheduler.rs:256-259
-    const double w = c.P().score_weight;
     while (c.H().aq_size > 0 && !c.H().error_code) {
         const uint64_t t_aq = prof_now();
-        QInfo q = aq_pop(c);
+        const QInfo q = aq_pop(c);
         K10S_PROF_ADD(c, PROF_AQPOP, t_aq);
-        uint32_t p = q.pod;
-        if (!pod_in_s(c, p)) continue;
-        double queue_t = t - q.initial + cycle_dur;
-        uint32_t nn = h->s_node_count;
-        double sched_time = 0.000001 * (double)nn;  // ConstantTimePerNodeModel (model.rs:24-26)
-        cycle_dur += sched_time;
-        uint32_t rc = c.V().pod(p).req_cpu;
-        uint64_t rr = c.V().pod(p).req_ram;
-        int st;
-        int32_t chosen = -1;
-        if (rc == 0 && rr == 0) {
-            st = K10S_SCHED_REQUESTED_RESOURCES_ARE_ZEROS;
-        } else if (nn == 0) {
-            st = K10S_SCHED_NO_NODES_IN_CLUSTER;
-        } else {
-            h->counters[K10S_C_ATTEMPTS] += 1;
-            h->counters[K10S_C_NODES_SCANNED] += nn;
-            st = -1;
-            uint32_t nread = 0;
-            const uint64_t t_scan = prof_now();
-            if (PLUG) {
-                st = schedule_scan_plugins(c, rc, rr, &chosen);
-                nread = c.S().n_nodes;
-            } else if (!nc_packed(c) && c.Ly().pruned && w == 1.0 && rc > 0 && rr > 0) {
-                st = schedule_scan_pruned(c, rc, rr, &chosen, &nread);
-            }
-            if (st < 0) {
-                if (nc_packed(c))
-                    st = schedule_scan<true, true>(nullptr, c.V().s_node(), c.V().s_present(), c.S().n_nodes, rc, rr,
-                                                   w, &chosen);
-                else
-                    st = schedule_scan<true, false>(c.V().s_cpu(), c.V().s_ram(), c.V().s_present(), c.S().n_nodes, rc,
-                                                    rr, w, &chosen);
-                nread = c.S().n_nodes;
-            }
-            h->counters[K10S_C_NODES_READ] += nread;
-            K10S_PROF_ADD(c, PROF_SCAN, t_scan);
-            K10S_PROF_COUNT(c, PROF_NSCAN);
-        }
-        if (st != K10S_SCHED_OK) {
-            q.timestamp = t + cycle_dur;
-            uq_insert(c, q);
-            emit(c, K10S_EV_AS_POD_NOT_SCHEDULED, c.P().sched_to_as_network_delay, -1, p, 0, t + cycle_dur, FQ_SCHED_TO_AS);
-            continue;
-        }
-        uint32_t n = (uint32_t)chosen;
-        nc_reserve(c, n, rc, rr);  // reserve_node_resources (118-123)
-        node_bound_changed(c, n);
-        c.V().node(n).flags |= NF_S_ASSIGN;  // assign_node_to_pod (125-151)
-        c.V().pod(p).s_assigned = (int32_t)n;
-        emit(c, K10S_EV_AS_ASSIGN_REQ, cycle_dur + c.P().sched_to_as_network_delay, -1, p, n, t + cycle_dur, FQ_ASSIGN);
-        h->counters[K10S_C_PLACEMENTS] += 1;
-        if (c.V().place()) {
-            uint32_t k = h->place_n;
-            if (k < c.Ly().cap_place) {
-                c.V().place()[k].assign_time = t + cycle_dur;
-                c.V().place()[k].pod = (int32_t)p;
-                c.V().place()[k].node = (int32_t)n;
-                h->place_n = k + 1;
-            } else {
-                h->flags |= 2u;
-            }
-        }
-        est_add(h->est[K10S_EST_POD_SCHEDULE_TIME], sched_time);
-        est_add(h->est[K10S_EST_POD_QUEUE_TIME], queue_t);
+        if (!pod_in_s(c, q.pod)) continue;   // removed from the cache (scheduler.rs:263-269)
+        cycle_attempt<PLUG>(c, t, q, false, cycle_dur, fails);
     }
-    double next = fmax_rs(cycle_dur, c.P().scheduling_cycle_interval);
-    emit0(c, K10S_EV_S_RUN_CYCLE, next);
+    cycle_end(c, cycle_dur, fails);
+}
+
+// The cycle in tiles (fit_tile above): run after a cycle with failed attempts, on the
+// LeastAllocated-only fast path with the packed cache (its own out-of-line function, so the serial
+// cycle's register allocation is unchanged).  The next K10S_TILE entries are popped in order (the
+// same pops the loop would make) and kept in the queue array slots their pops vacated (slot top-1-j
+// for the j-th: the array only shrinks during a cycle; HBM part), a removed pod marked and later
+// skipped like the loop's `continue`; their fit is tested together, then each is attempted in order.
+K10S_HD_NOINL void run_scheduling_cycle_tiles(Ctx& c, double t) {
+    if (!K10S_FULL_WAVE(XG_CYCLE)) return;
+    double cycle_dur = 0.0;
+    uint32_t fails = 0;
+    RepHdr* h = &c.H();
+    h->g_pods_q = (uint64_t)h->aq_size + (uint64_t)h->uq_size;  // scheduler.rs:256-259
+    while (c.H().aq_size > 0 && !c.H().error_code) {
+        QInfo* slot = c.V().aq();
+        const uint32_t top = uniform_u32(h->aq_size);
+        uint32_t nt = 0;
+        const uint64_t t_aq = prof_now();
+        for (; nt < K10S_TILE && c.H().aq_size > 0; nt++) {
+            QInfo q = aq_pop(c);
+            if (!pod_in_s(c, q.pod)) q.pod = 0xFFFFFFFFu;
+            slot[top - 1 - nt] = q;
+        }
+        K10S_PROF_ADD(c, PROF_AQPOP, t_aq);
+        wave_sync();
+        // the tile's requests (fast-path pods only: both requests > 0 and within the packed fields;
+        // a request beyond them fits no packed entry)
+        uint32_t rc8[K10S_TILE];
+        uint64_t rrq[K10S_TILE];
+        uint32_t need = 0, never = 0;
+        K10S_UNROLL
+        for (int j = 0; j < K10S_TILE; j++) {
+            rc8[j] = 0xFFFFFFFFu;
+            rrq[j] = ~0ull;
+            if ((uint32_t)j < nt) {
+                const uint32_t p = uniform_u32(slot[top - 1 - j].pod);
+                if (p != 0xFFFFFFFFu) {
+                    const uint32_t rc = uniform_u32(c.V().pod(p).req_cpu);
+                    const uint64_t rr = uniform_u64(c.V().pod(p).req_ram);
+                    if (rc > 0 && rr > 0) {
+                        if (rc <= K10S_PK_CPU && rr <= K10S_PK_RAM) {
+                            rc8[j] = rc << 8;
+                            rrq[j] = rr;
+                            need |= 1u << j;
+                        } else {
+                            never |= 1u << j;
+                        }
+                    }
+                }
+            }
+        }
+        uint32_t found = 0;
+        if (need && h->s_node_count > 0) {
+            uint32_t nread = 0;
+            const uint64_t t_fit = prof_now();
+            found = fit_tile(c.V().s_node(), c.S().n_nodes, rc8, rrq, need, &nread);
+            h->counters[K10S_C_NODES_READ] += nread;
+            K10S_PROF_ADD(c, PROF_SCAN, t_fit);
+        }
+        const uint32_t nofit = (need & ~found) | never;
+        for (uint32_t j = 0; j < nt && !c.H().error_code; j++) {
+            const QInfo q = slot[top - 1 - j];
+            if (uniform_u32(q.pod) == 0xFFFFFFFFu) continue;
+            QInfo u;
+            u.timestamp = uniform_f64(q.timestamp);
+            u.initial = uniform_f64(q.initial);
+            u.attempts = uniform_u32(q.attempts);
+            u.pod = uniform_u32(q.pod);
+            cycle_attempt<false>(c, t, u, (nofit >> j) & 1u, cycle_dur, fails);
+        }
+    }
+    cycle_end(c, cycle_dur, fails);
 }
 
 // ---- pods of a node in name order (wave ballot over pod indices) ---------------------------------
@@ -1735,7 +1897,10 @@ K10S_HD void s_release(Ctx& c, uint32_t p) {  // release_node_resources (153-162
     node_bound_changed(c, (uint32_t)n);
 }
 
-K10S_HD void run_scheduling_cycle(Ctx& c, double t) { run_scheduling_cycle_t<false>(c, t); }
+K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
+    if (nc_packed(c) && c.P().score_weight == 1.0 && c.H().cyc_fails != 0) run_scheduling_cycle_tiles(c, t);
+    else run_scheduling_cycle_t<false>(c, t);
+}
 // A replica whose profile is not LeastAllocated alone (K10S_SCORE_PLUGINS builds only: the host
 // engine and k10s_kernels_plugins.hip; compiled into the default kernel, the branch alone cost
 // 4.6 % at C3, profiles/r02_v4_score_plugins_ab.json).
@@ -3564,6 +3729,11 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
         }
     }
     K10S_PROF_ADD(c, PROF_LOOP, t_loop);
+#if K10S_DEVICE && K10S_BEACON
+    if (lane_id() == 0)   // word 12: the loop has exited (1 + launch-local event count)
+        __hip_atomic_store(k10s_beacon + (uint64_t)blockIdx.x * K10S_BEACON_WORDS + 12, (uint32_t)done + 1u,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
     h->counters[K10S_C_EVENTS] += done;
     if (h->error_code) status = K10S_REPLICA_ERROR;
     h->status = status;

@@ -113,6 +113,11 @@ __global__ K10S_RUN_BOUNDS void k10s_run_kernel(uint32_t n_replicas, int mode, d
 #endif
     __syncthreads();
     hdr_copy(hdr_global(r), (const uint32_t*)&k10s_hdr);
+#if K10S_BEACON
+    if (threadIdx.x == 0)   // word 13: the header is written back
+        __hip_atomic_store(k10s_beacon + (uint64_t)r * K10S_BEACON_WORDS + 13, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
     (void)active;   // the same pointer, read after the loop through the constant block
 #if K10S_DEVICE
     if (more && threadIdx.x == 0) atomicAdd(K10S_DC.active, 1u);

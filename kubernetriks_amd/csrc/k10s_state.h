@@ -261,7 +261,8 @@ struct RepHdr {
                                   // assignment request needs no read of it
     uint32_t ps_rm_n;             // pods storage dropped on a removal request (PS_REMOVE_POD_REQ): while
                                   // 0, every PodStartedRunning finds its pod in storage (below)
-    uint32_t pad_h2;
+    uint32_t cyc_fails;           // attempts of the previous scheduling cycle that found no node: the cycle
+                                  // runs the batched fit pass (k10s_engine.h fit_tile) only after one
     HeapEv fq_win[K10S_NFQ * K10S_FQW];
     HeapEv heap_lds[K10S_HEAP_TOP];
 #if K10S_AQ_TOP
