@@ -75,6 +75,7 @@ def parse():
     ap.add_argument("--cpu-workers", type=int, default=0, help="0 = the usable host cores (cgroup quota / affinity)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scan-kernel", action="store_true", help="skip the scheduling-kernel-alone measurement")
+    ap.add_argument("--backlog-steps", type=int, default=3, help="timed launches of the backlog side line")
     ap.add_argument("--no-backlog-line", action="store_true",
                     help="skip the one-launch c3_backlog measurement reported beside a c3 run")
     ap.add_argument("--pruned-scan", action="store_true", help="exact block-bound pruned scan (DESIGN.md §3)")
@@ -83,6 +84,7 @@ def parse():
     ap.add_argument("--score-plugins", choices=("least", "most", "both"), default="least",
                     help="score plugins of every replica (k10s_replica_params.score_plugins): LeastAllocated "
                          "(the reference's only one), MostAllocated (extension), or both (weights 1 and 1)")
+    ap.add_argument("--replica-rows", action="store_true", help="add every replica's counters/estimators (tests)")
     ap.add_argument("--profile", action="store_true", help="print the K10S_PROF cycle attribution (variant builds)")
     ap.add_argument("--selftest-host", action="store_true",
                     help="TEST ONLY: run the launcher and the cross-rank reduction on CPU (gloo) over the "
@@ -213,6 +215,31 @@ def pmc_traffic(workload, R, nodes, pods, pruned, score_plugins, engine):
             pm.get("score_plugins", "least") == score_plugins:
         return pm.get("hbm_bytes_per_launch")
     return None
+
+
+def roofline(entry_b, extra_b, scanned, nread, attempts, placements, launches, kernel_ms, traffic):
+    """The `roofline` object of k10s_run_kernel, per launch.  `achieved` / `frac` count the bytes the
+    kernel reads and writes for the scans: per node-cache entry READ (nodes_read: every scanned node,
+    plus the cycle tiles' shared fit passes, whose failed attempts read no entry of their own) the
+    entry's size (8 B packed cpu << 40 | ram, 12 B wide u32 + u64; + 12 B of capacity for
+    MostAllocated), 12 B per attempt (the pod's request) and one entry per placement (the
+    reservation).  `survey_pricing` is SURVEY.md 8(d)'s algorithmic volume of the serial reference
+    (12 B per node per attempt, whether read or not) over the same time: a work rate, not a bandwidth
+    (it exceeds the HBM peak when the tiles skip the failed attempts' scans).  `traffic`: HBM bytes per
+    launch from the committed rocprofv3 PMC pass on this build, else None."""
+    sec = kernel_ms * 1e-3 if kernel_ms > 0 else float("inf")
+    read = ((entry_b + extra_b) * nread + 12.0 * attempts + entry_b * placements) / launches
+    survey = ((12.0 + extra_b) * scanned + 12.0 * attempts + 12.0 * placements) / launches
+    return {"bound": "hbm", "achieved": read / sec / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": read / sec / HBM_PEAK, "traffic": traffic,
+            "traffic_frac": (traffic / sec / HBM_PEAK) if traffic else None,
+            "kernel": "k10s_run_kernel", "kernel_ms_per_launch": kernel_ms,
+            "bytes_per_launch": read, "node_entry_bytes": int(entry_b),
+            "pricing": (f"bytes read: {int(entry_b + extra_b)} B per node-cache entry read (nodes_read) + 12 B per "
+                        f"attempt + {int(entry_b)} B per placement"),
+            "survey_pricing": {"bytes_per_launch": survey, "equivalent_GBps": survey / sec / 1e9,
+                               "note": "SURVEY.md 8(d): 12 B per node per attempt + 12 B per attempt + 12 B per "
+                                       "placement of the serial reference; a work rate, not a bandwidth"}}
 
 
 def build_workload(args):
@@ -358,23 +385,12 @@ def main():
     value = placements / elapsed
 
     # roofline for the dominant kernel (per launch, this rank's launch time, all-rank bytes / world)
-    # per scanned node: the node-cache entry (8 B packed cpu << 40 | ram, 12 B wide u32 + u64;
-    # k10s_capacities.node_cache); MostAllocated also reads the node's capacity (12 B, wide only).
-    # Per attempt the pod's request (12 B); per placement the entry's reservation write.
-    # `achieved` is priced as SURVEY.md §8(d) prices the algorithm: 12 B per scanned node (u32 cpu + u64
-    # ram of the reference's node cache), 12 B per attempt (the request), 12 B per placement; + 12 B of
-    # capacity per node for MostAllocated.  The packed node cache (8 B per node, cpu << 40 | ram) moves
-    # fewer bytes for the same work: that physical rate is reported beside it (`*_physical`).
-    entry_b = float(eng.node_entry_bytes)
-    extra_b = 0.0 if args.score_plugins == "least" else 12.0
-    per_launch_bytes = ((12.0 + extra_b) * scanned + 12.0 * attempts + 12.0 * placements) / (args.steps * world)
-    achieved = per_launch_bytes / (mean_kernel_ms * 1e-3) if mean_kernel_ms > 0 else 0.0
-    phys_bytes = ((entry_b + extra_b) * scanned + 12.0 * attempts + entry_b * placements) / (args.steps * world)
-    achieved_phys = phys_bytes / (mean_kernel_ms * 1e-3) if mean_kernel_ms > 0 else 0.0
-    # what the scans actually read (pruned scan: block bounds + scanned blocks + bound upkeep)
-    touched_bytes = ((entry_b + extra_b) * nread + 12.0 * attempts + entry_b * placements) / (args.steps * world)
     traffic = None if args.selftest_host else pmc_traffic(args.workload, R, args.nodes, args.pods, args.pruned_scan,
                                                             args.score_plugins, version())
+    roof = roofline(float(eng.node_entry_bytes), 0.0 if args.score_plugins == "least" else 12.0, scanned, nread,
+                    attempts, placements, args.steps * world, mean_kernel_ms, traffic)
+    roof["scan_mode"] = "pruned" if args.pruned_scan else "full"
+    entry_b = float(eng.node_entry_bytes)
     out = {
         "metric": METRIC,
         "value": value,
@@ -393,16 +409,7 @@ def main():
                    "replicas_per_gpu": R, "total_replicas": R * world, "nodes": args.nodes, "pods_per_replica": args.pods,
                    "score_plugins": args.score_plugins, "node_entry_bytes": int(entry_b),
                    "parallelism": f"replica-sharded x{world} (RCCL all-reduce of counters and histograms only)"},
-        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK, "traffic": traffic,
-                     "kernel": "k10s_run_kernel", "kernel_ms_per_launch": mean_kernel_ms,
-                     "algorithmic_bytes_per_launch": per_launch_bytes,
-                     "pricing": "SURVEY.md 8(d): 12 B per scanned node + 12 B per attempt + 12 B per placement",
-                     "node_entry_bytes": int(entry_b), "physical_bytes_per_launch": phys_bytes,
-                     "achieved_physical": achieved_phys / 1e9, "frac_physical": achieved_phys / HBM_PEAK,
-                     "scan_mode": "pruned" if args.pruned_scan else "full",
-                     "touched_bytes_per_launch": touched_bytes,
-                     "touched_GBps": touched_bytes / (mean_kernel_ms * 1e-3) / 1e9 if mean_kernel_ms > 0 else 0.0},
+        "roofline": roof,
         "engine": version(),
         "rates": {"placements_per_s": value, "attempts_per_s": attempts / elapsed, "events_per_s": events / elapsed},
         "totals": {"placements": placements, "attempts": attempts, "events": events, "nodes_scanned": scanned,
@@ -414,6 +421,10 @@ def main():
                                                                        "events")},
                      "timings": summary["timings"], "histograms": summary.get("histograms")},
     }
+    if args.replica_rows:   # per-replica fingerprints in global replica order (tests of the rank sharding)
+        rc, re_, rs = ensemble.gather_rows(eng.raw_results())
+        out["replica_rows"] = {"counters": rc.tolist(), "estimators": re_.reshape(len(rc), -1).tolist(),
+                               "status": rs.tolist()}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args, cfg, cluster, workload, params)
@@ -474,28 +485,30 @@ def backlog_line(args, cfg, make_engine, caps, ensemble, num_counters, version):
     del probe
     params = ensemble.shard_params(defaults, args.replicas, 0, base_seed=123, perturb=True)
     eng = make_engine(scn, args.replicas, params=params, caps=caps, blob=blob)
+    steps, warmup = args.backlog_steps, 1
+    for _ in range(warmup):
+        eng.reset()
+        eng.run_until_all_finished(max_time=1e7)
+    c = np.zeros(num_counters, dtype=np.int64)
+    kms = []
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ms = eng.run_until_all_finished(max_time=1e7)
+    for _ in range(steps):
+        eng.reset()
+        kms.append(eng.run_until_all_finished(max_time=1e7))
+        c += eng.counter_matrix().sum(axis=0, dtype=np.uint64).astype(np.int64)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    c = eng.counter_matrix().sum(axis=0, dtype=np.uint64).astype(np.int64)
-    placements, attempts, scanned = int(c[12]), int(c[13]), int(c[15])
-    entry_b = float(eng.node_entry_bytes)
-    per_launch = 12.0 * scanned + 12.0 * attempts + 12.0 * placements   # SURVEY.md 8(d) pricing, as the headline
-    achieved = per_launch / (ms * 1e-3) if ms > 0 else 0.0
-    phys = entry_b * scanned + 12.0 * attempts + entry_b * placements
+    ms = sum(kms) / len(kms)
+    placements, attempts, scanned, nread = int(c[12]), int(c[13]), int(c[15]), int(c[16])
+    traffic = pmc_traffic("c3_backlog", args.replicas, args.nodes, args.pods, args.pruned_scan, "least", version())
+    roof = roofline(float(eng.node_entry_bytes), 0.0, scanned, nread, attempts, placements, steps, ms, traffic)
     log(f"backlog: {placements / elapsed / 1e6:.2f} M placements/s, run {ms:.1f} ms")
-    return {"workload": desc, "workload_name": "c3_backlog", "steps": 1, "warmup": 0,
+    return {"workload": desc, "workload_name": "c3_backlog", "steps": steps, "warmup": warmup,
             "placements_per_s": placements / elapsed, "attempts_per_s": attempts / elapsed,
-            "ms_per_step": elapsed * 1e3, "kernel_ms_per_launch": ms,
-            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK, "algorithmic_bytes_per_launch": per_launch,
-                         "node_entry_bytes": int(entry_b), "physical_bytes_per_launch": phys,
-                         "frac_physical": (phys / (ms * 1e-3) if ms > 0 else 0.0) / HBM_PEAK,
-                         "traffic": pmc_traffic("c3_backlog", args.replicas, args.nodes, args.pods, args.pruned_scan,
-                                                "least", version())},
-            "totals": {"placements": placements, "attempts": attempts, "requeued": int(c[17]), "flushed": int(c[18])},
+            "ms_per_step": elapsed * 1e3 / steps, "kernel_ms_per_launch": ms, "roofline": roof,
+            "totals": {"placements": placements, "attempts": attempts, "nodes_scanned": scanned, "nodes_read": nread,
+                       "requeued": int(c[17]), "flushed": int(c[18])},
             "engine": version()}
 
 

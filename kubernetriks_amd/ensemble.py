@@ -93,6 +93,16 @@ def ensemble_summary(raw_results: Sequence, group=None, force: bool = False) -> 
     return s
 
 
+def gather_rows(raw_results: Sequence, group=None):
+    """(counters int64 [R_job, NUM_COUNTERS], estimators f64 [R_job, len(EST_NAMES), 5], status int64 [R_job])
+    of every replica of the job in global replica order (all ranks when torch.distributed is
+    initialised): per-replica fingerprints, e.g. to check that rank g ran sweep cells [g·R, (g+1)·R)."""
+    cnt, est, st = _rows(raw_results)
+    if _collective(group, False):
+        cnt, est, st = _gather(cnt, group), _gather(est, group), _gather(st, group)
+    return cnt, est, st
+
+
 def histogram_sum(raw_results):
     """(len(EST_NAMES), HIST_BINS) int64: the replicas' estimator histograms summed."""
     import numpy as np

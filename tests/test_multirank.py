@@ -145,6 +145,25 @@ def test_bench_gpus_2_launches_two_ranks():
     assert two["totals"]["replica_status"] == one["totals"]["replica_status"] == {"1": 4}
 
 
+def test_bench_gpus_4_c5_sweep_cells_match_one_rank():
+    """bench.py --gpus 4 --workload c5 (4 gloo ranks x 2 replicas, the host-check engine): rank g runs
+    sweep cells [2g, 2g + 2) of workloads.c5_params (ensemble.shard_params(sweep=True)), so the job's
+    per-replica rows in global order equal one rank running cells 0..7, replica by replica."""
+    common = ["--selftest-host", "--workload", "c5", "--nodes", "48", "--pods", "90", "--arrival-window", "50",
+              "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--replica-rows"]
+    p4 = _bench(["--gpus", "4", "--replicas", "2", *common])
+    assert p4.returncode == 0, p4.stderr[-2000:]
+    four = json.loads([x for x in p4.stdout.splitlines() if x.startswith("{")][0])
+    assert four["n_gpus"] == 4 and four["config"]["total_replicas"] == 8
+    p1 = _bench(["--gpus", "1", "--replicas", "8", *common])
+    assert p1.returncode == 0, p1.stderr[-2000:]
+    one = json.loads([x for x in p1.stdout.splitlines() if x.startswith("{")][0])
+    assert four["replica_rows"] == one["replica_rows"]
+    rows = one["replica_rows"]["counters"]
+    assert len(rows) == 8 and len({tuple(r) for r in rows}) > 1   # the cells differ
+    assert four["totals"]["events"] == one["totals"]["events"] > 0
+
+
 def test_bench_world_size_mismatch_fails():
     p = _bench(["--gpus", "2", "--selftest-host", "--replicas", "1", "--nodes", "8", "--pods", "4", "--steps", "1",
                 "--warmup", "0", "--no-cpu-baseline"], {"WORLD_SIZE": "1", "RANK": "0"})
