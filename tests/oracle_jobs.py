@@ -26,11 +26,25 @@ def replay(scenario: str, max_time: float = 1e7) -> dict:
     return od
 
 
+def _usable_cores() -> int:
+    """The cgroup CPU quota when there is one (16 on the GPU box, whose os.cpu_count() shows the whole
+    machine), else the affinity set."""
+    import math
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(math.ceil(int(q) / int(period)))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def replay_many(scenarios, max_time: float = 1e7, workers: int = 0):
     """Oracle results for several scenarios, in order, over a spawned process pool."""
     import multiprocessing as mp
     from concurrent.futures import ProcessPoolExecutor
-    n = workers or min(len(scenarios), 8, os.cpu_count() or 1)
+    n = workers or min(len(scenarios), 16, _usable_cores())
     if n <= 1:
         return [replay(s, max_time) for s in scenarios]
     with ProcessPoolExecutor(max_workers=n, mp_context=mp.get_context("spawn")) as ex:

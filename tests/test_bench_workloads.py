@@ -1,7 +1,7 @@
 """The exact workloads bench.py measures, oracle-checked: the same traces, the same
 bulk scenario path (scenario_bulk + k10s_engine_create_bulk), the same replica count and the same
 per-replica parameters (ensemble.shard_params at the bench seed), with bit-exact oracle replays of
-replicas at the start, middle and end of the batch.  Only the result logs differ from bench.py's
+replicas spread over the batch (32 by hash, the first and last, and the fewest- and most-event ones).  Only the result logs differ from bench.py's
 engine (placements and pod records are kept here so they can be compared); they do not change
 what a replica simulates."""
 import pytest
@@ -13,7 +13,18 @@ from kubernetriks_amd import workloads as wl
 from kubernetriks_amd.scenario import SimulationConfig, scenario_bulk
 
 R, NODES, PODS, WINDOW = 8192, 4096, 16384, 1200.0   # bench.py defaults
-CHECK = [0, 4095, 8191]
+CHECK = 32   # replicas replayed per batch, chosen by hash across it (+ the edges and the event-count extremes)
+
+
+def pick(res, k: int):
+    """k replicas spread over the batch by a hash of their index, plus the first and last replica and
+    the replicas with the fewest and the most delivered events."""
+    import hashlib
+    n = len(res)
+    chosen = sorted(range(n), key=lambda r: hashlib.sha1(f"k10s-replay-{r}".encode()).hexdigest())[:k]
+    ev = [x["counters"]["events"] for x in res]
+    chosen += [0, n - 1, ev.index(min(ev)), ev.index(max(ev))]
+    return sorted(set(chosen))
 
 
 def _bench_batch(cluster, workload, check, score_plugins=1):
@@ -30,10 +41,12 @@ def _bench_batch(cluster, workload, check, score_plugins=1):
     caps.placement_log = PODS + 1024
     eng = Engine(scn, R, params=params, caps=caps, pods_blob=blob)
     eng.run_until_all_finished(1e7)
+    res = eng.results()
+    if isinstance(check, int):
+        check = pick(res, check)
     ods = oracle_jobs.replay_many([wl.replica_scenario(cfg, cluster, workload, params[r]) for r in check], 1e7)
     for r, od in zip(check, ods):
         assert parity.compare(od, eng, r=r, log=False) == [], r
-    res = eng.results()
     assert all(x["status"] == "finished" for x in res)
     return res
 

@@ -28,7 +28,8 @@ def engine_cls(backend):
     return Engine
 
 
-def _batch_parity(backend, parts, params_fn, R, check, mode=RUN_UNTIL_ALL_FINISHED, until=0.0, max_time=1e6):
+def _batch_parity(backend, parts, params_fn, R, check, mode=RUN_UNTIL_ALL_FINISHED, until=0.0, max_time=1e6,
+                  parallel=False):
     cfg, c, w = parts
     E = engine_cls(backend)
     probe = E(scenario_text(cfg, c, w), 1)
@@ -38,6 +39,12 @@ def _batch_parity(backend, parts, params_fn, R, check, mode=RUN_UNTIL_ALL_FINISH
         eng.run_until_all_finished(max_time)
     else:
         eng.step_until_time(until)
+    if parallel and mode == RUN_UNTIL_ALL_FINISHED:
+        import oracle_jobs
+        ods = oracle_jobs.replay_many([wl.replica_scenario(cfg, c, w, params[r]) for r in check], max_time)
+        for r, od in zip(check, ods):
+            assert parity.compare(od, eng, r=r, log=False) == [], r
+        return eng
     for r in check:
         o = ob.OracleSim(wl.replica_scenario(cfg, c, w, params[r]))
         st = o.run_until_all_finished(max_time) if mode == RUN_UNTIL_ALL_FINISHED else o.step_until_time(until)
@@ -138,8 +145,10 @@ def test_c5_sweep_at_baseline_size_gpu():
     """One GPU's share of the 65,536-replica sweep (8,192 replicas) on 4,096-node clusters."""
     R = 8192
     parts = (wl.SimulationConfig(),) + wl.c3_traces(n_nodes=4096, n_pods=600, arrival_window=200.0, seed=11)
+    # one replica of every (cycle interval x conditional move x delays x CA threshold) cell: replicas
+    # 0..71 (workloads.c5_params), replayed in parallel, plus the batch's far end
     eng = _batch_parity("gpu", parts, lambda d, n: wl.c5_params(d, n, base_seed=123), R,
-                        check=[0, 7, 4095, 8191])
+                        check=list(range(72)) + [4095, 8191], parallel=True)
     res = eng.results()
     assert all(r["status"] == "finished" for r in res)
     _identity(res)
