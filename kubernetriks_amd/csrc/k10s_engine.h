@@ -340,10 +340,49 @@ typedef const HeapEv* EvRef;
 #define K10S_EVREF(x) ((EvRef)(x))
 #endif
 #define K10S_EVARG EvRef ep
+// K10S_LAZY_EV (A/B knob): the handler reads each field of the event where a case uses it (an LDS read
+// and its readfirstlanes at the use) instead of all eight fields up front.
+#ifndef K10S_LAZY_EV
+#define K10S_LAZY_EV 0
+#endif
+#if K10S_LAZY_EV && K10S_DEVICE
+struct EvLazy {
+    EvRef ep;
+    struct U32 {
+        const __attribute__((address_space(3))) uint32_t* p;
+        K10S_D operator uint32_t() const { return uniform_u32(*p); }
+    };
+    struct F64 {
+        const __attribute__((address_space(3))) double* p;
+        K10S_D operator double() const { return uniform_f64(*p); }
+    };
+    struct Kind {
+        const __attribute__((address_space(3))) uint32_t* p;
+        K10S_D operator uint32_t() const { return uniform_u32(*p) & 0xFFFFu; }
+    };
+    struct Slot {
+        const __attribute__((address_space(3))) uint32_t* p;
+        K10S_D operator int32_t() const { return (int32_t)(int16_t)(uniform_u32(*p) >> 16); }
+    };
+    F64 time;
+    U32 seq;
+    Kind kind;
+    Slot slot;
+    U32 a, b;
+    F64 x;
+    K10S_D explicit EvLazy(EvRef e)
+        : ep(e), time{&e->time}, seq{&e->seq}, kind{(const __attribute__((address_space(3))) uint32_t*)&e->kind},
+          slot{(const __attribute__((address_space(3))) uint32_t*)&e->kind}, a{&e->a}, b{&e->b}, x{&e->x} {}
+};
+#define K10S_EV_PROLOGUE                     \
+    if (!K10S_FULL_WAVE(XG_HANDLER)) return; \
+    const EvLazy e(ep)
+#else
 #define K10S_EV_PROLOGUE                     \
     if (!K10S_FULL_WAVE(XG_HANDLER)) return; \
     HeapEv e = *ep;                          \
     uniform_event(e)
+#endif
 
 // ---- cycle attribution (K10S_PROF builds: tooling only, semantics-neutral) ----------------------
 // s_memtime deltas per loop phase, accumulated in RepHdr::prof and read by k10s_engine_profile.
@@ -480,6 +519,17 @@ enum { HS_EVENTS, HS_FIFO_POP, HS_REFILL, HS_HEAP_POP, HS_TRACE_POP, HS_SL_FAST,
        HS_EMIT_RING, HS_EMIT_HEAP, HS_SL_DIRTY, HS_SCANS, HS_REFILL_CLS0 = 12, HS_POP_CLS0 = 20, HS_AQ_HBM_GET = 28, HS_AQ_POP = 29, HS_SLPOS0 = 32 };
 // An emission changed source q's head: mark it for the source list.
 K10S_HD void sl_mark(RepHdr& H, uint32_t q) { H.sl_dirty |= 1u << q; }
+// K10S_TERM_BIT (A/B knob): the termination rule's "every trace pod terminated" test rides on the
+// source list's dirty word, which the loop reads at every event anyway: bit 31 is set (sticky) once
+// pods_left drops to 0, so the loop reads no separate header field for it.
+#ifndef K10S_TERM_BIT
+#define K10S_TERM_BIT 0
+#endif
+#define K10S_SL_TERM 0x80000000u
+K10S_HD void pods_left_dec(RepHdr& H) {
+    H.pods_left -= 1;
+    if (K10S_TERM_BIT && H.pods_left <= 0) H.sl_dirty |= K10S_SL_TERM;
+}
 
 K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uint32_t a, uint32_t b, double x,
                           int cls = FQ_HEAP) {
@@ -2660,7 +2710,7 @@ K10S_WARM void on_api_server(Ctx& c, K10S_EVARG) {
         break;
     case K10S_EV_AS_POD_FINISHED:
         h->counters[K10S_C_TERMINATED_PODS] += 1;
-        h->pods_left -= 1;
+        pods_left_dec(*h);
         h->counters[K10S_C_PODS_SUCCEEDED] += 1;
         h->g_cur_pods -= 1;  // api_server.rs:262-265
         emit(c, K10S_EV_PS_POD_FINISHED, pr->as_to_ps_network_delay, -1, e.a, e.b, e.x, FQ_AS_TO_PS);
@@ -2725,7 +2775,7 @@ K10S_WARM void on_api_server(Ctx& c, K10S_EVARG) {
     case K10S_EV_AS_POD_REMOVED:
         if (e.b) {
             h->counters[K10S_C_TERMINATED_PODS] += 1;
-            h->pods_left -= 1;
+            pods_left_dec(*h);
             h->counters[K10S_C_PODS_REMOVED] += 1;
             h->g_cur_pods -= 1;  // api_server.rs:388-391
         }
@@ -3355,10 +3405,10 @@ K10S_HD void sl_refresh(Ctx& c, uint32_t q, uint32_t ntr) {
     sl_update(c, q, has, uniform_u64((uint64_t)k), uniform_u32(s));
 }
 // Apply the head changes emissions made since the last update.
-K10S_HD void sl_apply_dirty(Ctx& c, uint32_t ntr) {
-    uint32_t d = uniform_u32(c.H().sl_dirty);
+K10S_HD void sl_apply_dirty(Ctx& c, uint32_t ntr, uint32_t d) {
+    d &= ~K10S_SL_TERM;
     if (!d) return;
-    c.H().sl_dirty = 0;
+    c.H().sl_dirty &= K10S_SL_TERM;
     do {
         const uint32_t q = (uint32_t)__builtin_ctz(d);
         d &= d - 1;
@@ -3369,7 +3419,7 @@ K10S_HD void sl_apply_dirty(Ctx& c, uint32_t ntr) {
 // Build the list from scratch (start of a launch: the header may come from anywhere).
 K10S_HD void sl_rebuild(Ctx& c, uint32_t ntr) {
     c.H().sl_n = 0;
-    c.H().sl_dirty = 0;
+    c.H().sl_dirty = (K10S_TERM_BIT && c.H().pods_left <= 0) ? K10S_SL_TERM : 0u;
     for (uint32_t q = 0; q < (uint32_t)K10S_NSRC; q++) sl_refresh(c, q, ntr);
 }
 
@@ -3578,7 +3628,9 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
     sl_rebuild(c, ntr);  // the sorted source list, from the sources' heads
     [[maybe_unused]] uint32_t it_stale = 0;
     while (!h->error_code) {
-        if (!until_mode() && h->pods_left <= 0 && is_multiple_of_1000(h->clock)) {
+        const uint32_t dirty = uniform_u32(h->sl_dirty);
+        if (!until_mode() && (K10S_TERM_BIT ? (dirty & K10S_SL_TERM) != 0 : h->pods_left <= 0) &&
+            is_multiple_of_1000(h->clock)) {
             status = K10S_REPLICA_FINISHED;
             break;
         }
@@ -3588,7 +3640,7 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
         int src = 0;
         bool have = false;
         const uint64_t t_sel = prof_now();
-        sl_apply_dirty(c, ntr);
+        sl_apply_dirty(c, ntr, dirty);
         EvRef ep = K10S_EVREF(&h->heap_top);
         for (;;) {
             if (uniform_u32(h->sl_n) == 0) break;
