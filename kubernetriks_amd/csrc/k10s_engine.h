@@ -1241,6 +1241,29 @@ K10S_D uint32_t screen_grp(const ScanGrp& g, uint32_t bits, uint32_t rc, uint64_
                          ((uint32_t)(l23.y > r23.y) << 3);
     return fit & ~out;
 }
+// K10S_SCREEN_MASKS (A/B knob): screen_grp's decisions as four lane masks (compares into SGPR pairs,
+// combined on the scalar unit) instead of a per-lane 4-bit integer built with v_cndmask / v_or.
+#ifndef K10S_SCREEN_MASKS
+#define K10S_SCREEN_MASKS 0
+#endif
+K10S_D void screen_grp_masks(const ScanGrp& g, uint32_t rc, uint64_t rr, float fa, float fr, float T, bool& k0,
+                             bool& k1, bool& k2, bool& k3) {
+    const f32x2 A01 = {cvt_f32_u32(g.cv.x), cvt_f32_u32(g.cv.y)};
+    const f32x2 A23 = {cvt_f32_u32(g.cv.z), cvt_f32_u32(g.cv.w)};
+    const f32x2 H01 = {cvt_f32_u32((uint32_t)(g.r01.x >> 32)), cvt_f32_u32((uint32_t)(g.r01.y >> 32))};
+    const f32x2 H23 = {cvt_f32_u32((uint32_t)(g.r23.x >> 32)), cvt_f32_u32((uint32_t)(g.r23.y >> 32))};
+    const f32x2 L01 = {cvt_f32_u32((uint32_t)g.r01.x), cvt_f32_u32((uint32_t)g.r01.y)};
+    const f32x2 L23 = {cvt_f32_u32((uint32_t)g.r23.x), cvt_f32_u32((uint32_t)g.r23.y)};
+    const f32x2 two32 = {4294967296.0f, 4294967296.0f};
+    const f32x2 R01 = __builtin_elementwise_fma(H01, two32, L01), R23 = __builtin_elementwise_fma(H23, two32, L23);
+    const f32x2 va = {fa, fa}, vr = {fr, fr}, vT = {T, T};
+    const f32x2 l01 = __builtin_elementwise_fma(va, R01, vr * A01), l23 = __builtin_elementwise_fma(va, R23, vr * A23);
+    const f32x2 r01 = (A01 * R01) * vT, r23 = (A23 * R23) * vT;
+    k0 = rc <= g.cv.x && rr <= g.r01.x && !(l01.x > r01.x);
+    k1 = rc <= g.cv.y && rr <= g.r01.y && !(l01.y > r01.y);
+    k2 = rc <= g.cv.z && rr <= g.r23.x && !(l23.x > r23.x);
+    k3 = rc <= g.cv.w && rr <= g.r23.y && !(l23.y > r23.y);
+}
 // A fitting node the screen did not rule out: the lane best's allocatables take the index (same
 // score), anything else is scored exactly (as scan_node_d).
 K10S_D void score_node_exact(uint32_t n, uint32_t ac, uint64_t ar, uint64_t rr, double frc, double frr, double& best_s,
@@ -1298,6 +1321,27 @@ K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, cons
     float T = __builtin_inff();  // thr + eps: +inf screens nothing out (the first step)
     // one 256-node step of a lane's group g at n0 (screen, exact scores, threshold)
     auto step = [&](const ScanGrp& g, uint32_t n0, auto full) {
+#if K10S_SCREEN_MASKS
+        // the same tests, each node's decision kept as a lane mask (no per-lane bit packing)
+        bool k0, k1, k2, k3;
+        screen_grp_masks(g, rc, rr, fa, fr, T, k0, k1, k2, k3);
+        if (!decltype(full)::value) {
+            const uint32_t bits = grp_bits(g, n0, n_nodes);
+            k0 = k0 && (bits & 1u);
+            k1 = k1 && (bits & 2u);
+            k2 = k2 && (bits & 4u);
+            k3 = k3 && (bits & 8u);
+        }
+        if (k0) score_node_exact(n0, g.cv.x, g.r01.x, rr, frc, frr, best_s, best_n, la, lr, lu);
+        if (k1) score_node_exact(n0 + 1, g.cv.y, g.r01.y, rr, frc, frr, best_s, best_n, la, lr, lu);
+        if (k2) score_node_exact(n0 + 2, g.cv.z, g.r23.x, rr, frc, frr, best_s, best_n, la, lr, lu);
+        if (k3) score_node_exact(n0 + 3, g.cv.w, g.r23.y, rr, frc, frr, best_s, best_n, la, lr, lu);
+        if (__ballot(k0 || k1 || k2 || k3)) {
+            const float thr = __builtin_bit_cast(float, uniform_u32(__builtin_bit_cast(uint32_t, wave_min_f32(lu))));
+            T = thr + K10S_SCREEN_EPS;
+        }
+        return;
+#endif
         const uint32_t bits = decltype(full)::value ? 0xFu : grp_bits(g, n0, n_nodes);
         const uint32_t need = screen_grp(g, bits, rc, rr, fa, fr, T);
         if (need) {
