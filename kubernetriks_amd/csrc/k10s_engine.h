@@ -340,12 +340,10 @@ typedef const HeapEv* EvRef;
 #define K10S_EVREF(x) ((EvRef)(x))
 #endif
 #define K10S_EVARG EvRef ep
-// K10S_LAZY_EV (A/B knob): the handler reads each field of the event where a case uses it (an LDS read
-// and its readfirstlanes at the use) instead of all eight fields up front.
-#ifndef K10S_LAZY_EV
-#define K10S_LAZY_EV 0
-#endif
-#if K10S_LAZY_EV && K10S_DEVICE
+// Device: a handler reads each field of its event where a case uses it (an LDS read and its
+// readfirstlanes at the use) instead of all eight fields up front: C3 1,215 -> 1,203 ms
+// (profiles/r04_t1_ab.json).
+#if K10S_DEVICE
 struct EvLazy {
     EvRef ep;
     struct U32 {
@@ -519,17 +517,7 @@ enum { HS_EVENTS, HS_FIFO_POP, HS_REFILL, HS_HEAP_POP, HS_TRACE_POP, HS_SL_FAST,
        HS_EMIT_RING, HS_EMIT_HEAP, HS_SL_DIRTY, HS_SCANS, HS_REFILL_CLS0 = 12, HS_POP_CLS0 = 20, HS_AQ_HBM_GET = 28, HS_AQ_POP = 29, HS_SLPOS0 = 32 };
 // An emission changed source q's head: mark it for the source list.
 K10S_HD void sl_mark(RepHdr& H, uint32_t q) { H.sl_dirty |= 1u << q; }
-// K10S_TERM_BIT (A/B knob): the termination rule's "every trace pod terminated" test rides on the
-// source list's dirty word, which the loop reads at every event anyway: bit 31 is set (sticky) once
-// pods_left drops to 0, so the loop reads no separate header field for it.
-#ifndef K10S_TERM_BIT
-#define K10S_TERM_BIT 0
-#endif
-#define K10S_SL_TERM 0x80000000u
-K10S_HD void pods_left_dec(RepHdr& H) {
-    H.pods_left -= 1;
-    if (K10S_TERM_BIT && H.pods_left <= 0) H.sl_dirty |= K10S_SL_TERM;
-}
+K10S_HD void pods_left_dec(RepHdr& H) { H.pods_left -= 1; }
 
 K10S_HELPER uint32_t emit(Ctx& c, uint32_t kind, double delay, int32_t slot, uint32_t a, uint32_t b, double x,
                           int cls = FQ_HEAP) {
@@ -1241,29 +1229,6 @@ K10S_D uint32_t screen_grp(const ScanGrp& g, uint32_t bits, uint32_t rc, uint64_
                          ((uint32_t)(l23.y > r23.y) << 3);
     return fit & ~out;
 }
-// K10S_SCREEN_MASKS (A/B knob): screen_grp's decisions as four lane masks (compares into SGPR pairs,
-// combined on the scalar unit) instead of a per-lane 4-bit integer built with v_cndmask / v_or.
-#ifndef K10S_SCREEN_MASKS
-#define K10S_SCREEN_MASKS 0
-#endif
-K10S_D void screen_grp_masks(const ScanGrp& g, uint32_t rc, uint64_t rr, float fa, float fr, float T, bool& k0,
-                             bool& k1, bool& k2, bool& k3) {
-    const f32x2 A01 = {cvt_f32_u32(g.cv.x), cvt_f32_u32(g.cv.y)};
-    const f32x2 A23 = {cvt_f32_u32(g.cv.z), cvt_f32_u32(g.cv.w)};
-    const f32x2 H01 = {cvt_f32_u32((uint32_t)(g.r01.x >> 32)), cvt_f32_u32((uint32_t)(g.r01.y >> 32))};
-    const f32x2 H23 = {cvt_f32_u32((uint32_t)(g.r23.x >> 32)), cvt_f32_u32((uint32_t)(g.r23.y >> 32))};
-    const f32x2 L01 = {cvt_f32_u32((uint32_t)g.r01.x), cvt_f32_u32((uint32_t)g.r01.y)};
-    const f32x2 L23 = {cvt_f32_u32((uint32_t)g.r23.x), cvt_f32_u32((uint32_t)g.r23.y)};
-    const f32x2 two32 = {4294967296.0f, 4294967296.0f};
-    const f32x2 R01 = __builtin_elementwise_fma(H01, two32, L01), R23 = __builtin_elementwise_fma(H23, two32, L23);
-    const f32x2 va = {fa, fa}, vr = {fr, fr}, vT = {T, T};
-    const f32x2 l01 = __builtin_elementwise_fma(va, R01, vr * A01), l23 = __builtin_elementwise_fma(va, R23, vr * A23);
-    const f32x2 r01 = (A01 * R01) * vT, r23 = (A23 * R23) * vT;
-    k0 = rc <= g.cv.x && rr <= g.r01.x && !(l01.x > r01.x);
-    k1 = rc <= g.cv.y && rr <= g.r01.y && !(l01.y > r01.y);
-    k2 = rc <= g.cv.z && rr <= g.r23.x && !(l23.x > r23.x);
-    k3 = rc <= g.cv.w && rr <= g.r23.y && !(l23.y > r23.y);
-}
 // A fitting node the screen did not rule out: the lane best's allocatables take the index (same
 // score), anything else is scored exactly (as scan_node_d).
 K10S_D void score_node_exact(uint32_t n, uint32_t ac, uint64_t ar, uint64_t rr, double frc, double frr, double& best_s,
@@ -1321,27 +1286,6 @@ K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, cons
     float T = __builtin_inff();  // thr + eps: +inf screens nothing out (the first step)
     // one 256-node step of a lane's group g at n0 (screen, exact scores, threshold)
     auto step = [&](const ScanGrp& g, uint32_t n0, auto full) {
-#if K10S_SCREEN_MASKS
-        // the same tests, each node's decision kept as a lane mask (no per-lane bit packing)
-        bool k0, k1, k2, k3;
-        screen_grp_masks(g, rc, rr, fa, fr, T, k0, k1, k2, k3);
-        if (!decltype(full)::value) {
-            const uint32_t bits = grp_bits(g, n0, n_nodes);
-            k0 = k0 && (bits & 1u);
-            k1 = k1 && (bits & 2u);
-            k2 = k2 && (bits & 4u);
-            k3 = k3 && (bits & 8u);
-        }
-        if (k0) score_node_exact(n0, g.cv.x, g.r01.x, rr, frc, frr, best_s, best_n, la, lr, lu);
-        if (k1) score_node_exact(n0 + 1, g.cv.y, g.r01.y, rr, frc, frr, best_s, best_n, la, lr, lu);
-        if (k2) score_node_exact(n0 + 2, g.cv.z, g.r23.x, rr, frc, frr, best_s, best_n, la, lr, lu);
-        if (k3) score_node_exact(n0 + 3, g.cv.w, g.r23.y, rr, frc, frr, best_s, best_n, la, lr, lu);
-        if (__ballot(k0 || k1 || k2 || k3)) {
-            const float thr = __builtin_bit_cast(float, uniform_u32(__builtin_bit_cast(uint32_t, wave_min_f32(lu))));
-            T = thr + K10S_SCREEN_EPS;
-        }
-        return;
-#endif
         const uint32_t bits = decltype(full)::value ? 0xFu : grp_bits(g, n0, n_nodes);
         const uint32_t need = screen_grp(g, bits, rc, rr, fa, fr, T);
         if (need) {
@@ -3449,10 +3393,10 @@ K10S_HD void sl_refresh(Ctx& c, uint32_t q, uint32_t ntr) {
     sl_update(c, q, has, uniform_u64((uint64_t)k), uniform_u32(s));
 }
 // Apply the head changes emissions made since the last update.
-K10S_HD void sl_apply_dirty(Ctx& c, uint32_t ntr, uint32_t d) {
-    d &= ~K10S_SL_TERM;
+K10S_HD void sl_apply_dirty(Ctx& c, uint32_t ntr) {
+    uint32_t d = uniform_u32(c.H().sl_dirty);
     if (!d) return;
-    c.H().sl_dirty &= K10S_SL_TERM;
+    c.H().sl_dirty = 0;
     do {
         const uint32_t q = (uint32_t)__builtin_ctz(d);
         d &= d - 1;
@@ -3463,7 +3407,7 @@ K10S_HD void sl_apply_dirty(Ctx& c, uint32_t ntr, uint32_t d) {
 // Build the list from scratch (start of a launch: the header may come from anywhere).
 K10S_HD void sl_rebuild(Ctx& c, uint32_t ntr) {
     c.H().sl_n = 0;
-    c.H().sl_dirty = (K10S_TERM_BIT && c.H().pods_left <= 0) ? K10S_SL_TERM : 0u;
+    c.H().sl_dirty = 0;
     for (uint32_t q = 0; q < (uint32_t)K10S_NSRC; q++) sl_refresh(c, q, ntr);
 }
 
@@ -3672,9 +3616,7 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
     sl_rebuild(c, ntr);  // the sorted source list, from the sources' heads
     [[maybe_unused]] uint32_t it_stale = 0;
     while (!h->error_code) {
-        const uint32_t dirty = uniform_u32(h->sl_dirty);
-        if (!until_mode() && (K10S_TERM_BIT ? (dirty & K10S_SL_TERM) != 0 : h->pods_left <= 0) &&
-            is_multiple_of_1000(h->clock)) {
+        if (!until_mode() && h->pods_left <= 0 && is_multiple_of_1000(h->clock)) {
             status = K10S_REPLICA_FINISHED;
             break;
         }
@@ -3684,7 +3626,7 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
         int src = 0;
         bool have = false;
         const uint64_t t_sel = prof_now();
-        sl_apply_dirty(c, ntr, dirty);
+        sl_apply_dirty(c, ntr);
         EvRef ep = K10S_EVREF(&h->heap_top);
         for (;;) {
             if (uniform_u32(h->sl_n) == 0) break;
