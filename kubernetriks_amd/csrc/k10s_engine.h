@@ -3594,6 +3594,18 @@ K10S_HD void fair_priority(uint64_t done) {
     (void)done;
 #endif
 }
+// Drop the heap's head, a lazily canceled pod finish, and move the heap's source-list entry to its
+// new head.  Out of line on purpose: inlined into the selection loop below, sl_update's lane-0
+// store (`has && lane == 0`) was threaded into the loop's back edge in the K10S_PROF build, which
+// the structurizer then compiled as a divergent loop (exec-masked flow blocks around heap_pop); the
+// first stale skip of c5_autoscaled replica 53 never left it.  A
+// call keeps every lane-divergent branch of the skip inside the callee, so the selection loop has
+// only uniform (scalar) branches in every build.
+K10S_HD_NOINL void drop_stale_head(Ctx& c, uint32_t ntr) {
+    c.H().stale_fin -= 1;
+    heap_pop(c);
+    sl_refresh(c, SRC_HEAP, ntr);
+}
 // Returns 1 if the replica still has work (event budget exhausted), else 0.  The working header
 // c.H() is LDS on the device (staged by the kernel) and the replica's header in place on the host.
 K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, uint64_t budget) {
@@ -3655,10 +3667,8 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
                 e.time = uniform_f64(h->heap_top.time);
                 // canceled (lazy cancel): only while some canceled finish is pending is the pod read
                 if (e.kind == K10S_EV_N_POD_FINISHED && uniform_u32(h->stale_fin) != 0 &&
-                    c.V().pod(e.a).finish_seq != e.seq) {
-                    h->stale_fin -= 1;
-                    heap_pop(c);
-                    sl_refresh(c, SRC_HEAP, ntr);
+                    uniform_u32(c.V().pod(e.a).finish_seq) != e.seq) {
+                    drop_stale_head(c, ntr);
                     if (K10S_LOOP_CAP(it_stale, 1u << 24, XG_LOOP_STALE)) break;
                     continue;
                 }
