@@ -51,6 +51,23 @@ def main():
         der["lds_bank_conflict_rate"] = per.get("SQ_LDS_BANK_CONFLICT", 0.0) / per["SQ_LDS_IDX_ACTIVE"]
     if "TCC_HIT_sum" in per and "TCC_MISS_sum" in per:
         der["l2_hit_rate"] = per["TCC_HIT_sum"] / (per["TCC_HIT_sum"] + per["TCC_MISS_sum"])
+    if per.get("TCC_EA0_RDREQ_sum"):
+        # memory-side read requests of the L2 that target DRAM (HBM or the Infinity Cache in front of
+        # it: the MALL sits on the memory side, so the L2 counters cannot split its hits from HBM)
+        der["dram_share_of_l2_read_requests"] = per.get("TCC_EA0_RDREQ_DRAM_sum", 0.0) / per["TCC_EA0_RDREQ_sum"]
+    if "FETCH_SIZE" in per:
+        der["memory_read_bytes_fetch_x2"] = 2.0 * per["FETCH_SIZE"] * 1024.0   # gfx950: FETCH_SIZE is half
+    if "WRITE_SIZE" in per:
+        der["memory_write_bytes"] = per["WRITE_SIZE"] * 1024.0
+    if "FETCH_SIZE" in per and "WRITE_SIZE" in per and kns:
+        tot = der["memory_read_bytes_fetch_x2"] + der["memory_write_bytes"]
+        der["memory_bytes_per_launch"] = tot
+        der["memory_TBps"] = tot / kns / 1e3
+        der["memory_frac_of_8TBps"] = tot / kns / 8e3
+        if events:
+            der["memory_bytes_per_event"] = tot / events
+    if "SQ_INSTS_VMEM" in per and events:
+        der["vmem_insts_per_event"] = per["SQ_INSTS_VMEM"] / events
     if events:
         for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_SMEM"):
             if k in per:
