@@ -65,7 +65,7 @@ __device__ uint32_t* k10s_beacon;   // [replica][K10S_BEACON_WORDS], host-mapped
 enum : uint32_t {
     XG_HEAP_POP = 1, XG_HEAP_MIN_CHILD, XG_HEAP_MIN_CHILD_EV, XG_SCHEDULE_SCAN, XG_SL_UPDATE, XG_FQ_REFILL,
     XG_PODS_IN_ORDER, XG_FOR_EACH_BIT, XG_CA_FIRST_FIT, XG_CA_SORT, XG_DISPATCH, XG_CYCLE, XG_GAUGE, XG_CACHE_FITS,
-    XG_FAIR, XG_HANDLER, XG_EMIT, XG_SCAN_PLUGINS,
+    XG_FAIR, XG_HANDLER, XG_EMIT, XG_SCAN_PLUGINS, XG_AQ_DRAIN,
     XG_LOOP_HEAP_POP = 0x40, XG_LOOP_EMIT, XG_LOOP_AQ_POP, XG_LOOP_AQ_UP, XG_LOOP_STALE,
 };
 #if K10S_DEVICE && K10S_EXEC_CHECK
@@ -815,13 +815,15 @@ K10S_HD uint32_t aq_sift_up(Ctx& c, uint32_t start, uint32_t pos, const QInfo& e
     aq_put(c, pos, elem);
     return pos;
 }
+// The action queue between two cycles is a push log (aq_drain below): a push appends.
 K10S_HELPER void aq_push(Ctx& c, const QInfo& q) {
     if (c.H().aq_size >= c.Ly().cap_aq) {
         fail(c, K10S_ERR_QUEUE_FULL);
         return;
     }
-    uint32_t old = c.H().aq_size++;
-    aq_sift_up(c, 0, old, q);
+    const uint32_t pos = uniform_u32(c.H().aq_size);
+    c.H().aq_size = pos + 1;
+    aq_put(c, pos, q);
 }
 // (Round 3 tried reading the 3-level subtree under the walk's position in one round trip below the
 // LDS levels: C3 +0.6 %, backlog -2 to -4 % from the extra SGPRs live in the scheduling cycle,
@@ -853,6 +855,121 @@ K10S_HELPER QInfo aq_pop(Ctx& c) {
     }
     aq_sift_up(c, 0, pos, item);
     return top;
+}
+
+// ---- the cycle's pop sequence, fixed when the cycle starts ----------------------------------------
+// Only the scheduling cycle pops the action queue, it pops until the queue is empty
+// (scheduler.rs:261-330, `while let Some(..) = self.action_queue.pop()`), and nothing is pushed while
+// it runs (a failed pod goes to the unschedulable map, every emission to the event queue).  So between
+// two cycles the BinaryHeap is built from empty by a sequence of pushes, and a cycle's pops are a
+// sequence known when it starts.  The queue therefore keeps its pushes in order (aq_push appends) and
+// aq_drain writes the cycle's whole pop sequence into the queue's HBM array when the cycle starts: pop
+// k at slot n-1-k (the slot that pop frees in the heap, so nothing outside the array is needed).
+// * Keys pairwise distinct (total_key of the timestamp: Ord is other.timestamp.total_cmp(&self.
+//   timestamp), queue.rs:13-27): a max-heap pops in descending Ord whatever its shape, i.e. in
+//   ascending key order.  Device: lane l holds entries l, l+64, l+128, l+192 (n <= 256), counts for
+//   each the keys below and not above it (every key broadcast by readlane: n·(2 + 4·M) VALU for
+//   the whole cycle) and writes it to its rank; a count of equal keys other than its own flags a tie.
+// * Some keys equal, or n > 256: the Rust heap's order among equal keys depends on its shape, so the
+//   pushes' heap is rebuilt exactly (each push's sift-up replayed in push order) and popped as before.
+// This replaces a cycle's n pops (each a sift down with dependent child loads below the LDS levels)
+// by one pass over the queue.
+#define K10S_AQ_SORT_M 4
+K10S_HD_NOINL uint32_t aq_drain(Ctx& c) {
+    RepHdr& H = c.H();
+    const uint32_t n = uniform_u32(H.aq_size);
+    QInfo* d = c.V().aq();
+    if (n == 0) return 0;
+#if K10S_DEVICE
+    if (!K10S_FULL_WAVE(XG_AQ_DRAIN)) return 0;
+    if (n <= 64u * K10S_AQ_SORT_M) {
+        const uint32_t lane = (uint32_t)lane_id();
+        QInfo e[K10S_AQ_SORT_M];
+        int64_t k[K10S_AQ_SORT_M];
+        uint32_t lt[K10S_AQ_SORT_M], le[K10S_AQ_SORT_M];
+        K10S_UNROLL
+        for (int m = 0; m < K10S_AQ_SORT_M; m++) {
+            const uint32_t i = lane + 64u * (uint32_t)m;
+            e[m].timestamp = 0.0;
+            e[m].initial = 0.0;
+            e[m].attempts = 0;
+            e[m].pod = 0;
+            if (i < n) e[m] = i < K10S_AQ_TOP ? H.aq_lds[i] : d[i];
+            k[m] = total_key(e[m].timestamp);
+            lt[m] = 0;
+            le[m] = 0;
+        }
+        K10S_UNROLL
+        for (int mj = 0; mj < K10S_AQ_SORT_M; mj++) {
+            if (64u * (uint32_t)mj >= n) break;
+            const uint32_t left = n - 64u * (uint32_t)mj, cnt = left < 64u ? left : 64u;
+            const uint32_t klo = (uint32_t)(uint64_t)k[mj], khi = (uint32_t)((uint64_t)k[mj] >> 32);
+            for (uint32_t j = 0; j < cnt; j++) {
+                const int64_t kj = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)khi, (int)j) << 32) |
+                                             (uint32_t)__builtin_amdgcn_readlane((int)klo, (int)j));
+                K10S_UNROLL
+                for (int m = 0; m < K10S_AQ_SORT_M; m++) {
+                    lt[m] += kj < k[m] ? 1u : 0u;
+                    le[m] += kj <= k[m] ? 1u : 0u;
+                }
+            }
+        }
+        bool tie = false;
+        K10S_UNROLL
+        for (int m = 0; m < K10S_AQ_SORT_M; m++)
+            if (lane + 64u * (uint32_t)m < n) tie |= le[m] - lt[m] != 1u;
+        if (!__ballot(tie)) {
+            K10S_UNROLL
+            for (int m = 0; m < K10S_AQ_SORT_M; m++)
+                if (lane + 64u * (uint32_t)m < n) d[n - 1u - lt[m]] = e[m];
+            H.aq_size = 0;
+            wave_sync();
+            return n;
+        }
+    }
+#else
+    if (n <= 64u * K10S_AQ_SORT_M) {   // the same rank computation, one entry at a time
+        QInfo e[64 * K10S_AQ_SORT_M];
+        uint32_t lt[64 * K10S_AQ_SORT_M];
+        bool tie = false;
+        for (uint32_t i = 0; i < n; i++) e[i] = aq_get(c, i);
+        for (uint32_t i = 0; i < n; i++) {
+            const int64_t ki = total_key(e[i].timestamp);
+            uint32_t l = 0, q = 0;
+            for (uint32_t j = 0; j < n; j++) {
+                const int64_t kj = total_key(e[j].timestamp);
+                l += kj < ki ? 1u : 0u;
+                q += kj <= ki ? 1u : 0u;
+            }
+            lt[i] = l;
+            tie |= q - l != 1u;
+        }
+        if (!tie) {
+            for (uint32_t i = 0; i < n; i++) d[n - 1u - lt[i]] = e[i];
+            H.aq_size = 0;
+            return n;
+        }
+    }
+#endif
+    // equal keys (or a long queue): the pushes' heap, rebuilt in push order, popped
+    for (uint32_t i = 1; i < n; i++) aq_sift_up(c, 0, i, aq_get(c, i));
+    for (uint32_t j = 0; j < n; j++) {
+        const QInfo q = aq_pop(c);
+        d[n - 1u - j] = q;
+    }
+    wave_sync();
+    return n;
+}
+// The cycle's k-th pop (after aq_drain returned n).
+K10S_HD QInfo aq_drained(Ctx& c, uint32_t n, uint32_t k) {
+    QInfo q = c.V().aq()[n - 1u - k];
+#if K10S_DEVICE
+    q.timestamp = uniform_f64(q.timestamp);
+    q.initial = uniform_f64(q.initial);
+    q.attempts = uniform_u32(q.attempts);
+    q.pod = uniform_u32(q.pod);
+#endif
+    return q;
 }
 
 // ---- unschedulable_pods: BTreeMap<(insert_timestamp total_cmp, pod name)> as a sorted array -----
@@ -1815,10 +1932,11 @@ K10S_HD_NOINL void run_scheduling_cycle_t(Ctx& c, double t) {
     uint32_t fails = 0;
     RepHdr* h = &c.H();
     h->g_pods_q = (uint64_t)h->aq_size + (uint64_t)h->uq_size;  // scheduler.rs:256-259
-    while (c.H().aq_size > 0 && !c.H().error_code) {
-        const uint64_t t_aq = prof_now();
-        const QInfo q = aq_pop(c);
-        K10S_PROF_ADD(c, PROF_AQPOP, t_aq);
+    const uint64_t t_aq = prof_now();
+    const uint32_t n = aq_drain(c);   // the cycle's pops, in order
+    K10S_PROF_ADD(c, PROF_AQPOP, t_aq);
+    for (uint32_t k = 0; k < n && !c.H().error_code; k++) {
+        const QInfo q = aq_drained(c, n, k);
         if (!pod_in_s(c, q.pod)) continue;   // removed from the cache (scheduler.rs:263-269)
         cycle_attempt<PLUG>(c, t, q, false, cycle_dur, fails);
     }
@@ -1827,40 +1945,35 @@ K10S_HD_NOINL void run_scheduling_cycle_t(Ctx& c, double t) {
 
 // The cycle in tiles (fit_tile above): run after a cycle with failed attempts, on the
 // LeastAllocated-only fast path with the packed cache (its own out-of-line function, so the serial
-// cycle's register allocation is unchanged).  The next K10S_TILE entries are popped in order (the
-// same pops the loop would make) and kept in the queue array slots their pops vacated (slot top-1-j
-// for the j-th: the array only shrinks during a cycle; HBM part), a removed pod marked and later
-// skipped like the loop's `continue`; their fit is tested together, then each is attempted in order.
+// cycle's register allocation is unchanged).  The cycle's pops come in order from aq_drain; each
+// tile takes the next K10S_TILE of them (a removed pod skipped like the loop's `continue`), tests
+// their fit together, then attempts each in order.
 K10S_HD_NOINL void run_scheduling_cycle_tiles(Ctx& c, double t) {
     if (!K10S_FULL_WAVE(XG_CYCLE)) return;
     double cycle_dur = 0.0;
     uint32_t fails = 0;
     RepHdr* h = &c.H();
     h->g_pods_q = (uint64_t)h->aq_size + (uint64_t)h->uq_size;  // scheduler.rs:256-259
-    while (c.H().aq_size > 0 && !c.H().error_code) {
-        QInfo* slot = c.V().aq();
-        const uint32_t top = uniform_u32(h->aq_size);
-        uint32_t nt = 0;
-        const uint64_t t_aq = prof_now();
-        for (; nt < K10S_TILE && c.H().aq_size > 0; nt++) {
-            QInfo q = aq_pop(c);
-            if (!pod_in_s(c, q.pod)) q.pod = 0xFFFFFFFFu;
-            slot[top - 1 - nt] = q;
-        }
-        K10S_PROF_ADD(c, PROF_AQPOP, t_aq);
-        wave_sync();
+    const uint64_t t_aq = prof_now();
+    const uint32_t n = aq_drain(c);   // the cycle's pops, in order
+    K10S_PROF_ADD(c, PROF_AQPOP, t_aq);
+    for (uint32_t k0 = 0; k0 < n && !c.H().error_code; k0 += K10S_TILE) {
+        const uint32_t nt = n - k0 < (uint32_t)K10S_TILE ? n - k0 : (uint32_t)K10S_TILE;
         // the tile's requests (fast-path pods only: both requests > 0 and within the packed fields;
-        // a request beyond them fits no packed entry)
+        // a request beyond them fits no packed entry); skip: removed from the cache (the loop's
+        // `continue`, scheduler.rs:263-269; membership does not change during a cycle)
         uint32_t rc8[K10S_TILE];
         uint64_t rrq[K10S_TILE];
-        uint32_t need = 0, never = 0;
+        uint32_t need = 0, never = 0, skip = 0;
         K10S_UNROLL
         for (int j = 0; j < K10S_TILE; j++) {
             rc8[j] = 0xFFFFFFFFu;
             rrq[j] = ~0ull;
             if ((uint32_t)j < nt) {
-                const uint32_t p = uniform_u32(slot[top - 1 - j].pod);
-                if (p != 0xFFFFFFFFu) {
+                const uint32_t p = uniform_u32(c.V().aq()[n - 1u - (k0 + (uint32_t)j)].pod);
+                if (!pod_in_s(c, p)) {
+                    skip |= 1u << j;
+                } else {
                     const uint32_t rc = uniform_u32(c.V().pod(p).req_cpu);
                     const uint64_t rr = uniform_u64(c.V().pod(p).req_ram);
                     if (rc > 0 && rr > 0) {
@@ -1885,14 +1998,8 @@ K10S_HD_NOINL void run_scheduling_cycle_tiles(Ctx& c, double t) {
         }
         const uint32_t nofit = (need & ~found) | never;
         for (uint32_t j = 0; j < nt && !c.H().error_code; j++) {
-            const QInfo q = slot[top - 1 - j];
-            if (uniform_u32(q.pod) == 0xFFFFFFFFu) continue;
-            QInfo u;
-            u.timestamp = uniform_f64(q.timestamp);
-            u.initial = uniform_f64(q.initial);
-            u.attempts = uniform_u32(q.attempts);
-            u.pod = uniform_u32(q.pod);
-            cycle_attempt<false>(c, t, u, (nofit >> j) & 1u, cycle_dur, fails);
+            if ((skip >> j) & 1u) continue;
+            cycle_attempt<false>(c, t, aq_drained(c, n, k0 + j), (nofit >> j) & 1u, cycle_dur, fails);
         }
     }
     cycle_end(c, cycle_dur, fails);

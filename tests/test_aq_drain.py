@@ -1,0 +1,101 @@
+"""The cycle's pop sequence (k10s_engine.h aq_drain): the action queue keeps its pushes in order and
+the scheduling cycle orders them once when it starts — by rank when the keys are pairwise distinct
+(1-64, 65-256 entries: one to four entries per lane), by rebuilding the pushes' BinaryHeap and
+popping it when some keys are equal or the queue is longer than 256 (queue.rs:13-27,
+scheduler.rs:261-330).  Each case is checked against the oracle (a restatement of the Rust
+BinaryHeap push/pop) bit for bit: counters, clock, estimators, every placement and the event log,
+on the host build and the GPU."""
+import random
+
+import pytest
+
+import parity
+from hostcheck_bridge import HostEngine
+from kubernetriks_amd.scenario import GenericClusterTrace, GenericWorkloadTrace, Node, Pod, SimulationConfig, scenario_text
+
+BACKENDS = [pytest.param("host", id="host"), pytest.param("gpu", id="gpu", marks=pytest.mark.gpu)]
+GIB = 1 << 30
+
+
+def _engine(backend):
+    if backend == "host":
+        return HostEngine
+    from kubernetriks_amd.native import Engine
+    return Engine
+
+
+def queue_scenario(seed, n_pods, per_cycle, ties=0.0, cycle=10.0, n_nodes=48, move_all=False):
+    """About `per_cycle` pods arrive between two cycles, at distinct times unless `ties` (the share of
+    pods that take the previous pod's creation time); `move_all`: a small cluster, so failed pods
+    come back through the unschedulable map with equal-time batches."""
+    rng = random.Random(seed)
+    cfg = SimulationConfig()
+    cfg.scheduling_cycle_interval = cycle
+    cfg.enable_unscheduled_pods_conditional_move = False
+    c = GenericClusterTrace()
+    for k in range(n_nodes):
+        c.create_node(0.0, Node(f"node_{k:03d}", rng.choice([8000, 16000, 32000]), rng.choice([32, 64, 128]) * GIB))
+    w = GenericWorkloadTrace()
+    t = 0.0
+    rate = per_cycle / cycle
+    for i in range(n_pods):
+        if i == 0 or rng.random() >= ties:
+            t += rng.expovariate(rate)
+        cpu = rng.choice([250, 500, 1000, 2000]) * (4 if move_all else 1)
+        ram = int(rng.uniform(0.5, 4.0) * GIB) * (8 if move_all else 1)
+        w.create_pod(round(t, 6), Pod(f"pod_{i:05d}", cpu, ram, float(rng.randint(5, 200))))
+    return scenario_text(cfg, c, w)
+
+
+CASES = {
+    "one_per_lane": dict(seed=1, n_pods=400, per_cycle=40),          # n <= 64, distinct keys
+    "two_per_lane": dict(seed=2, n_pods=900, per_cycle=110),         # 65..128
+    "four_per_lane": dict(seed=3, n_pods=1500, per_cycle=230),       # 129..256
+    "over_256": dict(seed=4, n_pods=1600, per_cycle=400),            # > 256: the heap path
+    "ties": dict(seed=5, n_pods=600, per_cycle=50, ties=0.3),        # equal keys: the heap path
+    "ties_long": dict(seed=6, n_pods=1500, per_cycle=300, ties=0.5),
+    "requeued": dict(seed=7, n_pods=700, per_cycle=60, n_nodes=6, move_all=True),
+}
+# what each case's cycles see (pushes by PodScheduleRequest between two cycles; requeues aside):
+# (smallest largest queue, largest largest queue, cycles with equal keys: "none" / "all")
+DESIGN = {
+    "one_per_lane": (1, 64, "none"), "two_per_lane": (65, 128, "none"), "four_per_lane": (129, 256, "none"),
+    "over_256": (257, 10 ** 9, None), "ties": (1, 256, "all"), "ties_long": (257, 10 ** 9, "all"),
+}
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_cycle_pop_sequence_matches_oracle(backend, case):
+    scn = queue_scenario(**CASES[case])
+    od, eng = parity.run_pair(_engine(backend), scn, max_time=1e6)
+    assert parity.compare(od, eng) == [], case
+    k = eng.results()[0]["counters"]
+    assert k["placements"] > 0
+
+
+def _cycle_queues(od):
+    from kubernetriks_amd.native import EVENT_KIND_NAMES
+    inv = {v: k for k, v in EVENT_KIND_NAMES.items()}
+    sizes, cur = [], []
+    for e in od["log"]:
+        if e[2] == inv["S_POD_SCHEDULE_REQ"]:
+            cur.append(e[1])
+        elif e[2] == inv["S_RUN_CYCLE"] and cur:
+            sizes.append((len(cur), len(cur) != len(set(cur))))
+            cur = []
+    return sizes
+
+
+@pytest.mark.parametrize("case", sorted(DESIGN))
+def test_cases_reach_their_regime(case):
+    """The scenarios exercise the path their name says (queue length per cycle, equal keys)."""
+    lo, hi, ties = DESIGN[case]
+    od, _ = parity.run_pair(HostEngine, queue_scenario(**CASES[case]), max_time=1e6)
+    q = _cycle_queues(od)
+    biggest = max(n for n, _ in q)
+    assert lo <= biggest <= hi, (case, biggest)
+    if ties == "none":
+        assert not any(t for _, t in q), case
+    elif ties == "all":
+        assert all(t for n, t in q if n > 1), case
