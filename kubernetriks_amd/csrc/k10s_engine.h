@@ -514,7 +514,8 @@ extern "C" uint64_t k10s_host_stats[48];
 #define K10S_HSTAT(i) ((void)0)
 #endif
 enum { HS_EVENTS, HS_FIFO_POP, HS_REFILL, HS_HEAP_POP, HS_TRACE_POP, HS_SL_FAST, HS_SL_UPDATE, HS_EMIT_WIN,
-       HS_EMIT_RING, HS_EMIT_HEAP, HS_SL_DIRTY, HS_SCANS, HS_REFILL_CLS0 = 12, HS_POP_CLS0 = 20, HS_AQ_HBM_GET = 28, HS_AQ_POP = 29, HS_SLPOS0 = 32 };
+       HS_EMIT_RING, HS_EMIT_HEAP, HS_SL_DIRTY, HS_SCANS, HS_REFILL_CLS0 = 12, HS_POP_CLS0 = 20, HS_AQ_HBM_GET = 28, HS_AQ_POP = 29, HS_SLPOS0 = 32,
+       HS_NEXT_EMITTED = 36, HS_NEXT_EMITTED_FIFO = 37, HS_AQ_SORTED = 38, HS_AQ_HEAPED = 39, HS_AQ_SIM = 40 };
 // An emission changed source q's head: mark it for the source list.
 K10S_HD void sl_mark(RepHdr& H, uint32_t q) { H.sl_dirty |= 1u << q; }
 K10S_HD void pods_left_dec(RepHdr& H) { H.pods_left -= 1; }
@@ -870,11 +871,67 @@ K10S_HELPER QInfo aq_pop(Ctx& c) {
 //   ascending key order.  Device: lane l holds entries l, l+64, l+128, l+192 (n <= 256), counts for
 //   each the keys below and not above it (every key broadcast by readlane: n·(2 + 4·M) VALU for
 //   the whole cycle) and writes it to its rank; a count of equal keys other than its own flags a tie.
-// * Some keys equal, or n > 256: the Rust heap's order among equal keys depends on its shape, so the
-//   pushes' heap is rebuilt exactly (each push's sift-up replayed in push order) and popped as before.
+// * Some keys equal: the Rust heap's order among equal keys depends on its shape, so the pushes' heap
+//   is rebuilt exactly (each push's sift-up replayed in push order) and popped: in registers on the
+//   keys' ranks for n <= 128 (C3's integer-second arrivals make equal keys the rule), in the queue's
+//   memory as before for longer queues (and for n > 256).
 // This replaces a cycle's n pops (each a sift down with dependent child loads below the LDS levels)
 // by one pass over the queue.
+// The Rust BinaryHeap of the pushes (aq_sift_up, aq_pop) replayed on values rank << 8 | push index
+// (rank = the number of smaller keys: equal keys have equal ranks, and only the keys' order matters
+// to the heap; n <= 128): get(q) / set(q, v) address heap position q, rank(i) is push i's rank, and
+// out(i, n-1-k) receives the k-th pop.  a <= b in the queue's Ord (later timestamp = smaller) <=>
+// rank(b) <= rank(a).
+template <typename Get, typename Set, typename Rank, typename Out>
+K10S_HD void aq_sim(uint32_t n, Get get, Set set, Rank rank, Out out) {
+    auto sift_up = [&](uint32_t pos, uint32_t v) {
+        while (pos > 0) {
+            const uint32_t parent = (pos - 1u) >> 1;
+            const uint32_t pv = get(parent);
+            if ((pv >> 8) <= (v >> 8)) break;
+            set(pos, pv);
+            pos = parent;
+        }
+        set(pos, v);
+    };
+    for (uint32_t i = 0; i < n; i++) sift_up(i, rank(i) << 8 | i);
+    for (uint32_t j = 0; j < n; j++) {
+        const uint32_t end = n - 1u - j;
+        const uint32_t item = get(end);
+        uint32_t top = item;
+        if (end > 0) {   // sift_down_to_bottom(0) with `item` in the hole, then sift_up
+            top = get(0);
+            uint32_t pos = 0, child = 1;
+            while (end >= 2u && child <= end - 2u) {
+                uint32_t a = get(child);
+                const uint32_t b = get(child + 1u);
+                if ((b >> 8) <= (a >> 8)) {
+                    child += 1u;
+                    a = b;
+                }
+                set(pos, a);
+                pos = child;
+                child = 2u * pos + 1u;
+            }
+            if (child == end - 1u) {
+                set(pos, get(child));
+                pos = child;
+            }
+            sift_up(pos, item);
+        }
+        out(top & 0xFFu, end);
+    }
+}
 #define K10S_AQ_SORT_M 4
+#if K10S_DEVICE
+// v with lane `lane` (wave-uniform) replaced by `val` (wave-uniform): v_writelane_b32 (VALU, no
+// memory); this compiler has no builtin for it.
+K10S_D uint32_t writelane_u32(uint32_t v, uint32_t val, uint32_t lane) {
+    // (gfx9 reads one SGPR per VALU instruction besides M0: the lane select goes through M0)
+    asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(val), "s"(lane) : "m0");
+    return v;
+}
+#endif
 K10S_HD_NOINL uint32_t aq_drain(Ctx& c) {
     RepHdr& H = c.H();
     const uint32_t n = uniform_u32(H.aq_size);
@@ -926,6 +983,34 @@ K10S_HD_NOINL uint32_t aq_drain(Ctx& c) {
             wave_sync();
             return n;
         }
+        if (n <= 128u) {
+            // equal keys, n <= 128: the pushes' heap simulated in registers (aq_sim): heap position
+            // q in lane q & 63 of H0 / H1, the k-th pop's destination slot in D0 / D1
+            uint32_t H0 = 0, H1 = 0, D0 = 0, D1 = 0;
+            aq_sim(
+                n,
+                [&](uint32_t q) -> uint32_t {
+                    return q < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)H0, (int)q)
+                                   : (uint32_t)__builtin_amdgcn_readlane((int)H1, (int)(q - 64u));
+                },
+                [&](uint32_t q, uint32_t v) {
+                    if (q < 64u) H0 = writelane_u32(H0, v, q);
+                    else H1 = writelane_u32(H1, v, q - 64u);
+                },
+                [&](uint32_t i) -> uint32_t {
+                    return i < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)lt[0], (int)i)
+                                   : (uint32_t)__builtin_amdgcn_readlane((int)lt[1], (int)(i - 64u));
+                },
+                [&](uint32_t i, uint32_t slot) {
+                    if (i < 64u) D0 = writelane_u32(D0, slot, i);
+                    else D1 = writelane_u32(D1, slot, i - 64u);
+                });
+            if (lane < n) d[D0] = e[0];
+            if (lane + 64u < n) d[D1] = e[1];
+            H.aq_size = 0;
+            wave_sync();
+            return n;
+        }
     }
 #else
     if (n <= 64u * K10S_AQ_SORT_M) {   // the same rank computation, one entry at a time
@@ -947,11 +1032,23 @@ K10S_HD_NOINL uint32_t aq_drain(Ctx& c) {
         if (!tie) {
             for (uint32_t i = 0; i < n; i++) d[n - 1u - lt[i]] = e[i];
             H.aq_size = 0;
+            K10S_HSTAT(HS_AQ_SORTED);
+            return n;
+        }
+        if (n <= 128u) {   // the device's register simulation, on arrays
+            uint32_t hv[128], dst[128];
+            aq_sim(
+                n, [&](uint32_t q) { return hv[q]; }, [&](uint32_t q, uint32_t v) { hv[q] = v; },
+                [&](uint32_t i) { return lt[i]; }, [&](uint32_t i, uint32_t slot) { dst[i] = slot; });
+            for (uint32_t i = 0; i < n; i++) d[dst[i]] = e[i];
+            H.aq_size = 0;
+            K10S_HSTAT(HS_AQ_SIM);
             return n;
         }
     }
 #endif
     // equal keys (or a long queue): the pushes' heap, rebuilt in push order, popped
+    K10S_HSTAT(HS_AQ_HEAPED);
     for (uint32_t i = 1; i < n; i++) aq_sift_up(c, 0, i, aq_get(c, i));
     for (uint32_t j = 0; j < n; j++) {
         const QInfo q = aq_pop(c);
@@ -3734,6 +3831,9 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
     const uint64_t t_loop = prof_now();
     sl_rebuild(c, ntr);  // the sorted source list, from the sources' heads
     [[maybe_unused]] uint32_t it_stale = 0;
+#if !K10S_DEVICE && defined(K10S_HOST_STATS)
+    uint32_t hs_next_before = 0xFFFFFFFFu;
+#endif
     while (!h->error_code) {
         if (!until_mode() && h->pods_left <= 0 && is_multiple_of_1000(h->clock)) {
             status = K10S_REPLICA_FINISHED;
@@ -3804,6 +3904,13 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
             more = 1;
             break;
         }
+#if !K10S_DEVICE && defined(K10S_HOST_STATS)
+        if (e.seq >= hs_next_before) {   // emitted by the previous event's handler
+            K10S_HSTAT(HS_NEXT_EMITTED);
+            if (src < K10S_NFQ) K10S_HSTAT(HS_NEXT_EMITTED_FIFO);
+        }
+        hs_next_before = h->next_seq;
+#endif
         h->clock = e.time;
         h->cur_kind = e.kind;
         h->cur_seq = e.seq;
