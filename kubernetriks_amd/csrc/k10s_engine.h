@@ -65,7 +65,7 @@ __device__ uint32_t* k10s_beacon;   // [replica][K10S_BEACON_WORDS], host-mapped
 enum : uint32_t {
     XG_HEAP_POP = 1, XG_HEAP_MIN_CHILD, XG_HEAP_MIN_CHILD_EV, XG_SCHEDULE_SCAN, XG_SL_UPDATE, XG_FQ_REFILL,
     XG_PODS_IN_ORDER, XG_FOR_EACH_BIT, XG_CA_FIRST_FIT, XG_CA_SORT, XG_DISPATCH, XG_CYCLE, XG_GAUGE, XG_CACHE_FITS,
-    XG_FAIR, XG_HANDLER, XG_EMIT, XG_SCAN_PLUGINS, XG_AQ_DRAIN,
+    XG_FAIR, XG_HANDLER, XG_EMIT, XG_SCAN_PLUGINS,
     XG_LOOP_HEAP_POP = 0x40, XG_LOOP_EMIT, XG_LOOP_AQ_POP, XG_LOOP_AQ_UP, XG_LOOP_STALE,
 };
 #if K10S_DEVICE && K10S_EXEC_CHECK
@@ -515,7 +515,7 @@ extern "C" uint64_t k10s_host_stats[48];
 #endif
 enum { HS_EVENTS, HS_FIFO_POP, HS_REFILL, HS_HEAP_POP, HS_TRACE_POP, HS_SL_FAST, HS_SL_UPDATE, HS_EMIT_WIN,
        HS_EMIT_RING, HS_EMIT_HEAP, HS_SL_DIRTY, HS_SCANS, HS_REFILL_CLS0 = 12, HS_POP_CLS0 = 20, HS_AQ_HBM_GET = 28, HS_AQ_POP = 29, HS_SLPOS0 = 32,
-       HS_NEXT_EMITTED = 36, HS_NEXT_EMITTED_FIFO = 37, HS_AQ_SORTED = 38, HS_AQ_HEAPED = 39, HS_AQ_SIM = 40 };
+       HS_NEXT_EMITTED = 36, HS_NEXT_EMITTED_FIFO = 37 };
 // An emission changed source q's head: mark it for the source list.
 K10S_HD void sl_mark(RepHdr& H, uint32_t q) { H.sl_dirty |= 1u << q; }
 K10S_HD void pods_left_dec(RepHdr& H) { H.pods_left -= 1; }
@@ -793,6 +793,23 @@ K10S_HD QInfo aq_get(Ctx& c, uint32_t i) {
 #endif
     return q;
 }
+// The same slot as loaded, without making its fields wave-uniform: a sift moves whole entries but
+// compares only timestamps, so the entries stay in VGPRs (stored back as loaded) and only the
+// timestamp goes through readfirstlane (aq_ts) — 2 instead of 6 per entry read.
+K10S_HD QInfo aq_raw(Ctx& c, uint32_t i) {
+#if K10S_AQ_TOP
+    if (i < K10S_AQ_TOP) return c.H().aq_lds[i];
+#endif
+    K10S_HSTAT(HS_AQ_HBM_GET);
+    return c.V().aq()[i];
+}
+K10S_HD int64_t aq_ts(const QInfo& q) {
+#if K10S_DEVICE
+    return total_key(uniform_f64(q.timestamp));
+#else
+    return total_key(q.timestamp);
+#endif
+}
 K10S_HD void aq_put(Ctx& c, uint32_t i, const QInfo& q) {
 #if K10S_AQ_TOP
     if (i < K10S_AQ_TOP) {
@@ -805,26 +822,25 @@ K10S_HD void aq_put(Ctx& c, uint32_t i, const QInfo& q) {
 
 K10S_HD uint32_t aq_sift_up(Ctx& c, uint32_t start, uint32_t pos, const QInfo& elem) {
     [[maybe_unused]] uint32_t it = 0;
+    const int64_t ke = aq_ts(elem);
     while (pos > start) {
         if (K10S_LOOP_CAP(it, 40, XG_LOOP_AQ_UP)) break;
         uint32_t parent = (pos - 1) / 2;
-        QInfo p = aq_get(c, parent);
-        if (q_le(elem, p)) break;
+        const QInfo p = aq_raw(c, parent);
+        if (ke >= aq_ts(p)) break;   // q_le(elem, p)
         aq_put(c, pos, p);
         pos = parent;
     }
     aq_put(c, pos, elem);
     return pos;
 }
-// The action queue between two cycles is a push log (aq_drain below): a push appends.
 K10S_HELPER void aq_push(Ctx& c, const QInfo& q) {
     if (c.H().aq_size >= c.Ly().cap_aq) {
         fail(c, K10S_ERR_QUEUE_FULL);
         return;
     }
-    const uint32_t pos = uniform_u32(c.H().aq_size);
-    c.H().aq_size = pos + 1;
-    aq_put(c, pos, q);
+    uint32_t old = c.H().aq_size++;
+    aq_sift_up(c, 0, old, q);
 }
 // (Round 3 tried reading the 3-level subtree under the walk's position in one round trip below the
 // LDS levels: C3 +0.6 %, backlog -2 to -4 % from the extra SGPRs live in the scheduling cycle,
@@ -841,232 +857,22 @@ K10S_HELPER QInfo aq_pop(Ctx& c) {
     [[maybe_unused]] uint32_t it = 0;
     while (end >= 2 && child <= end - 2) {
         if (K10S_LOOP_CAP(it, 40, XG_LOOP_AQ_POP)) break;
-        QInfo a = aq_get(c, child), b = aq_get(c, child + 1);
-        if (q_le(a, b)) {
+        const QInfo a = aq_raw(c, child), b = aq_raw(c, child + 1);
+        if (aq_ts(b) <= aq_ts(a)) {   // q_le(a, b): the right child
+            aq_put(c, pos, b);
             child += 1;
-            a = b;
+        } else {
+            aq_put(c, pos, a);
         }
-        aq_put(c, pos, a);
         pos = child;
         child = 2 * pos + 1;
     }
     if (child == end - 1) {
-        aq_put(c, pos, aq_get(c, child));
+        aq_put(c, pos, aq_raw(c, child));
         pos = child;
     }
     aq_sift_up(c, 0, pos, item);
     return top;
-}
-
-// ---- the cycle's pop sequence, fixed when the cycle starts ----------------------------------------
-// Only the scheduling cycle pops the action queue, it pops until the queue is empty
-// (scheduler.rs:261-330, `while let Some(..) = self.action_queue.pop()`), and nothing is pushed while
-// it runs (a failed pod goes to the unschedulable map, every emission to the event queue).  So between
-// two cycles the BinaryHeap is built from empty by a sequence of pushes, and a cycle's pops are a
-// sequence known when it starts.  The queue therefore keeps its pushes in order (aq_push appends) and
-// aq_drain writes the cycle's whole pop sequence into the queue's HBM array when the cycle starts: pop
-// k at slot n-1-k (the slot that pop frees in the heap, so nothing outside the array is needed).
-// * Keys pairwise distinct (total_key of the timestamp: Ord is other.timestamp.total_cmp(&self.
-//   timestamp), queue.rs:13-27): a max-heap pops in descending Ord whatever its shape, i.e. in
-//   ascending key order.  Device: lane l holds entries l, l+64, l+128, l+192 (n <= 256), counts for
-//   each the keys below and not above it (every key broadcast by readlane: n·(2 + 4·M) VALU for
-//   the whole cycle) and writes it to its rank; a count of equal keys other than its own flags a tie.
-// * Some keys equal: the Rust heap's order among equal keys depends on its shape, so the pushes' heap
-//   is rebuilt exactly (each push's sift-up replayed in push order) and popped: in registers on the
-//   keys' ranks for n <= 128 (C3's integer-second arrivals make equal keys the rule), in the queue's
-//   memory as before for longer queues (and for n > 256).
-// This replaces a cycle's n pops (each a sift down with dependent child loads below the LDS levels)
-// by one pass over the queue.
-// The Rust BinaryHeap of the pushes (aq_sift_up, aq_pop) replayed on values rank << 8 | push index
-// (rank = the number of smaller keys: equal keys have equal ranks, and only the keys' order matters
-// to the heap; n <= 128): get(q) / set(q, v) address heap position q, rank(i) is push i's rank, and
-// out(i, n-1-k) receives the k-th pop.  a <= b in the queue's Ord (later timestamp = smaller) <=>
-// rank(b) <= rank(a).
-template <typename Get, typename Set, typename Rank, typename Out>
-K10S_HD void aq_sim(uint32_t n, Get get, Set set, Rank rank, Out out) {
-    auto sift_up = [&](uint32_t pos, uint32_t v) {
-        while (pos > 0) {
-            const uint32_t parent = (pos - 1u) >> 1;
-            const uint32_t pv = get(parent);
-            if ((pv >> 8) <= (v >> 8)) break;
-            set(pos, pv);
-            pos = parent;
-        }
-        set(pos, v);
-    };
-    for (uint32_t i = 0; i < n; i++) sift_up(i, rank(i) << 8 | i);
-    for (uint32_t j = 0; j < n; j++) {
-        const uint32_t end = n - 1u - j;
-        const uint32_t item = get(end);
-        uint32_t top = item;
-        if (end > 0) {   // sift_down_to_bottom(0) with `item` in the hole, then sift_up
-            top = get(0);
-            uint32_t pos = 0, child = 1;
-            while (end >= 2u && child <= end - 2u) {
-                uint32_t a = get(child);
-                const uint32_t b = get(child + 1u);
-                if ((b >> 8) <= (a >> 8)) {
-                    child += 1u;
-                    a = b;
-                }
-                set(pos, a);
-                pos = child;
-                child = 2u * pos + 1u;
-            }
-            if (child == end - 1u) {
-                set(pos, get(child));
-                pos = child;
-            }
-            sift_up(pos, item);
-        }
-        out(top & 0xFFu, end);
-    }
-}
-#define K10S_AQ_SORT_M 4
-#if K10S_DEVICE
-// v with lane `lane` (wave-uniform) replaced by `val` (wave-uniform): v_writelane_b32 (VALU, no
-// memory); this compiler has no builtin for it.
-K10S_D uint32_t writelane_u32(uint32_t v, uint32_t val, uint32_t lane) {
-    // (gfx9 reads one SGPR per VALU instruction besides M0: the lane select goes through M0)
-    asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(val), "s"(lane) : "m0");
-    return v;
-}
-#endif
-K10S_HD_NOINL uint32_t aq_drain(Ctx& c) {
-    RepHdr& H = c.H();
-    const uint32_t n = uniform_u32(H.aq_size);
-    QInfo* d = c.V().aq();
-    if (n == 0) return 0;
-#if K10S_DEVICE
-    if (!K10S_FULL_WAVE(XG_AQ_DRAIN)) return 0;
-    if (n <= 64u * K10S_AQ_SORT_M) {
-        const uint32_t lane = (uint32_t)lane_id();
-        QInfo e[K10S_AQ_SORT_M];
-        int64_t k[K10S_AQ_SORT_M];
-        uint32_t lt[K10S_AQ_SORT_M], le[K10S_AQ_SORT_M];
-        K10S_UNROLL
-        for (int m = 0; m < K10S_AQ_SORT_M; m++) {
-            const uint32_t i = lane + 64u * (uint32_t)m;
-            e[m].timestamp = 0.0;
-            e[m].initial = 0.0;
-            e[m].attempts = 0;
-            e[m].pod = 0;
-            if (i < n) e[m] = i < K10S_AQ_TOP ? H.aq_lds[i] : d[i];
-            k[m] = total_key(e[m].timestamp);
-            lt[m] = 0;
-            le[m] = 0;
-        }
-        K10S_UNROLL
-        for (int mj = 0; mj < K10S_AQ_SORT_M; mj++) {
-            if (64u * (uint32_t)mj >= n) break;
-            const uint32_t left = n - 64u * (uint32_t)mj, cnt = left < 64u ? left : 64u;
-            const uint32_t klo = (uint32_t)(uint64_t)k[mj], khi = (uint32_t)((uint64_t)k[mj] >> 32);
-            for (uint32_t j = 0; j < cnt; j++) {
-                const int64_t kj = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)khi, (int)j) << 32) |
-                                             (uint32_t)__builtin_amdgcn_readlane((int)klo, (int)j));
-                K10S_UNROLL
-                for (int m = 0; m < K10S_AQ_SORT_M; m++) {
-                    lt[m] += kj < k[m] ? 1u : 0u;
-                    le[m] += kj <= k[m] ? 1u : 0u;
-                }
-            }
-        }
-        bool tie = false;
-        K10S_UNROLL
-        for (int m = 0; m < K10S_AQ_SORT_M; m++)
-            if (lane + 64u * (uint32_t)m < n) tie |= le[m] - lt[m] != 1u;
-        if (!__ballot(tie)) {
-            K10S_UNROLL
-            for (int m = 0; m < K10S_AQ_SORT_M; m++)
-                if (lane + 64u * (uint32_t)m < n) d[n - 1u - lt[m]] = e[m];
-            H.aq_size = 0;
-            wave_sync();
-            return n;
-        }
-        if (n <= 128u) {
-            // equal keys, n <= 128: the pushes' heap simulated in registers (aq_sim): heap position
-            // q in lane q & 63 of H0 / H1, the k-th pop's destination slot in D0 / D1
-            uint32_t H0 = 0, H1 = 0, D0 = 0, D1 = 0;
-            aq_sim(
-                n,
-                [&](uint32_t q) -> uint32_t {
-                    return q < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)H0, (int)q)
-                                   : (uint32_t)__builtin_amdgcn_readlane((int)H1, (int)(q - 64u));
-                },
-                [&](uint32_t q, uint32_t v) {
-                    if (q < 64u) H0 = writelane_u32(H0, v, q);
-                    else H1 = writelane_u32(H1, v, q - 64u);
-                },
-                [&](uint32_t i) -> uint32_t {
-                    return i < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)lt[0], (int)i)
-                                   : (uint32_t)__builtin_amdgcn_readlane((int)lt[1], (int)(i - 64u));
-                },
-                [&](uint32_t i, uint32_t slot) {
-                    if (i < 64u) D0 = writelane_u32(D0, slot, i);
-                    else D1 = writelane_u32(D1, slot, i - 64u);
-                });
-            if (lane < n) d[D0] = e[0];
-            if (lane + 64u < n) d[D1] = e[1];
-            H.aq_size = 0;
-            wave_sync();
-            return n;
-        }
-    }
-#else
-    if (n <= 64u * K10S_AQ_SORT_M) {   // the same rank computation, one entry at a time
-        QInfo e[64 * K10S_AQ_SORT_M];
-        uint32_t lt[64 * K10S_AQ_SORT_M];
-        bool tie = false;
-        for (uint32_t i = 0; i < n; i++) e[i] = aq_get(c, i);
-        for (uint32_t i = 0; i < n; i++) {
-            const int64_t ki = total_key(e[i].timestamp);
-            uint32_t l = 0, q = 0;
-            for (uint32_t j = 0; j < n; j++) {
-                const int64_t kj = total_key(e[j].timestamp);
-                l += kj < ki ? 1u : 0u;
-                q += kj <= ki ? 1u : 0u;
-            }
-            lt[i] = l;
-            tie |= q - l != 1u;
-        }
-        if (!tie) {
-            for (uint32_t i = 0; i < n; i++) d[n - 1u - lt[i]] = e[i];
-            H.aq_size = 0;
-            K10S_HSTAT(HS_AQ_SORTED);
-            return n;
-        }
-        if (n <= 128u) {   // the device's register simulation, on arrays
-            uint32_t hv[128], dst[128];
-            aq_sim(
-                n, [&](uint32_t q) { return hv[q]; }, [&](uint32_t q, uint32_t v) { hv[q] = v; },
-                [&](uint32_t i) { return lt[i]; }, [&](uint32_t i, uint32_t slot) { dst[i] = slot; });
-            for (uint32_t i = 0; i < n; i++) d[dst[i]] = e[i];
-            H.aq_size = 0;
-            K10S_HSTAT(HS_AQ_SIM);
-            return n;
-        }
-    }
-#endif
-    // equal keys (or a long queue): the pushes' heap, rebuilt in push order, popped
-    K10S_HSTAT(HS_AQ_HEAPED);
-    for (uint32_t i = 1; i < n; i++) aq_sift_up(c, 0, i, aq_get(c, i));
-    for (uint32_t j = 0; j < n; j++) {
-        const QInfo q = aq_pop(c);
-        d[n - 1u - j] = q;
-    }
-    wave_sync();
-    return n;
-}
-// The cycle's k-th pop (after aq_drain returned n).
-K10S_HD QInfo aq_drained(Ctx& c, uint32_t n, uint32_t k) {
-    QInfo q = c.V().aq()[n - 1u - k];
-#if K10S_DEVICE
-    q.timestamp = uniform_f64(q.timestamp);
-    q.initial = uniform_f64(q.initial);
-    q.attempts = uniform_u32(q.attempts);
-    q.pod = uniform_u32(q.pod);
-#endif
-    return q;
 }
 
 // ---- unschedulable_pods: BTreeMap<(insert_timestamp total_cmp, pod name)> as a sorted array -----
@@ -2029,11 +1835,10 @@ K10S_HD_NOINL void run_scheduling_cycle_t(Ctx& c, double t) {
     uint32_t fails = 0;
     RepHdr* h = &c.H();
     h->g_pods_q = (uint64_t)h->aq_size + (uint64_t)h->uq_size;  // scheduler.rs:256-259
-    const uint64_t t_aq = prof_now();
-    const uint32_t n = aq_drain(c);   // the cycle's pops, in order
-    K10S_PROF_ADD(c, PROF_AQPOP, t_aq);
-    for (uint32_t k = 0; k < n && !c.H().error_code; k++) {
-        const QInfo q = aq_drained(c, n, k);
+    while (c.H().aq_size > 0 && !c.H().error_code) {
+        const uint64_t t_aq = prof_now();
+        const QInfo q = aq_pop(c);
+        K10S_PROF_ADD(c, PROF_AQPOP, t_aq);
         if (!pod_in_s(c, q.pod)) continue;   // removed from the cache (scheduler.rs:263-269)
         cycle_attempt<PLUG>(c, t, q, false, cycle_dur, fails);
     }
@@ -2042,35 +1847,40 @@ K10S_HD_NOINL void run_scheduling_cycle_t(Ctx& c, double t) {
 
 // The cycle in tiles (fit_tile above): run after a cycle with failed attempts, on the
 // LeastAllocated-only fast path with the packed cache (its own out-of-line function, so the serial
-// cycle's register allocation is unchanged).  The cycle's pops come in order from aq_drain; each
-// tile takes the next K10S_TILE of them (a removed pod skipped like the loop's `continue`), tests
-// their fit together, then attempts each in order.
+// cycle's register allocation is unchanged).  The next K10S_TILE entries are popped in order (the
+// same pops the loop would make) and kept in the queue array slots their pops vacated (slot top-1-j
+// for the j-th: the array only shrinks during a cycle; HBM part), a removed pod marked and later
+// skipped like the loop's `continue`; their fit is tested together, then each is attempted in order.
 K10S_HD_NOINL void run_scheduling_cycle_tiles(Ctx& c, double t) {
     if (!K10S_FULL_WAVE(XG_CYCLE)) return;
     double cycle_dur = 0.0;
     uint32_t fails = 0;
     RepHdr* h = &c.H();
     h->g_pods_q = (uint64_t)h->aq_size + (uint64_t)h->uq_size;  // scheduler.rs:256-259
-    const uint64_t t_aq = prof_now();
-    const uint32_t n = aq_drain(c);   // the cycle's pops, in order
-    K10S_PROF_ADD(c, PROF_AQPOP, t_aq);
-    for (uint32_t k0 = 0; k0 < n && !c.H().error_code; k0 += K10S_TILE) {
-        const uint32_t nt = n - k0 < (uint32_t)K10S_TILE ? n - k0 : (uint32_t)K10S_TILE;
+    while (c.H().aq_size > 0 && !c.H().error_code) {
+        QInfo* slot = c.V().aq();
+        const uint32_t top = uniform_u32(h->aq_size);
+        uint32_t nt = 0;
+        const uint64_t t_aq = prof_now();
+        for (; nt < K10S_TILE && c.H().aq_size > 0; nt++) {
+            QInfo q = aq_pop(c);
+            if (!pod_in_s(c, q.pod)) q.pod = 0xFFFFFFFFu;
+            slot[top - 1 - nt] = q;
+        }
+        K10S_PROF_ADD(c, PROF_AQPOP, t_aq);
+        wave_sync();
         // the tile's requests (fast-path pods only: both requests > 0 and within the packed fields;
-        // a request beyond them fits no packed entry); skip: removed from the cache (the loop's
-        // `continue`, scheduler.rs:263-269; membership does not change during a cycle)
+        // a request beyond them fits no packed entry)
         uint32_t rc8[K10S_TILE];
         uint64_t rrq[K10S_TILE];
-        uint32_t need = 0, never = 0, skip = 0;
+        uint32_t need = 0, never = 0;
         K10S_UNROLL
         for (int j = 0; j < K10S_TILE; j++) {
             rc8[j] = 0xFFFFFFFFu;
             rrq[j] = ~0ull;
             if ((uint32_t)j < nt) {
-                const uint32_t p = uniform_u32(c.V().aq()[n - 1u - (k0 + (uint32_t)j)].pod);
-                if (!pod_in_s(c, p)) {
-                    skip |= 1u << j;
-                } else {
+                const uint32_t p = uniform_u32(slot[top - 1 - j].pod);
+                if (p != 0xFFFFFFFFu) {
                     const uint32_t rc = uniform_u32(c.V().pod(p).req_cpu);
                     const uint64_t rr = uniform_u64(c.V().pod(p).req_ram);
                     if (rc > 0 && rr > 0) {
@@ -2095,8 +1905,14 @@ K10S_HD_NOINL void run_scheduling_cycle_tiles(Ctx& c, double t) {
         }
         const uint32_t nofit = (need & ~found) | never;
         for (uint32_t j = 0; j < nt && !c.H().error_code; j++) {
-            if ((skip >> j) & 1u) continue;
-            cycle_attempt<false>(c, t, aq_drained(c, n, k0 + j), (nofit >> j) & 1u, cycle_dur, fails);
+            const QInfo q = slot[top - 1 - j];
+            if (uniform_u32(q.pod) == 0xFFFFFFFFu) continue;
+            QInfo u;
+            u.timestamp = uniform_f64(q.timestamp);
+            u.initial = uniform_f64(q.initial);
+            u.attempts = uniform_u32(q.attempts);
+            u.pod = uniform_u32(q.pod);
+            cycle_attempt<false>(c, t, u, (nofit >> j) & 1u, cycle_dur, fails);
         }
     }
     cycle_end(c, cycle_dur, fails);
@@ -3690,6 +3506,19 @@ K10S_HD void consume_source(Ctx& c, int src, uint32_t ntr) {
             H.sl[0].key = key;
             H.sl[0].seq = seq;
             K10S_HSTAT(HS_SL_FAST);
+            return;
+        }
+        // the new head falls between sl[1] and sl[2] (64 % of the list updates at C3,
+        // tools/host_stats.py): sl[1] moves to the front and src takes its place — the list
+        // sl_update would build, without the lane-parallel pass
+        const int64_t k2 = (int64_t)uniform_u64((uint64_t)H.sl[2].key);
+        const uint32_t s2 = uniform_u32(H.sl[2].seq);
+        if (n <= 2 || sl_less(key, seq, k2, s2)) {
+            H.sl[0] = H.sl[1];
+            H.sl[1].key = key;
+            H.sl[1].seq = seq;
+            H.sl[1].src = (uint32_t)src;
+            K10S_HSTAT(HS_SLPOS0 + 1);
             return;
         }
     }

@@ -1,10 +1,12 @@
-"""The cycle's pop sequence (k10s_engine.h aq_drain): the action queue keeps its pushes in order and
-the scheduling cycle orders them once when it starts — by rank when the keys are pairwise distinct
-(1-64, 65-256 entries: one to four entries per lane), by rebuilding the pushes' BinaryHeap and
-popping it when some keys are equal or the queue is longer than 256 (queue.rs:13-27,
-scheduler.rs:261-330).  Each case is checked against the oracle (a restatement of the Rust
-BinaryHeap push/pop) bit for bit: counters, clock, estimators, every placement and the event log,
-on the host build and the GPU."""
+"""The scheduling cycle's pop order from the action queue (k10s_engine.h aq_push / aq_pop: the Rust
+BinaryHeap<QueuedPodInfo> of queue.rs:13-27, popped until empty by scheduler.rs:261-330) at the
+queue lengths and key patterns that matter: 1-64, 65-128, 129-256 and more than 256 entries per
+cycle, pairwise distinct keys, equal keys (pods created in the same instant: the heap's shape decides
+their order), and pods requeued from the unschedulable map.  Each case is checked against the oracle
+bit for bit (counters, clock, estimators, every placement and the event log) on the host build and
+the GPU; a second test checks that each scenario reaches the regime its name says.  (Round 4 also
+measured replacing the pops by one ordering pass per cycle — a rank sort for distinct keys, the heap
+simulated on key ranks in registers for equal keys — and did not keep it: DESIGN.md §7d.)"""
 import random
 
 import pytest

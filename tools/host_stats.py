@@ -53,8 +53,7 @@ def main():
                       "rings": per_ring, "aq_pops": int(st[29]), "aq_hbm_reads": int(st[28]),
                       "sl_insert_pos_0_1_2_3plus": [int(st[32 + i]) for i in range(4)],
                       "next_event_emitted_by_previous": round(int(st[36]) / ev, 4),
-                      "next_event_emitted_by_previous_fifo": round(int(st[37]) / ev, 4),
-                      "cycles_ranked_simulated_heaped": [int(st[38]), int(st[40]), int(st[39])]}, indent=1))
+                      "next_event_emitted_by_previous_fifo": round(int(st[37]) / ev, 4)}, indent=1))
 
 
 if __name__ == "__main__":
