@@ -843,9 +843,18 @@ K10S_HELPER void aq_push(Ctx& c, const QInfo& q) {
     aq_sift_up(c, 0, old, q);
 }
 // (Round 3 tried reading the 3-level subtree under the walk's position in one round trip below the
-// LDS levels: C3 +0.6 %, backlog -2 to -4 % from the extra SGPRs live in the scheduling cycle,
-// profiles/r03_k4_sflag_subtree_ab.json; not kept.)
-K10S_HELPER QInfo aq_pop(Ctx& c) {
+// LDS levels, into wave-uniform registers: C3 +0.6 %, backlog -2 to -4 % from the extra SGPRs live in
+// the scheduling cycle, profiles/r03_k4_sflag_subtree_ab.json; not kept.  K10S_AQ_BATCH below keeps
+// the subtree in VGPR lanes instead.)
+#ifndef K10S_AQ_BATCH
+#define K10S_AQ_BATCH 0
+#endif
+#if K10S_AQ_BATCH == 2
+#define K10S_AQ_POP_ATTR K10S_HD_NOINL
+#else
+#define K10S_AQ_POP_ATTR K10S_HELPER
+#endif
+K10S_AQ_POP_ATTR QInfo aq_pop(Ctx& c) {
     K10S_HSTAT(HS_AQ_POP);
     const uint32_t end = --c.H().aq_size;
     QInfo item = aq_get(c, end);
@@ -855,6 +864,47 @@ K10S_HELPER QInfo aq_pop(Ctx& c) {
     uint32_t pos = 0;
     uint32_t child = 1;
     [[maybe_unused]] uint32_t it = 0;
+#if K10S_DEVICE && K10S_AQ_BATCH
+    // Three levels per memory round trip: lane r < 14 loads node r of the depth-3 subtree under pos
+    // (level d = 1, 2, 3 at lanes 0-1, 2-5, 6-13; heap position ((pos + 1) << d) - 1 + j), the walk
+    // compares the two candidate children of each level by readlane of their time keys, and every
+    // lane whose entry moves up stores it at its new position in one masked store.  The walk itself
+    // is the loop below, unchanged (same comparisons, same moves).
+    {
+        const uint32_t lane = (uint32_t)lane_id();
+        const uint32_t d = lane < 2u ? 1u : lane < 6u ? 2u : 3u;
+        const uint32_t j = lane + 2u - (1u << d);
+        while (end >= 2 && child <= end - 2) {
+            if (K10S_LOOP_CAP(it, 40, XG_LOOP_AQ_POP)) break;
+            const uint32_t q = ((pos + 1u) << d) - 1u + j;
+            QInfo x;
+            x.timestamp = 0.0;
+            x.initial = 0.0;
+            x.attempts = 0;
+            x.pod = 0;
+            if (lane < 14u && q < end) x = aq_raw(c, q);
+            const uint64_t kx = (uint64_t)total_key(x.timestamp);
+            const uint32_t klo = (uint32_t)kx, khi = (uint32_t)(kx >> 32);
+            uint32_t dest = 0xFFFFFFFFu;
+            uint32_t jc = 0;   // the walk's node within its subtree level
+            K10S_UNROLL
+            for (uint32_t lv = 1; lv <= 3u; lv++) {
+                if (!(child <= end - 2)) break;
+                const uint32_t la = (1u << lv) - 2u + 2u * jc;
+                const int64_t ka = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)khi, (int)la) << 32) |
+                                             (uint32_t)__builtin_amdgcn_readlane((int)klo, (int)la));
+                const int64_t kb = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)khi, (int)(la + 1u)) << 32) |
+                                             (uint32_t)__builtin_amdgcn_readlane((int)klo, (int)(la + 1u)));
+                const uint32_t pick = kb <= ka ? 1u : 0u;   // q_le(a, b): the right child
+                dest = lane == la + pick ? pos : dest;
+                pos = child + pick;
+                child = 2u * pos + 1u;
+                jc = 2u * jc + pick;
+            }
+            if (dest != 0xFFFFFFFFu) aq_put(c, dest, x);
+        }
+    }
+#endif
     while (end >= 2 && child <= end - 2) {
         if (K10S_LOOP_CAP(it, 40, XG_LOOP_AQ_POP)) break;
         const QInfo a = aq_raw(c, child), b = aq_raw(c, child + 1);
@@ -3506,19 +3556,6 @@ K10S_HD void consume_source(Ctx& c, int src, uint32_t ntr) {
             H.sl[0].key = key;
             H.sl[0].seq = seq;
             K10S_HSTAT(HS_SL_FAST);
-            return;
-        }
-        // the new head falls between sl[1] and sl[2] (64 % of the list updates at C3,
-        // tools/host_stats.py): sl[1] moves to the front and src takes its place — the list
-        // sl_update would build, without the lane-parallel pass
-        const int64_t k2 = (int64_t)uniform_u64((uint64_t)H.sl[2].key);
-        const uint32_t s2 = uniform_u32(H.sl[2].seq);
-        if (n <= 2 || sl_less(key, seq, k2, s2)) {
-            H.sl[0] = H.sl[1];
-            H.sl[1].key = key;
-            H.sl[1].seq = seq;
-            H.sl[1].src = (uint32_t)src;
-            K10S_HSTAT(HS_SLPOS0 + 1);
             return;
         }
     }

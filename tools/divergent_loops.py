@@ -61,7 +61,7 @@ def divergent_loops(asm_lines, kernel=KERNEL):
         for j in range(st, en):
             l = asm_lines[j]
             if l.startswith(".LBB") or l.startswith("; %bb."):
-                inside = j == h or tag in l
+                inside = j == h or re.search(re.escape(tag) + r"\b", l) is not None   # BBx_1 is not BBx_15
             if inside:
                 body.append(l)
         inner = any("Inner Loop Header" in x for x in comment)
