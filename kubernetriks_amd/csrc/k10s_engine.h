@@ -135,26 +135,6 @@ K10S_D DevConstPtr dc_ptr() {
 }
 #define K10S_DC (*dc_ptr())
 #endif
-// The run kernel's arguments, passed as one struct (so that it sits at the start of the kernarg
-// segment).  The event loop reads the per-launch ones (mode, time limits, budget) through an opaque
-// copy of the kernarg pointer, like the launch constants above: scalar loads where they are used,
-// instead of 7 SGPRs live across the loop and saved around every handler call (120 -> 88 lane
-// spills and scratch accesses in the run kernel).
-struct RunArgs {
-    uint32_t n_replicas;
-    int mode;
-    double until_time, max_time;
-    uint64_t budget;
-    uint32_t* active;
-};
-#if K10S_DEVICE
-typedef const __attribute__((address_space(4))) RunArgs* RunArgsPtr;
-K10S_D RunArgsPtr ra_ptr() {
-    RunArgsPtr p = (RunArgsPtr)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(p));
-    return p;
-}
-#endif
 
 // Typed accessors over one replica's region; section bases are recomputed from the (constant)
 // layout at each use instead of being held live across the event loop.
@@ -3708,18 +3688,8 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
 #define ntr (c.S().n_trace)
 #define cap_log (c.Ly().cap_log)
     // one time limit per mode (until_time / max_time)
-#if K10S_DEVICE   // (the arguments as the kernel received them, read at each use: RunArgs above)
-    (void)mode;
-    (void)until_time;
-    (void)max_time;
-    (void)budget;
-#define until_mode0 (ra_ptr()->mode == K10S_RUN_UNTIL_TIME ? 1u : 0u)
-#define limit (ra_ptr()->mode == K10S_RUN_UNTIL_TIME ? ra_ptr()->until_time : ra_ptr()->max_time)
-#define budget (ra_ptr()->budget)
-#else
     const uint32_t until_mode0 = mode == K10S_RUN_UNTIL_TIME ? 1u : 0u;
     const double limit = until_mode0 ? until_time : max_time;
-#endif
     auto until_mode = [&]() -> bool { return until_mode0 != 0; };
     uint64_t done = 0;
     int more = 0;
@@ -3898,11 +3868,6 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
     return more;
 #undef ntr
 #undef cap_log
-#if K10S_DEVICE
-#undef until_mode0
-#undef limit
-#undef budget
-#endif
 }
 
 }  // namespace k10s

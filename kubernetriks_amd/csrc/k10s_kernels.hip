@@ -89,9 +89,10 @@ __global__ __launch_bounds__(64) void k10s_init_kernel(uint32_t n_replicas) {
     hdr_copy(hdr_global(r), (const uint32_t*)&k10s_hdr);
 }
 
-__global__ K10S_RUN_BOUNDS void k10s_run_kernel(RunArgs ra) {
+__global__ K10S_RUN_BOUNDS void k10s_run_kernel(uint32_t n_replicas, int mode, double until_time, double max_time,
+                                                uint64_t budget, uint32_t* active) {
     uint32_t r = blockIdx.x;
-    if (r >= ra.n_replicas) return;
+    if (r >= n_replicas) return;
 #if K10S_WALL
     // tooling builds only: launch wall-time placement of each replica (100 MHz realtime counter,
     // hardware ids) in the profile slots, for the finish-time spread of one resident round
@@ -100,7 +101,7 @@ __global__ K10S_RUN_BOUNDS void k10s_run_kernel(RunArgs ra) {
     sec_setup(r);
     hdr_copy((uint32_t*)&k10s_hdr, hdr_global(r));
     Ctx c;
-    int more = run_replica(c, ra.mode, ra.until_time, ra.max_time, ra.budget);
+    int more = run_replica(c, mode, until_time, max_time, budget);
     (void)more;
 #if K10S_WALL
     if (threadIdx.x == 0) {
@@ -117,6 +118,7 @@ __global__ K10S_RUN_BOUNDS void k10s_run_kernel(RunArgs ra) {
         __hip_atomic_store(k10s_beacon + (uint64_t)r * K10S_BEACON_WORDS + 13, 1u, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
 #endif
+    (void)active;   // the same pointer, read after the loop through the constant block
 #if K10S_DEVICE
     if (more && threadIdx.x == 0) atomicAdd(K10S_DC.active, 1u);
 #endif
@@ -199,14 +201,8 @@ hipError_t k10s_launch_run(const void* h_dcv, uint32_t n_replicas, int mode, dou
     e = hipGetSymbolAddress(&board, HIP_SYMBOL(k10s_fair_board));
     if (e == hipSuccess) e = hipMemsetAsync(board, 0, sizeof(k10s_fair_board), s);
     if (e != hipSuccess) return e;
-    RunArgs ra;
-    ra.n_replicas = n_replicas;
-    ra.mode = mode;
-    ra.until_time = until_time;
-    ra.max_time = max_time;
-    ra.budget = budget;
-    ra.active = d_active;   // (read after the loop through the constant block: K10S_DC.active)
-    hipLaunchKernelGGL(k10s_run_kernel, dim3(n_replicas), dim3(64), 0, s, ra);
+    hipLaunchKernelGGL(k10s_run_kernel, dim3(n_replicas), dim3(64), 0, s, n_replicas, mode, until_time, max_time,
+                       budget, d_active);
     return hipGetLastError();
 }
 

@@ -48,7 +48,7 @@ def test_event_loop_is_uniform(loops, variant, plugins):
 
 def test_detects_a_divergent_event_loop():
     """The analysis flags round 3's shape: a structurized loop nested in the event loop."""
-    asm = """_Z15k10s_run_kernelN4k10s7RunArgsE:
+    asm = """_Z15k10s_run_kerneljiddmPj:
 .LBB1_1:                                ; =>This Inner Loop Header: Depth=1
 \tv_add_u32 v0, 1, v0
 \ts_andn2_b64 exec, exec, s[4:5]

@@ -17,12 +17,11 @@ import subprocess
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "_Z15k10s_run_kernel"   # mangled-name prefix (the argument list follows)
+KERNEL = "_Z15k10s_run_kerneljiddmPj"
 
 
 def divergent_loops(asm_lines, kernel=KERNEL):
-    st = next(i for i, l in enumerate(asm_lines) if l.startswith(kernel) and l.split(":")[0].startswith(kernel)
-              and not l.startswith("\t"))
+    st = next(i for i, l in enumerate(asm_lines) if l.startswith(kernel + ":"))
     en = next(i for i in range(st, len(asm_lines)) if asm_lines[i].startswith(".Lfunc_end"))
     labels = {}
     for i in range(st, en):
@@ -76,7 +75,7 @@ def divergent_loops(asm_lines, kernel=KERNEL):
 def compile_and_check(flags, plugins=False):
     """Divergent loops of the run kernel of one translation unit (k10s_kernels.hip, or with
     plugins=True the plugin-scoring k10s_kernels_plugins.hip) built with the product flags + flags."""
-    src, kernel = ("k10s_kernels_plugins.hip", "_Z23k10s_run_kernel_plugins") if plugins else \
+    src, kernel = ("k10s_kernels_plugins.hip", "_Z23k10s_run_kernel_pluginsjiddmPj") if plugins else \
         ("k10s_kernels.hip", KERNEL)
     out_s = "/tmp/k10s_divergent_loops_%d_%d.s" % (os.getpid(), abs(hash((tuple(flags), plugins))))
     cmd = ["hipcc", "-O3", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950", "--cuda-device-only", "-S",
