@@ -843,18 +843,11 @@ K10S_HELPER void aq_push(Ctx& c, const QInfo& q) {
     aq_sift_up(c, 0, old, q);
 }
 // (Round 3 tried reading the 3-level subtree under the walk's position in one round trip below the
-// LDS levels, into wave-uniform registers: C3 +0.6 %, backlog -2 to -4 % from the extra SGPRs live in
-// the scheduling cycle, profiles/r03_k4_sflag_subtree_ab.json; not kept.  K10S_AQ_BATCH below keeps
-// the subtree in VGPR lanes instead.)
-#ifndef K10S_AQ_BATCH
-#define K10S_AQ_BATCH 0
-#endif
-#if K10S_AQ_BATCH == 2
-#define K10S_AQ_POP_ATTR K10S_HD_NOINL
-#else
-#define K10S_AQ_POP_ATTR K10S_HELPER
-#endif
-K10S_AQ_POP_ATTR QInfo aq_pop(Ctx& c) {
+// LDS levels into wave-uniform registers: C3 +0.6 %, backlog -2 to -4 % from the extra SGPRs live in
+// the scheduling cycle, profiles/r03_k4_sflag_subtree_ab.json.  Round 4 keeps the subtree in VGPR
+// lanes instead (below): backlog +8.7 %, C3 +0.2 %; the same pop out of line lost 1.5-2 % on C3,
+// profiles/r04_h11_aq_batch_ab.json.)
+K10S_HELPER QInfo aq_pop(Ctx& c) {
     K10S_HSTAT(HS_AQ_POP);
     const uint32_t end = --c.H().aq_size;
     QInfo item = aq_get(c, end);
@@ -864,7 +857,7 @@ K10S_AQ_POP_ATTR QInfo aq_pop(Ctx& c) {
     uint32_t pos = 0;
     uint32_t child = 1;
     [[maybe_unused]] uint32_t it = 0;
-#if K10S_DEVICE && K10S_AQ_BATCH
+#if K10S_DEVICE
     // Three levels per memory round trip: lane r < 14 loads node r of the depth-3 subtree under pos
     // (level d = 1, 2, 3 at lanes 0-1, 2-5, 6-13; heap position ((pos + 1) << d) - 1 + j), the walk
     // compares the two candidate children of each level by readlane of their time keys, and every
