@@ -823,41 +823,6 @@ K10S_HD void aq_put(Ctx& c, uint32_t i, const QInfo& q) {
 K10S_HD uint32_t aq_sift_up(Ctx& c, uint32_t start, uint32_t pos, const QInfo& elem) {
     [[maybe_unused]] uint32_t it = 0;
     const int64_t ke = aq_ts(elem);
-#if K10S_DEVICE
-    if (start == 0 && pos > 0) {
-        // the first step as the loop takes it: most pushes stop at the parent (arrivals come in
-        // time order), and one entry is all they read
-        const uint32_t parent = (pos - 1) / 2;
-        const QInfo p = aq_raw(c, parent);
-        if (ke >= aq_ts(p)) {
-            aq_put(c, pos, elem);
-            return pos;
-        }
-        aq_put(c, pos, p);
-        pos = parent;
-    }
-    if (start == 0) {
-        // The rest in one memory round trip: lane k loads pos's k-th ancestor ((pos + 1) >> (k + 1)) - 1; the
-        // Rust loop stops at the first ancestor going up whose key is <= the element's (elem <= it
-        // in the queue's Ord), so that ancestor is the lowest set bit of one ballot; the ancestors
-        // below it each move down to their child on the path (one store per lane) and the element
-        // takes the highest vacated position.
-        const uint32_t lane = (uint32_t)lane_id();
-        const uint32_t depth = 31u - (uint32_t)__builtin_clz(pos + 1u);   // ancestors of pos
-        QInfo x;
-        x.timestamp = 0.0;
-        x.initial = 0.0;
-        x.attempts = 0;
-        x.pod = 0;
-        if (lane < depth) x = aq_raw(c, ((pos + 1u) >> (lane + 1u)) - 1u);
-        const uint64_t stop = __ballot(lane < depth && total_key(x.timestamp) <= ke);
-        const uint32_t moved = stop ? (uint32_t)__builtin_ctzll(stop) : depth;
-        if (lane < moved) aq_put(c, ((pos + 1u) >> lane) - 1u, x);
-        const uint32_t fin = ((pos + 1u) >> moved) - 1u;
-        aq_put(c, fin, elem);
-        return fin;
-    }
-#endif
     while (pos > start) {
         if (K10S_LOOP_CAP(it, 40, XG_LOOP_AQ_UP)) break;
         uint32_t parent = (pos - 1) / 2;
