@@ -389,7 +389,11 @@ enum : int { PROF_LOOP = 0, PROF_SELECT = 1, PROF_CONSUME = 2, PROF_DISPATCH = 3
              PROF_NEMIT = 12, PROF_AQPUSH = 13 };
 K10S_HD uint64_t prof_now() {
 #if K10S_PROF && K10S_DEVICE
-    return (uint64_t)__builtin_readcyclecounter();
+    // an ordered read (volatile, memory clobber): the builtin's reads could move across the code they
+    // bracket once that code was inlined (round 4's c5_autoscaled profile had a corrupt phase slot)
+    uint64_t t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+    return t;
 #else
     return 0;
 #endif
@@ -953,7 +957,63 @@ K10S_HD bool pod_in_s(const Ctx& c, uint32_t p) { return c.V().pod(p).sflag != 0
 // move_pods_to_active_queue over a selection, in key order (scheduler.rs:174-185)
 // mode 0: all (move_all_to_active_queue, 235-244); 1: flush (188-203, stay > 300 s);
 // 2: freed-resources conditional (366-379); 3: inverted add-node conditional (396-405).
+#if K10S_DEVICE
+// move_all_to_active_queue on the device (scheduler.rs:235-244), out of line: the map's entries are
+// read 64 at a time, one per lane, with their pods' cache flags (two memory round trips per 64
+// entries instead of two per entry), then moved or kept in key order exactly as the loop below does
+// (the entries of a batch come out of the lanes by readlane).  The backlog workload requeues the
+// whole unschedulable map on every pod finish.
+__device__ __attribute__((noinline)) void s_move_all_dev(Ctx& c) {
+    QInfo* d = c.V().uq();
+    const uint32_t n = uniform_u32(c.H().uq_size);
+    const uint32_t lane = (uint32_t)lane_id();
+    uint32_t w = 0;
+    uint64_t moved = 0;
+    auto rl = [](uint32_t v, uint32_t j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j); };
+    for (uint32_t base = 0; base < n; base += 64u) {
+        const uint32_t cnt = n - base < 64u ? n - base : 64u;
+        QInfo x;
+        x.timestamp = 0.0;
+        x.initial = 0.0;
+        x.attempts = 0;
+        x.pod = 0;
+        uint32_t in_s = 0;
+        if (lane < cnt) {
+            x = d[base + lane];
+            in_s = c.V().pod(x.pod).sflag;
+        }
+        const uint64_t live = __ballot(lane < cnt && in_s != 0);
+        const uint64_t ts = f2u(x.timestamp), ti = f2u(x.initial);
+        for (uint32_t j = 0; j < cnt; j++) {
+            QInfo q;
+            q.timestamp = u2f(((uint64_t)rl((uint32_t)(ts >> 32), j) << 32) | rl((uint32_t)ts, j));
+            q.initial = u2f(((uint64_t)rl((uint32_t)(ti >> 32), j) << 32) | rl((uint32_t)ti, j));
+            q.attempts = rl(x.attempts, j);
+            q.pod = rl(x.pod, j);
+            if ((live >> j) & 1u) {
+                q.attempts += 1;
+                aq_push(c, q);
+                if (c.H().error_code) {
+                    c.H().counters[K10S_C_REQUEUED] += moved;
+                    return;
+                }
+                moved += 1;
+            } else {
+                d[w++] = q;  // a stale entry of a deleted pod stays
+            }
+        }
+    }
+    c.H().counters[K10S_C_REQUEUED] += moved;
+    c.H().uq_size = w;
+}
+#endif
 K10S_HELPER void s_move(Ctx& c, int mode, double t, uint32_t cpu, uint64_t ram) {
+#if K10S_DEVICE
+    if (mode == 0) {
+        if (uniform_u32(c.H().uq_size) != 0) s_move_all_dev(c);
+        return;
+    }
+#endif
     QInfo* d = c.V().uq();
     uint32_t n = c.H().uq_size;
     uint32_t w = 0;
