@@ -86,6 +86,34 @@ def test_fuzz_gpu(seed):
     _fuzz("gpu", seed)
 
 
+# Wide random scenarios: 50-200 nodes (node caches of one to four 64-lane scan steps, where the
+# small sweep above never leaves the first step) and 200-800 pods over a 1,200 s horizon, with and
+# without removals.  K10S_FUZZ_WIDE_GPU_SEEDS=N widens the GPU sweep.
+FUZZ_WIDE_HOST = list(range(10_000, 10_024))
+FUZZ_WIDE_GPU = list(range(10_000, 10_000 + int(os.environ.get("K10S_FUZZ_WIDE_GPU_SEEDS", "24"))))
+
+
+def _fuzz_wide(backend, seed):
+    rng = random.Random(seed)
+    kw = dict(ca=(seed % 3 == 1), hpa=(seed % 4 == 2), removals=(seed % 2 == 0))
+    scn = gen.random_scenario(seed, n_pods=rng.choice([200, 400, 800]), n_nodes=rng.randint(50, 200),
+                              horizon=1200.0, **kw)
+    mode = RUN_UNTIL_TIME if kw["hpa"] else RUN_UNTIL_ALL_FINISHED
+    od, eng = parity.run_pair(engine_cls(backend), scn, mode=mode, until=3000.0, max_time=20000.0)
+    assert parity.compare(od, eng) == [], seed
+
+
+@pytest.mark.parametrize("seed", FUZZ_WIDE_HOST)
+def test_fuzz_wide_host(seed):
+    _fuzz_wide("host", seed)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", FUZZ_WIDE_GPU)
+def test_fuzz_wide_gpu(seed):
+    _fuzz_wide("gpu", seed)
+
+
 # Delay-class FIFO rings are an optimisation of the event queue: tiny rings (constant spill to the
 # heap), one-entry rings and no rings at all must deliver the identical event sequence.
 FIFO_CASES = [(seed, fifo) for seed in (1, 4, 6, 10, 13, 22) for fifo in (1, 2, 0xFFFFFFFF)]
