@@ -83,6 +83,21 @@ def test_plugin_sets_match_oracle(backend, seed):
 
 
 @pytest.mark.parametrize("backend", BACKENDS)
+@pytest.mark.parametrize("seed", range(8))
+def test_plugin_sets_wide_match_oracle(backend, seed):
+    """The same profiles over 70-200 mixed-size nodes (two to four 64-lane scan steps of the plugin
+    kernel's scan), 300 pods, removals on even seeds."""
+    plugins = (SCORE_MOST_ALLOCATED, SCORE_LEAST_ALLOCATED | SCORE_MOST_ALLOCATED)[seed % 2]
+    w_la, w_ma = [(None, None), (0.37, 1.9), (1.0, -2.5), (2.0, 0.0)][seed % 4]
+    n_nodes = 70 + (seed * 37) % 131
+    scn = with_plugins(gen.random_scenario(500 + seed, n_pods=300, n_nodes=n_nodes, horizon=1200.0,
+                                           same_nodes=False, removals=(seed % 2 == 0), ca=(seed % 3 == 0)),
+                       plugins, w_la, w_ma)
+    od, eng = parity.run_pair(engine_cls(backend), scn, max_time=40000.0)
+    assert parity.compare(od, eng) == [], (seed, plugins)
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
 def test_per_replica_plugin_sweep(backend):
     """One batch, replicas differing only in score plugins / weights (k10s_replica_params), each
     equal to the oracle on the scenario with that profile."""
