@@ -200,6 +200,18 @@ def test_budgeted_launches_equal_one_launch(backend):
 
 
 @pytest.mark.parametrize("backend", BACKENDS)
+@pytest.mark.parametrize("seed,budget", [(10_001, 37), (10_004, 101), (10_007, 1), (10_010, 513)])
+def test_budgeted_wide_scenarios_match_oracle(backend, seed, budget):
+    """Wide random scenarios (_fuzz_wide's shapes, without HPA) paused every `budget` events, each
+    resumed launch re-reading the replica from HBM, against the oracle's single run."""
+    rng = random.Random(seed)
+    scn = gen.random_scenario(seed, n_pods=rng.choice([200, 400, 800]), n_nodes=rng.randint(50, 200),
+                              horizon=1200.0, ca=(seed % 3 == 1), removals=(seed % 2 == 0))
+    od, eng = parity.run_pair(engine_cls(backend), scn, max_time=20000.0, budget=budget)
+    assert parity.compare(od, eng) == [], (seed, budget)
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
 def test_batched_replicas_match_oracle_per_replica(backend):
     """R seed-perturbed replicas in one batch: each equals the oracle on its materialized trace."""
     c, w = wl.c3_traces(n_nodes=256, n_pods=600, arrival_window=300.0, seed=5)
