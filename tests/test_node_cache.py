@@ -39,6 +39,23 @@ def test_wide_layout_matches_oracle(backend, seed):
     assert parity.compare(od, eng) == [], seed
 
 
+@pytest.mark.parametrize("backend", BACKENDS)
+@pytest.mark.parametrize("seed", range(10_000, 10_012))
+def test_wide_layout_multi_step_scans_match_oracle(backend, seed):
+    """test_engine_parity's wide random scenarios (50-200 nodes: one to four 64-lane scan steps)
+    forced onto the wide layout."""
+    import random
+    rng = random.Random(seed)
+    kw = dict(ca=(seed % 3 == 1), hpa=(seed % 4 == 2), removals=(seed % 2 == 0))
+    scn = gen.random_scenario(seed, n_pods=rng.choice([200, 400, 800]), n_nodes=rng.randint(50, 200),
+                              horizon=1200.0, **kw)
+    mode = RUN_UNTIL_TIME if kw["hpa"] else RUN_UNTIL_ALL_FINISHED
+    od, eng = parity.run_pair(engine_cls(backend), scn, mode=mode, until=3000.0, max_time=20000.0,
+                              node_cache=WIDE)
+    assert eng.node_entry_bytes == 12
+    assert parity.compare(od, eng) == [], seed
+
+
 def edge_scenario(cpu: int, ram: int, seed: int = 0) -> str:
     """Nodes at (and one step below) the given capacities, pods sized so nodes fill up, release and
     refill: allocatable crosses every field value from 0 to the capacity."""
