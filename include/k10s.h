@@ -355,6 +355,16 @@ int32_t k10s_engine_pod_records(const k10s_engine* e, uint32_t replica, k10s_pod
 int32_t k10s_engine_group_sizes(const k10s_engine* e, uint32_t replica, uint32_t* created, uint32_t* total,
                                 uint32_t cap, uint32_t* n);
 
+/* Generated-name universes of the compiled batch: names per pod group ("{group}_{k}", the HPA's pods)
+   and per CA node group ("{group}_{k}").  k10s_capacities.group_name_bound / ca_name_bound set the
+   first universe (0 = derived from the scenario).  The reference bounds neither
+   (kube_horizontal_pod_autoscaler.rs:178-182, api_server.rs:421); when a replica would create a name
+   beyond its universe (K10S_ERR_NAME_BOUND), k10s_engine_run / k10s_engine_sync recompile the batch
+   with that universe doubled (up to 2^20 names) and replay every run call since the last
+   initialize, so results equal the reference's; the name tables below then describe the regrown
+   batch (re-read them after a run). */
+int32_t k10s_engine_name_bounds(const k10s_engine* e, uint32_t* group_bound, uint32_t* ca_bound);
+
 /* Name tables of the compiled scenario (index -> name), for mapping logs back to names. */
 uint32_t k10s_engine_num_nodes(const k10s_engine* e);
 uint32_t k10s_engine_num_pods(const k10s_engine* e);

@@ -610,12 +610,16 @@ bool build_scenario(const std::string& text, uint32_t group_bound_in, uint32_t c
             wt.push_back(e);
         }
         // initialize emits every trace event at delay = its timestamp (simulator.rs:234-253): dslab-core
-        // refuses a negative (or NaN) delay with a panic, so such a trace never starts a simulation
+        // refuses a negative (or NaN) delay with a panic, so such a trace never starts a simulation.
+        // The scenario is refused as a whole, at compile time, even when the event lies past some
+        // replica's workload_prefix (that replica alone would not emit it): one compiled scenario
+        // serves every replica of the batch.
         for (const std::vector<TraceEv>* v : {&ct, &wt})
             for (const TraceEv& t : *v)
                 if (!(t.time >= 0.0))
                     throw std::runtime_error("trace event at a negative (or NaN) timestamp: the reference panics in "
-                                             "initialize (dslab-core refuses an event delay < 0)");
+                                             "initialize (dslab-core refuses an event delay < 0); refused for the "
+                                             "whole batch, whatever the replicas' workload_prefix");
         hs.trace.resize(ct.size() + wt.size());
         std::merge(ct.begin(), ct.end(), wt.begin(), wt.end(), hs.trace.begin(), [](const TraceEv& a, const TraceEv& b) {
             int64_t ka = total_key(a.time), kb = total_key(b.time);

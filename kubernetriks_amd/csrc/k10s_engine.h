@@ -1707,6 +1707,10 @@ K10S_HD int schedule_scan_pruned(Ctx& c, uint32_t rc, uint64_t rr, int32_t* chos
         uint64_t k = bkey;
         int32_t bi = bkey ? (int32_t)lane : -1;
         wave_argmax(k, bi);
+        // every lane holds the reduced pair; saying so keeps this loop's branches scalar (a divergent
+        // structurization would run the next wave_argmax under a partial EXEC: tools/divergent_loops.py)
+        k = uniform_u64(k);
+        bi = (int32_t)uniform_u32((uint32_t)bi);
         if (k == 0) break;
         if (best_n >= 0 && (k < best_key || (k == best_key && (int32_t)(((uint32_t)bi + 1u) << sh) <= best_n))) break;
         const uint32_t lo = (uint32_t)bi << sh;
@@ -1728,6 +1732,8 @@ K10S_HD int schedule_scan_pruned(Ctx& c, uint32_t rc, uint64_t rr, int32_t* chos
         }
         touched += hi - lo;
         wave_argmax(lk, ln);
+        lk = uniform_u64(lk);
+        ln = (int32_t)uniform_u32((uint32_t)ln);
         if (ln >= 0 && (lk > best_key || (lk == best_key && ln > best_n))) {
             best_key = lk;
             best_n = ln;

@@ -2,6 +2,7 @@
 // memory, launches, result readback.  Requires a HIP device; there is no CPU fallback.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -43,7 +44,9 @@ int32_t set_err(int32_t code, const std::string& msg) {
     } while (0)
 }  // namespace
 
-struct k10s_engine {
+// Everything one compiled batch owns on the device and the host.  Kept apart from the handle so a
+// regrown batch (more generated names, see regrow below) can take the handle's place in one swap.
+struct EngineCore {
     HostScenario hs;
     Scenario dsc;       // device view
     Layout L;
@@ -53,17 +56,33 @@ struct k10s_engine {
     void* d_scen = nullptr;
     uint8_t* d_state = nullptr;
     Params* d_params = nullptr;
-    uint32_t* d_active = nullptr;
+    uint32_t* d_active = nullptr;  // [0] replicas with work left, [1] a replica stopped at a name bound
     uint32_t* h_active = nullptr;  // pinned
     RepHdr* h_hdr = nullptr;       // pinned staging for the replica headers (results / profile readback),
                                    // allocated at create; hdr_mu serializes its fill-and-read
-    std::mutex hdr_mu;
     DevConst* h_dc = nullptr;      // pinned launch constants
     std::vector<Params> params;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool plugins = false;          // some replica's profile is not LeastAllocated alone
     bool wide = false;             // launch the wide-cache kernel copy (k10s_kernels_plugins.hip): a
                                    // plugin replica, or a node cache that is not packed (L.packed == 0)
+};
+
+// One call that advanced the replicas since the last initialize: a regrown batch replays them.
+struct RunCall {
+    int32_t mode;
+    double until_time, max_time;
+    uint64_t budget;
+    bool single;   // one launch (k10s_engine_step_async) rather than a launch loop (k10s_engine_run)
+};
+
+struct k10s_engine : EngineCore {
+    std::mutex hdr_mu;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // what the batch was compiled from (a regrow recompiles it with larger name universes)
+    std::string text;
+    std::vector<uint8_t> blob;
+    k10s_capacities caps;
+    std::vector<RunCall> history;
 };
 
 // All engines of a device launch on one stream: the launch constants are one __constant__ block per
@@ -78,26 +97,190 @@ static hipStream_t engine_stream(int device) {
     return streams[device];
 }
 
-static void engine_free(k10s_engine* e) {
-    if (!e) return;
-    (void)hipSetDevice(e->device);
-    if (e->d_scen) (void)hipFree(e->d_scen);
-    if (e->d_state) (void)hipFree(e->d_state);
-    if (e->d_params) (void)hipFree(e->d_params);
-    if (e->d_active) (void)hipFree(e->d_active);
-    if (e->h_active) (void)hipHostFree(e->h_active);
-    if (e->h_hdr) (void)hipHostFree(e->h_hdr);
-    if (e->h_dc) (void)hipHostFree(e->h_dc);
-    if (e->ev0) (void)hipEventDestroy(e->ev0);
-    if (e->ev1) (void)hipEventDestroy(e->ev1);
-    delete e;  // e->stream is the device's shared engine stream: not destroyed
+static void core_free(EngineCore& e) {
+    (void)hipSetDevice(e.device);
+    if (e.d_scen) (void)hipFree(e.d_scen);
+    if (e.d_state) (void)hipFree(e.d_state);
+    if (e.d_params) (void)hipFree(e.d_params);
+    if (e.d_active) (void)hipFree(e.d_active);
+    if (e.h_active) (void)hipHostFree(e.h_active);
+    if (e.h_hdr) (void)hipHostFree(e.h_hdr);
+    if (e.h_dc) (void)hipHostFree(e.h_dc);
+    e.d_scen = nullptr;
+    e.d_state = nullptr;
+    e.d_params = nullptr;
+    e.d_active = e.h_active = nullptr;
+    e.h_hdr = nullptr;
+    e.h_dc = nullptr;   // e.stream is the device's shared engine stream: not destroyed
 }
 
-static int32_t engine_init(k10s_engine* e) {
+static void engine_free(k10s_engine* e) {
+    if (!e) return;
+    core_free(*e);
+    if (e->ev0) (void)hipEventDestroy(e->ev0);
+    if (e->ev1) (void)hipEventDestroy(e->ev1);
+    delete e;
+}
+
+static int32_t core_init(EngineCore& e) {
+    HIPCHK(hipSetDevice(e.device));
+    HIPCHK(hipMemsetAsync(e.d_active, 0, 8, e.stream));
+    HIPCHK((e.wide ? k10s_launch_init_plugins : k10s_launch_init)(e.h_dc, e.R, e.stream));
+    HIPCHK(hipStreamSynchronize(e.stream));
+    return K10S_OK;
+}
+
+// Compile the scenario and allocate + initialize the batch.  params: n_replicas entries, or NULL for
+// the scenario defaults.  Returns K10S_OK or an error code (message in g_err); on failure the core
+// holds nothing the caller must free beyond what core_free releases.
+static int32_t core_create(EngineCore& e, const char* text, const uint8_t* blob, uint64_t blob_len,
+                           const k10s_replica_params* params, uint32_t n_replicas, const k10s_capacities& c,
+                           int32_t device) {
+    e.device = device;
+    e.R = n_replicas;
+    std::string err;
+    if (!build_scenario(text, c.group_name_bound, c.ca_name_bound, e.hs, err, blob, blob_len))
+        return set_err(K10S_E_INVALID, "scenario: " + err);
+    e.params.resize(n_replicas);
+    for (uint32_t r = 0; r < n_replicas; r++) {
+        if (params) {
+            e.params[r] = params[r];
+        } else {
+            e.params[r] = e.hs.defaults;
+            e.params[r].seed = e.hs.defaults.seed + r;
+        }
+        e.params[r].ca_max_node_count = e.hs.defaults.ca_max_node_count;  // fixed by the node pool
+        if (e.params[r].score_plugins != K10S_SCORE_LEAST_ALLOCATED) e.plugins = true;
+        const std::string perr = params_error(e.params[r], e.hs);
+        if (!perr.empty()) return set_err(K10S_E_INVALID, "params[" + std::to_string(r) + "]: " + perr);
+    }
+    // the node cache is packed unless some replica needs the wide SoA (k10s_capacities.node_cache)
+    const bool tnn = times_nonneg(e.hs, e.params.data(), n_replicas);
+    e.L = make_layout(e.hs, c, !e.plugins && tnn, tnn);
+    e.wide = e.plugins || !e.L.packed;
+    if (hipSetDevice(device) != hipSuccess) return set_err(K10S_E_HIP, "hipSetDevice");
+    if (!(e.stream = engine_stream(device))) return set_err(K10S_E_HIP, "hipStreamCreate");
+    Scenario offs;
+    std::vector<uint8_t> img = pack_scenario(e.hs, offs);
+    if (hipMalloc(&e.d_scen, img.size()) != hipSuccess) return set_err(K10S_E_HIP, "hipMalloc scenario");
+    if (hipMemcpy(e.d_scen, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess)
+        return set_err(K10S_E_HIP, "upload scenario");
+    e.dsc = rebase_scenario(offs, (const uint8_t*)e.d_scen);
+    size_t bytes = (size_t)e.L.stride * n_replicas;
+    size_t free_b = 0, total_b = 0;
+    (void)hipMemGetInfo(&free_b, &total_b);
+    if (bytes + (64ull << 20) > free_b && c.delay_fifo == 0 && e.L.cap_fq > 512) {
+        // the default rings grow with the node count (up to 8 x 8,192 x 32 B = 2 MiB per replica): when
+        // that does not fit, fall back to 512-entry rings (a fuller ring only spills to the heap)
+        k10s_capacities c512 = c;
+        c512.delay_fifo = 512;
+        e.L = make_layout(e.hs, c512, !e.plugins && tnn, tnn);
+        bytes = (size_t)e.L.stride * n_replicas;
+    }
+    if (bytes + (64ull << 20) > free_b)
+        return set_err(K10S_E_CAPACITY, "replica state (" + std::to_string(bytes >> 20) + " MiB) exceeds free device memory");
+    if (hipMalloc(&e.d_state, bytes) != hipSuccess) return set_err(K10S_E_HIP, "hipMalloc replica state");
+    if (hipMalloc(&e.d_params, sizeof(Params) * n_replicas) != hipSuccess) return set_err(K10S_E_HIP, "hipMalloc params");
+    if (hipMemcpy(e.d_params, e.params.data(), sizeof(Params) * n_replicas, hipMemcpyHostToDevice) != hipSuccess)
+        return set_err(K10S_E_HIP, "upload params");
+    if (hipMalloc(&e.d_active, 64) != hipSuccess) return set_err(K10S_E_HIP, "hipMalloc active");
+    if (hipHostMalloc(&e.h_active, 64) != hipSuccess) return set_err(K10S_E_HIP, "hipHostMalloc");
+    std::memset(e.h_active, 0, 64);
+    if (hipHostMalloc(&e.h_hdr, sizeof(RepHdr) * (size_t)e.R) != hipSuccess) return set_err(K10S_E_HIP, "hipHostMalloc");
+    if (hipHostMalloc(&e.h_dc, sizeof(DevConst)) != hipSuccess) return set_err(K10S_E_HIP, "hipHostMalloc");
+    std::memset(e.h_dc, 0, sizeof(DevConst));
+    e.h_dc->sc = e.dsc;
+    e.h_dc->L = e.L;
+    e.h_dc->params = e.d_params;
+    e.h_dc->base = e.d_state;
+    e.h_dc->active = e.d_active;
+    return core_init(e);
+}
+
+// One launch over every replica (no sync); h_active[0..1] receive the launch's flags when it is done.
+static int32_t core_launch(EngineCore& e, const RunCall& rc) {
+    HIPCHK(hipSetDevice(e.device));
+    HIPCHK(hipMemsetAsync(e.d_active, 0, 4, e.stream));   // word 1 (name bound) stays set until a regrow
+    HIPCHK((e.wide ? k10s_launch_run_plugins : k10s_launch_run)(e.h_dc, e.R, rc.mode, rc.until_time, rc.max_time,
+                                                                 rc.budget, e.d_active, e.stream));
+    HIPCHK(hipMemcpyAsync(e.h_active, e.d_active, 8, hipMemcpyDeviceToHost, e.stream));
+    return K10S_OK;
+}
+
+// One recorded call: a single launch, or launches until no replica has work left.
+static int32_t core_call(EngineCore& e, const RunCall& rc) {
+    for (;;) {
+        int32_t r = core_launch(e, rc);
+        if (r != K10S_OK) return r;
+        HIPCHK(hipStreamSynchronize(e.stream));
+        if (rc.single || rc.budget == 0 || e.h_active[0] == 0) return K10S_OK;
+    }
+}
+
+// All replica headers into the engine's pinned staging buffer (one strided DMA; a pageable
+// destination would be copied through a bounce buffer).  The caller holds e->hdr_mu across the fill
+// and its reads of h_hdr, so concurrent read-back calls on one engine do not interleave.
+static int32_t read_all_hdrs(EngineCore* e) {
     HIPCHK(hipSetDevice(e->device));
-    HIPCHK((e->wide ? k10s_launch_init_plugins : k10s_launch_init)(e->h_dc, e->R, e->stream));
+    HIPCHK(hipMemcpy2DAsync(e->h_hdr, sizeof(RepHdr), e->d_state + e->L.hdr, e->L.stride, sizeof(RepHdr), e->R,
+                            hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     return K10S_OK;
+}
+
+// Generated names without a bound.  The reference names the HPA's pods "{group}_{total_created}"
+// (kube_horizontal_pod_autoscaler.rs:178-182, api_server.rs:421) and the cluster autoscaler's nodes
+// "{group}_{k}" (kube_cluster_autoscaler.rs) with no limit; the engine ranks every name of the run
+// ahead of time (name rank = index), so it compiles a finite universe per group
+// (k10s_capacities.group_name_bound / ca_name_bound, derived from the scenario when 0) and a replica
+// that would create a name beyond it stops with K10S_ERR_NAME_BOUND.  The run kernel flags such a
+// stop (active word 1); this recompiles the batch with the exhausted universe doubled and replays
+// every call since the last initialize on it, until no replica stops there.  Every replica is
+// deterministic, so the others come out identical; the handle keeps its identity (name tables and
+// replica_bytes may grow).  A bound at K10S_NAME_BOUND_MAX is left as the error.
+#define K10S_NAME_BOUND_MAX (1u << 20)
+static int32_t regrow(k10s_engine* e) {
+    for (;;) {
+        if (e->h_active[1] == 0) return K10S_OK;
+        bool grow_ca = false, grow_group = false;
+        {
+            std::lock_guard<std::mutex> g(e->hdr_mu);
+            int32_t rc = read_all_hdrs(e);
+            if (rc != K10S_OK) return rc;
+            for (uint32_t r = 0; r < e->R; r++) {
+                if (e->h_hdr[r].error_code != K10S_ERR_NAME_BOUND) continue;
+                if (e->h_hdr[r].error_kind == K10S_EV_PS_CA_REQ) grow_ca = true;
+                else grow_group = true;
+            }
+        }
+        k10s_capacities c = e->caps;
+        c.group_name_bound = e->hs.group_bound;
+        c.ca_name_bound = e->hs.ca_bound;
+        bool grown = false;
+        if (grow_group && c.group_name_bound < K10S_NAME_BOUND_MAX) {
+            c.group_name_bound = std::min<uint32_t>(2 * std::max<uint32_t>(c.group_name_bound, 32), K10S_NAME_BOUND_MAX);
+            grown = true;
+        }
+        if (grow_ca && c.ca_name_bound < K10S_NAME_BOUND_MAX) {
+            c.ca_name_bound = std::min<uint32_t>(2 * std::max<uint32_t>(c.ca_name_bound, 32), K10S_NAME_BOUND_MAX);
+            grown = true;
+        }
+        if (!grown) {
+            e->h_active[1] = 0;
+            return K10S_OK;
+        }
+        EngineCore n;
+        int32_t rc = core_create(n, e->text.c_str(), e->blob.empty() ? nullptr : e->blob.data(), e->blob.size(),
+                                 e->params.data(), e->R, c, e->device);
+        for (size_t i = 0; rc == K10S_OK && i < e->history.size(); i++) rc = core_call(n, e->history[i]);
+        if (rc != K10S_OK) {
+            core_free(n);
+            return rc;
+        }
+        std::lock_guard<std::mutex> g(e->hdr_mu);
+        std::swap(static_cast<EngineCore&>(*e), n);
+        core_free(n);
+    }
 }
 
 extern "C" {
@@ -258,91 +441,22 @@ k10s_engine* k10s_engine_create_bulk(const char* scenario_text, const void* pods
         set_err(K10S_E_INVALID, "device index out of range");
         return nullptr;
     }
-    k10s_capacities c;
-    std::memset(&c, 0, sizeof c);
-    if (caps) c = *caps;
     auto* e = new k10s_engine();
-    e->device = device;
-    e->R = n_replicas;
-    std::string err;
-    if (!build_scenario(scenario_text, c.group_name_bound, c.ca_name_bound, e->hs, err,
-                        static_cast<const uint8_t*>(pods_blob), blob_len)) {
-        set_err(K10S_E_INVALID, "scenario: " + err);
-        delete e;
-        return nullptr;
+    std::memset(&e->caps, 0, sizeof e->caps);
+    if (caps) e->caps = *caps;
+    e->text = scenario_text;
+    if (pods_blob && blob_len) e->blob.assign((const uint8_t*)pods_blob, (const uint8_t*)pods_blob + blob_len);
+    const int32_t rc = core_create(*e, scenario_text, e->blob.empty() ? nullptr : e->blob.data(), e->blob.size(),
+                                   params, n_replicas, e->caps, device);
+    if (rc == K10S_OK) {
+        (void)hipEventCreate(&e->ev0);
+        (void)hipEventCreate(&e->ev1);
+        return e;
     }
-    e->params.resize(n_replicas);
-    for (uint32_t r = 0; r < n_replicas; r++) {
-        if (params) {
-            e->params[r] = params[r];
-        } else {
-            e->params[r] = e->hs.defaults;
-            e->params[r].seed = e->hs.defaults.seed + r;
-        }
-        e->params[r].ca_max_node_count = e->hs.defaults.ca_max_node_count;  // fixed by the node pool
-        if (e->params[r].score_plugins != K10S_SCORE_LEAST_ALLOCATED) e->plugins = true;
-        const std::string perr = params_error(e->params[r], e->hs);
-        if (!perr.empty()) {
-            set_err(K10S_E_INVALID, "params[" + std::to_string(r) + "]: " + perr);
-            delete e;
-            return nullptr;
-        }
-    }
-    // the node cache is packed unless some replica needs the wide SoA (k10s_capacities.node_cache)
-    const bool tnn = times_nonneg(e->hs, e->params.data(), n_replicas);
-    e->L = make_layout(e->hs, c, !e->plugins && tnn, tnn);
-    e->wide = e->plugins || !e->L.packed;
-    auto fail = [&](const std::string& m) -> k10s_engine* {
-        set_err(K10S_E_HIP, m);
-        engine_free(e);
-        return nullptr;
-    };
-    if (hipSetDevice(device) != hipSuccess) return fail("hipSetDevice");
-    if (!(e->stream = engine_stream(device))) return fail("hipStreamCreate");
-    (void)hipEventCreate(&e->ev0);
-    (void)hipEventCreate(&e->ev1);
-    Scenario offs;
-    std::vector<uint8_t> img = pack_scenario(e->hs, offs);
-    if (hipMalloc(&e->d_scen, img.size()) != hipSuccess) return fail("hipMalloc scenario");
-    if (hipMemcpy(e->d_scen, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess) return fail("upload scenario");
-    e->dsc = rebase_scenario(offs, (const uint8_t*)e->d_scen);
-    size_t bytes = (size_t)e->L.stride * n_replicas;
-    size_t free_b = 0, total_b = 0;
-    (void)hipMemGetInfo(&free_b, &total_b);
-    if (bytes + (64ull << 20) > free_b && c.delay_fifo == 0 && e->L.cap_fq > 512) {
-        // the default rings grow with the node count (up to 8 x 8,192 x 32 B = 2 MiB per replica): when
-        // that does not fit, fall back to 512-entry rings (a fuller ring only spills to the heap)
-        k10s_capacities c512 = c;
-        c512.delay_fifo = 512;
-        e->L = make_layout(e->hs, c512, !e->plugins && tnn, tnn);
-        bytes = (size_t)e->L.stride * n_replicas;
-    }
-    if (bytes + (64ull << 20) > free_b) {
-        set_err(K10S_E_CAPACITY, "replica state (" + std::to_string(bytes >> 20) + " MiB) exceeds free device memory");
-        engine_free(e);
-        return nullptr;
-    }
-    if (hipMalloc(&e->d_state, bytes) != hipSuccess) return fail("hipMalloc replica state");
-    if (hipMalloc(&e->d_params, sizeof(Params) * n_replicas) != hipSuccess) return fail("hipMalloc params");
-    if (hipMemcpy(e->d_params, e->params.data(), sizeof(Params) * n_replicas, hipMemcpyHostToDevice) != hipSuccess)
-        return fail("upload params");
-    if (hipMalloc(&e->d_active, 64) != hipSuccess) return fail("hipMalloc active");
-    if (hipHostMalloc(&e->h_active, 64) != hipSuccess) return fail("hipHostMalloc");
-    if (hipHostMalloc(&e->h_hdr, sizeof(RepHdr) * (size_t)e->R) != hipSuccess) return fail("hipHostMalloc");
-    if (hipHostMalloc(&e->h_dc, sizeof(DevConst)) != hipSuccess) return fail("hipHostMalloc");
-    std::memset(e->h_dc, 0, sizeof(DevConst));
-    e->h_dc->sc = e->dsc;
-    e->h_dc->L = e->L;
-    e->h_dc->params = e->d_params;
-    e->h_dc->base = e->d_state;
-    e->h_dc->active = e->d_active;
-    if (engine_init(e) != K10S_OK) {
-        std::string m = g_err;
-        engine_free(e);
-        set_err(K10S_E_HIP, m);
-        return nullptr;
-    }
-    return e;
+    const std::string m = g_err;
+    engine_free(e);
+    set_err(rc, m);
+    return nullptr;
 }
 
 void k10s_engine_destroy(k10s_engine* e) { engine_free(e); }
@@ -355,38 +469,37 @@ int32_t k10s_engine_default_params(const k10s_engine* e, k10s_replica_params* ou
 
 int32_t k10s_engine_reset(k10s_engine* e) {
     if (!e) return set_err(K10S_E_INVALID, "null");
-    return engine_init(e);
+    e->history.clear();
+    return core_init(*e);
 }
 
 int32_t k10s_engine_step_async(k10s_engine* e, int32_t mode, double until_time, double max_time,
                                uint64_t max_events_per_launch) {
     if (!e) return set_err(K10S_E_INVALID, "null");
     if (mode != K10S_RUN_UNTIL_ALL_FINISHED && mode != K10S_RUN_UNTIL_TIME) return set_err(K10S_E_INVALID, "bad mode");
-    HIPCHK(hipSetDevice(e->device));
-    HIPCHK(hipMemsetAsync(e->d_active, 0, 4, e->stream));
-    HIPCHK((e->wide ? k10s_launch_run_plugins : k10s_launch_run)(e->h_dc, e->R, mode, until_time, max_time,
-                                                                     max_events_per_launch, e->d_active, e->stream));
-    HIPCHK(hipMemcpyAsync(e->h_active, e->d_active, 4, hipMemcpyDeviceToHost, e->stream));
-    return K10S_OK;
+    const RunCall rc{mode, until_time, max_time, max_events_per_launch, true};
+    e->history.push_back(rc);
+    return core_launch(*e, rc);
 }
 
 int32_t k10s_engine_sync(k10s_engine* e) {
     if (!e) return set_err(K10S_E_INVALID, "null");
+    HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
-    return K10S_OK;
+    return regrow(e);
 }
 
 int32_t k10s_engine_run(k10s_engine* e, int32_t mode, double until_time, double max_time,
                         uint64_t max_events_per_launch, double* elapsed_ms) {
     if (!e) return set_err(K10S_E_INVALID, "null");
+    if (mode != K10S_RUN_UNTIL_ALL_FINISHED && mode != K10S_RUN_UNTIL_TIME) return set_err(K10S_E_INVALID, "bad mode");
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipEventRecord(e->ev0, e->stream));
-    for (;;) {
-        int32_t rc = k10s_engine_step_async(e, mode, until_time, max_time, max_events_per_launch);
-        if (rc != K10S_OK) return rc;
-        HIPCHK(hipStreamSynchronize(e->stream));
-        if (max_events_per_launch == 0 || *e->h_active == 0) break;
-    }
+    const RunCall rc{mode, until_time, max_time, max_events_per_launch, false};
+    e->history.push_back(rc);
+    int32_t r = core_call(*e, rc);
+    if (r == K10S_OK) r = regrow(e);
+    if (r != K10S_OK) return r;
     HIPCHK(hipEventRecord(e->ev1, e->stream));
     HIPCHK(hipEventSynchronize(e->ev1));
     if (elapsed_ms) {
@@ -394,17 +507,6 @@ int32_t k10s_engine_run(k10s_engine* e, int32_t mode, double until_time, double 
         HIPCHK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
         *elapsed_ms = ms;
     }
-    return K10S_OK;
-}
-
-// All replica headers into the engine's pinned staging buffer (one strided DMA; a pageable
-// destination would be copied through a bounce buffer).  The caller holds e->hdr_mu across the fill
-// and its reads of h_hdr, so concurrent read-back calls on one engine do not interleave.
-static int32_t read_all_hdrs(k10s_engine* e) {
-    HIPCHK(hipSetDevice(e->device));
-    HIPCHK(hipMemcpy2DAsync(e->h_hdr, sizeof(RepHdr), e->d_state + e->L.hdr, e->L.stride, sizeof(RepHdr), e->R,
-                            hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
     return K10S_OK;
 }
 
@@ -516,6 +618,12 @@ const char* k10s_engine_group_name(const k10s_engine* e, uint32_t i) {
     return (e && i < e->hs.group_names.size()) ? e->hs.group_names[i].c_str() : "";
 }
 uint64_t k10s_engine_replica_bytes(const k10s_engine* e) { return e ? e->L.stride : 0; }
+int32_t k10s_engine_name_bounds(const k10s_engine* e, uint32_t* group_bound, uint32_t* ca_bound) {
+    if (!e || !group_bound || !ca_bound) return set_err(K10S_E_INVALID, "null");
+    *group_bound = e->hs.group_bound;
+    *ca_bound = e->hs.ca_bound;
+    return K10S_OK;
+}
 uint32_t k10s_engine_node_entry_bytes(const k10s_engine* e) { return e ? (e->L.packed ? 8u : 12u) : 0u; }
 
 }  // extern "C"

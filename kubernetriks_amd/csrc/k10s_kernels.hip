@@ -6,8 +6,10 @@
 //                         node cache) is lane-parallel, everything else wave-uniform
 //   k10s_schedule_kernel  unit-parity surface: R independent schedule_one calls, one wave each
 //
-// No MFMA: nothing on this path is a dense contraction.  Node state is SoA in HBM (12 B/node),
-// read coalesced (lane l reads node base+l), reductions by cross-lane shuffles (DPP/swizzle).
+// No MFMA: nothing on this path is a dense contraction.  The scheduler's node cache is one packed
+// u64 per node in HBM (cpu << 40 | ram: 8 B/node; the wide u32 + u64 SoA, 12 B/node, in the
+// plugins copy), read coalesced (lane l reads 4 consecutive nodes per 256-node step), reductions by
+// cross-lane shuffles (DPP/permlane).
 // Built with -ffp-contract=off and without fast-math: the f64 score arithmetic must round exactly
 // like the Rust reference (correctly rounded division, no FMA contraction).
 #include <hip/hip_runtime.h>
@@ -121,6 +123,9 @@ __global__ K10S_RUN_BOUNDS void k10s_run_kernel(uint32_t n_replicas, int mode, d
     (void)active;   // the same pointer, read after the loop through the constant block
 #if K10S_DEVICE
     if (more && threadIdx.x == 0) atomicAdd(K10S_DC.active, 1u);
+    // a replica stopped at a generated-name bound: the host recompiles the batch with a larger
+    // universe and replays it (k10s_host.cpp regrow)
+    if (threadIdx.x == 0 && k10s_hdr.error_code == K10S_ERR_NAME_BOUND) K10S_DC.active[1] = 1u;
 #endif
 }
 
@@ -206,8 +211,14 @@ hipError_t k10s_launch_run(const void* h_dcv, uint32_t n_replicas, int mode, dou
     return hipGetLastError();
 }
 
+#if K10S_BEACON && defined(K10S_PLUGINS_TU)
+// tooling builds only: the plugins copy's beacon pointer (its own device symbol, k10s_beacon_plugins)
+hipError_t k10s_beacon_set_plugins(void* d) { return hipMemcpyToSymbol(HIP_SYMBOL(k10s_beacon), &d, sizeof d); }
+#endif
 #if K10S_BEACON && !defined(K10S_PLUGINS_TU)
-// tooling builds only: host-mapped beacon memory for n_replicas replicas; returns its host address
+hipError_t k10s_beacon_set_plugins(void* d);
+// tooling builds only: host-mapped beacon memory for n_replicas replicas; returns its host address.
+// Both kernel copies get the pointer (a wide-layout or plugin engine launches the plugins copy).
 extern "C" void* k10s_debug_beacon_alloc(uint32_t n_replicas) {
     void* h = nullptr;
     void* d = nullptr;
@@ -216,6 +227,7 @@ extern "C" void* k10s_debug_beacon_alloc(uint32_t n_replicas) {
     memset(h, 0xFF, bytes);
     if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) return nullptr;
     if (hipMemcpyToSymbol(HIP_SYMBOL(k10s_beacon), &d, sizeof d) != hipSuccess) return nullptr;
+    if (k10s_beacon_set_plugins(d) != hipSuccess) return nullptr;
     return h;
 }
 #endif

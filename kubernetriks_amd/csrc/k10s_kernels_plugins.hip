@@ -16,6 +16,7 @@
 #define k10s_hdr k10s_hdr_plugins
 #define k10s_sec k10s_sec_plugins
 #define k10s_fair_board k10s_fair_board_plugins
+#define k10s_beacon k10s_beacon_plugins   // (K10S_BEACON tooling builds) this copy's own pointer, set with the other
 #define k10s_run k10s_run_plugins
 #define k10s_init_kernel k10s_init_kernel_plugins
 #define k10s_run_kernel k10s_run_kernel_plugins

@@ -144,11 +144,12 @@ def _decl(L, prefix: str):
         "group_name": (ctypes.c_char_p, [vp, u32]), "replica_bytes": (u64, [vp]),
         "node_entry_bytes": (u32, [vp]),
         "default_params": (i32, [vp, P(ReplicaParams)]),
+        "name_bounds": (i32, [vp, P(u32), P(u32)]),
     }
     out = {}
     for name, (res, args) in sig.items():
-        if name == "node_entry_bytes" and not hasattr(L, prefix + name):
-            continue   # a library from before the packed node cache (A/B tooling): wide, 12 B
+        if name in ("node_entry_bytes", "name_bounds") and not hasattr(L, prefix + name):
+            continue   # a library from an earlier round (A/B tooling)
         f = getattr(L, prefix + name)
         f.restype = res
         f.argtypes = args
@@ -170,6 +171,20 @@ class EngineBase:
             self._pod_names = [f["pod_name"](self._h, i).decode() for i in range(f["num_pods"](self._h))]
             self._group_names = [f["group_name"](self._h, i).decode() for i in range(f["num_groups"](self._h))]
         return self._node_names, self._pod_names, self._group_names
+
+    def _forget_names(self):
+        """A run may regrow the batch's generated-name universes (k10s_engine_name_bounds): the
+        name tables are re-read after every run."""
+        for a in ("_node_names", "_pod_names", "_group_names"):
+            self.__dict__.pop(a, None)
+
+    @property
+    def name_bounds(self):
+        """(names per pod group, names per CA node group) of the compiled batch; a run that would
+        exceed one recompiles the batch with it doubled (include/k10s.h k10s_engine_name_bounds)."""
+        g, c = ctypes.c_uint32(), ctypes.c_uint32()
+        self._check(self._fn["name_bounds"](self._h, ctypes.byref(g), ctypes.byref(c)))
+        return int(g.value), int(c.value)
 
     @property
     def node_names(self) -> List[str]:
@@ -363,6 +378,7 @@ class Engine(EngineBase):
     def run(self, mode: int = RUN_UNTIL_ALL_FINISHED, until_time: float = 0.0, max_time: float = 1e12,
             max_events_per_launch: int = 0) -> float:
         ms = ctypes.c_double()
+        self._forget_names()
         self._check(self._L.k10s_engine_run(self._h, mode, until_time, max_time, max_events_per_launch,
                                             ctypes.byref(ms)))
         return ms.value
@@ -401,6 +417,7 @@ class Engine(EngineBase):
         self._check(self._L.k10s_engine_step_async(self._h, mode, until_time, max_time, budget))
 
     def sync(self):
+        self._forget_names()
         self._check(self._L.k10s_engine_sync(self._h))
 
 

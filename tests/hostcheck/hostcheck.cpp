@@ -3,6 +3,7 @@
 // Compiles kubernetriks_amd/csrc/k10s_engine.h with g++ (K10S_LANES == 1) so the kernels' logic
 // can be diffed against the CPU oracle on machines without a GPU.  It is not part of the product:
 // the product C ABI (include/k10s.h, libk10s.so) only runs on the GPU and fails loudly without one.
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -22,6 +23,17 @@ struct HC {
     std::vector<Params> params;
     std::vector<uint8_t> state;
     uint32_t R = 0;
+    // what the batch was compiled from and every run call since, for the name-bound regrow (the
+    // product's k10s_host.cpp regrow, restated for this build)
+    std::string text;
+    std::vector<uint8_t> blob;
+    k10s_capacities caps;
+    struct Call {
+        int mode;
+        double until, max_time;
+        uint64_t budget;
+    };
+    std::vector<Call> history;
 };
 
 // The engine's working header is a separate copy during a run, like the LDS staging of the device
@@ -44,16 +56,11 @@ void* hc_create(const char* text, const k10s_replica_params* params, uint32_t R,
                 char* err, int errlen) {
     return hc_create_bulk(text, nullptr, 0, params, R, caps, err, errlen);
 }
-void* hc_create_bulk(const char* text, const void* blob, uint64_t blob_len, const k10s_replica_params* params,
-                     uint32_t R, const k10s_capacities* caps, char* err, int errlen) {
+static HC* hc_compile(const char* text, const void* blob, uint64_t blob_len, const k10s_replica_params* params,
+                      uint32_t R, const k10s_capacities& c, std::string& e) {
     HC* h = new HC();
-    std::string e;
-    k10s_capacities c;
-    std::memset(&c, 0, sizeof c);
-    if (caps) c = *caps;
     if (!build_scenario(text, c.group_name_bound, c.ca_name_bound, h->hs, e, static_cast<const uint8_t*>(blob),
                         blob_len)) {
-        if (err) std::snprintf(err, (size_t)errlen, "%s", e.c_str());
         delete h;
         return nullptr;
     }
@@ -72,7 +79,7 @@ void* hc_create_bulk(const char* text, const void* blob, uint64_t blob_len, cons
         h->params[r].ca_max_node_count = h->hs.defaults.ca_max_node_count;
         const std::string perr = params_error(h->params[r], h->hs);
         if (!perr.empty()) {
-            if (err) std::snprintf(err, (size_t)errlen, "params[%u]: %s", r, perr.c_str());
+            e = "params[" + std::to_string(r) + "]: " + perr;
             delete h;
             return nullptr;
         }
@@ -89,6 +96,19 @@ void* hc_create_bulk(const char* text, const void* blob, uint64_t blob_len, cons
         init_replica(c);
         *c.v.h() = work;
     }
+    h->text = text;
+    if (blob && blob_len) h->blob.assign((const uint8_t*)blob, (const uint8_t*)blob + blob_len);
+    h->caps = c;
+    return h;
+}
+void* hc_create_bulk(const char* text, const void* blob, uint64_t blob_len, const k10s_replica_params* params,
+                     uint32_t R, const k10s_capacities* caps, char* err, int errlen) {
+    std::string e;
+    k10s_capacities c;
+    std::memset(&c, 0, sizeof c);
+    if (caps) c = *caps;
+    HC* h = hc_compile(text, blob, blob_len, params, R, c, e);
+    if (!h && err) std::snprintf(err, (size_t)errlen, "%s", e.c_str());
     return h;
 }
 void hc_free(void* p) { delete (HC*)p; }
@@ -96,20 +116,63 @@ int hc_default_params(void* p, k10s_replica_params* out) {
     *out = ((HC*)p)->hs.defaults;
     return 0;
 }
-int hc_run(void* p, int mode, double until, double max_time, uint64_t budget) {
-    HC* h = (HC*)p;
-    int active = 0;
+static void hc_call(HC* h, const HC::Call& k) {
     for (uint32_t r = 0; r < h->R; r++) {
         RepHdr work;
         Ctx c = make_ctx(h, r, &work);
         int more = 1;
         while (more) {  // one iteration = one device launch: stage, run, write back
             work = *c.v.h();
-            more = run_replica(c, mode, until, max_time, budget);
+            more = run_replica(c, k.mode, k.until, k.max_time, k.budget);
             *c.v.h() = work;
         }
     }
-    return active;
+}
+int hc_run(void* p, int mode, double until, double max_time, uint64_t budget) {
+    HC* h = (HC*)p;
+    const HC::Call k{mode, until, max_time, budget};
+    h->history.push_back(k);
+    hc_call(h, k);
+    // name-bound regrow (k10s_host.cpp regrow): recompile with the exhausted universe doubled and
+    // replay every call, until no replica stops at K10S_ERR_NAME_BOUND
+    for (;;) {
+        bool grow_ca = false, grow_group = false;
+        for (uint32_t r = 0; r < h->R; r++) {
+            const RepHdr& H = *make_rep(h->state.data(), h->L, r).h();
+            if (H.error_code != K10S_ERR_NAME_BOUND) continue;
+            if (H.error_kind == K10S_EV_PS_CA_REQ) grow_ca = true;
+            else grow_group = true;
+        }
+        k10s_capacities c = h->caps;
+        c.group_name_bound = h->hs.group_bound;
+        c.ca_name_bound = h->hs.ca_bound;
+        const uint32_t MAXB = 1u << 20;
+        bool grown = false;
+        if (grow_group && c.group_name_bound < MAXB) {
+            c.group_name_bound = std::min<uint32_t>(2 * std::max<uint32_t>(c.group_name_bound, 32), MAXB);
+            grown = true;
+        }
+        if (grow_ca && c.ca_name_bound < MAXB) {
+            c.ca_name_bound = std::min<uint32_t>(2 * std::max<uint32_t>(c.ca_name_bound, 32), MAXB);
+            grown = true;
+        }
+        if (!grown) return 0;
+        std::string e;
+        HC* n = hc_compile(h->text.c_str(), h->blob.empty() ? nullptr : h->blob.data(), h->blob.size(),
+                           h->params.data(), h->R, c, e);
+        if (!n) return -1;
+        n->caps = h->caps;   // the caller's capacities; the bounds live in hs
+        n->history = h->history;
+        for (const HC::Call& x : n->history) hc_call(n, x);
+        std::swap(*h, *n);
+        delete n;
+    }
+}
+int hc_name_bounds(void* p, uint32_t* group_bound, uint32_t* ca_bound) {
+    HC* h = (HC*)p;
+    *group_bound = h->hs.group_bound;
+    *ca_bound = h->hs.ca_bound;
+    return 0;
 }
 int hc_results(void* p, k10s_replica_result* out) {
     HC* h = (HC*)p;

@@ -37,12 +37,8 @@ def parity_caps(log: bool = True, fifo: int = 0, pruned: int = 0, gauges: int = 
     c.event_log = (1 << 20) if log else 0
     c.placement_log = 1 << 20
     c.pod_records = 1
-    # The HPA's generated pod names "{group}_{k}" form a precomputed universe of group_name_bound
-    # names per group (k10s.h; exceeding it is the capacity error K10S_ERR_NAME_BOUND, the default is
-    # 8 x the group's max + 64).  Long random runs that scale a group up and down churn through more
-    # (fuzz seeds 546, 878, 898, 1106, 1530 of 2,000 did, profiles/r04_fuzz2000_gpu.log): parity runs
-    # use a universe of 4,096 names per group.
-    c.group_name_bound = 4096
+    # (the generated-name universes stay at their defaults: a replica that outgrows one is rerun in a
+    # regrown batch by the engine itself, k10s.h k10s_engine_name_bounds)
     return c
 
 

@@ -59,3 +59,16 @@ def test_schedule_one_batch_rejects_misaligned_buffers():
                                    ctypes.c_void_p(req_r.ctypes.data), ctypes.c_double(1.0), 1,
                                    ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(out.ctypes.data + 4), None)
     assert rc != 0 and b"aligned" in L.k10s_last_error()
+
+
+def test_beacon_tooling_library_links_both_kernel_copies():
+    """A -DK10S_BEACON=1 library (tools/beacon_trace.py) links: each kernel copy owns its beacon
+    pointer (k10s_beacon / k10s_beacon_plugins) and k10s_debug_beacon_alloc sets both."""
+    import subprocess
+    from kubernetriks_amd.build import build
+    out = os.path.join(REPO, "build", "libk10s_beacon_linkcheck.so")
+    build(force=True, extra=["-DK10S_BEACON=1"], out=out)
+    syms = subprocess.run(["nm", "-D", "--defined-only", out], capture_output=True, text=True, check=True).stdout
+    assert "k10s_debug_beacon_alloc" in syms
+    L = ctypes.CDLL(out)
+    assert hasattr(L, "k10s_debug_beacon_alloc")

@@ -1,9 +1,11 @@
 """The exact workloads bench.py measures, oracle-checked: the same traces, the same
 bulk scenario path (scenario_bulk + k10s_engine_create_bulk), the same replica count and the same
 per-replica parameters (ensemble.shard_params at the bench seed), with bit-exact oracle replays of
-replicas spread over the batch (32 by hash, the first and last, and the fewest- and most-event ones).  Only the result logs differ from bench.py's
-engine (placements and pod records are kept here so they can be compared); they do not change
-what a replica simulates."""
+replicas spread over the batch (32 by hash, the first and last, and the fewest- and most-event ones).
+The replayed batch keeps placement logs and pod records so they can be compared; the batch with
+bench.py's own capacities (no logs, the default delay rings, full scans: the exact timed
+configuration) runs beside it and must produce the identical counter matrix,
+estimators, histograms, clocks and statuses for every replica."""
 import pytest
 
 import oracle_jobs
@@ -42,6 +44,20 @@ def _bench_batch(cluster, workload, check, score_plugins=1):
     eng = Engine(scn, R, params=params, caps=caps, pods_blob=blob)
     eng.run_until_all_finished(1e7)
     res = eng.results()
+    # the timed configuration itself: bench.py's Capacities() (pruned_scan 0, delay_fifo 0, no logs)
+    from kubernetriks_amd.native import Capacities
+    timed = Engine(scn, R, params=params, caps=Capacities(), pods_blob=blob)
+    timed.run_until_all_finished(1e7)
+    assert (timed.counter_matrix() == eng.counter_matrix()).all()
+    tres = timed.results()
+    for r in range(R):
+        a, b = res[r], tres[r]
+        assert (a["status"], a["error_code"], parity.fbits(a["time"])) == \
+            (b["status"], b["error_code"], parity.fbits(b["time"])), r
+        for k in a["estimators"]:
+            ea, eb = a["estimators"][k], b["estimators"][k]
+            assert ea[0] == eb[0] and all(parity.feq(x, y) for x, y in zip(ea[1:5], eb[1:5])) and ea[5] == eb[5], (r, k)
+    del timed
     if isinstance(check, int):
         check = pick(res, check)
     ods = oracle_jobs.replay_many([wl.replica_scenario(cfg, cluster, workload, params[r]) for r in check], 1e7)
