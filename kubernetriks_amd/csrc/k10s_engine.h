@@ -227,6 +227,11 @@ struct Ctx {
 };
 
 K10S_HD void fail(Ctx& c, uint32_t code) {
+#if K10S_DEVICE
+    // the code is materialized here, on the (cold) error path: as a plain constant the compiler
+    // hoisted each code's VGPR copy out of the event loop and held six of the loop's 64 VGPRs with them
+    asm volatile("" : "+s"(code));
+#endif
     RepHdr& h = c.H();
     if (h.error_code == 0) {
         h.error_code = code;
@@ -235,6 +240,20 @@ K10S_HD void fail(Ctx& c, uint32_t code) {
         h.error_time = h.clock;
     }
 }
+
+// Runs of one event kind handled together (defined with the event queue below); called by the
+// handlers of the run kinds.
+// (tuning knob, semantics-neutral: bit 0 the api-server / storage kinds, bit 1 the scheduler's)
+#ifndef K10S_RUNS
+#define K10S_RUNS 3
+#endif
+K10S_HD_NOINL uint32_t run_batch(Ctx& c, uint32_t k);
+#define K10S_RUN_CALL(c, k) (uniform_u32(run_batch((c), (k))) != 0u)
+#if K10S_RUNS & 1
+#define K10S_RUN(c, k) K10S_RUN_CALL(c, k)
+#else
+#define K10S_RUN(c, k) false
+#endif
 
 // ---- the scheduler's node cache (allocatable per node in name order: the scan target) -----------
 // Two layouts of the same values (Layout.packed, chosen per engine by make_layout):
@@ -519,7 +538,7 @@ extern "C" uint64_t k10s_host_stats[48];
 #endif
 enum { HS_EVENTS, HS_FIFO_POP, HS_REFILL, HS_HEAP_POP, HS_TRACE_POP, HS_SL_FAST, HS_SL_UPDATE, HS_EMIT_WIN,
        HS_EMIT_RING, HS_EMIT_HEAP, HS_SL_DIRTY, HS_SCANS, HS_REFILL_CLS0 = 12, HS_POP_CLS0 = 20, HS_AQ_HBM_GET = 28, HS_AQ_POP = 29, HS_SLPOS0 = 32,
-       HS_NEXT_EMITTED = 36, HS_NEXT_EMITTED_FIFO = 37 };
+       HS_NEXT_EMITTED = 36, HS_NEXT_EMITTED_FIFO = 37, HS_RUNS = 38, HS_RUN_EVENTS = 39, HS_RUN_REFUSED = 40 };
 // An emission changed source q's head: mark it for the source list.
 K10S_HD void sl_mark(RepHdr& H, uint32_t q) { H.sl_dirty |= 1u << q; }
 K10S_HD void pods_left_dec(RepHdr& H) { H.pods_left -= 1; }
@@ -2073,6 +2092,16 @@ K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
 // 4.6 % at C3, profiles/r02_v4_score_plugins_ab.json).
 K10S_HD void run_scheduling_cycle_plugins(Ctx& c, double t) { run_scheduling_cycle_t<true>(c, t); }
 
+K10S_HD void on_scheduler(Ctx& c, const HeapEv& e);
+// PodScheduleRequest and AddNodeToCache, out of line: both come in runs (run_batch), whose call stays
+// out of the event loop's body this way.
+K10S_WARM void on_sched_run(Ctx& c, K10S_EVARG) {
+    K10S_EV_PROLOGUE;
+    if (K10S_RUN_CALL(c, (uint32_t)e.kind)) return;
+    HeapEv ev = *ep;
+    uniform_event(ev);
+    on_scheduler(c, ev);
+}
 K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
     RepHdr* h = &c.H();
     switch (e.kind) {
@@ -2547,6 +2576,7 @@ K10S_WARM void on_ps(Ctx& c, K10S_EVARG) {
     const Params* pr = &c.P();
     switch (e.kind) {
     case K10S_EV_PS_CREATE_NODE_REQ: {
+        if (K10S_RUN(c, K10S_EV_PS_CREATE_NODE_REQ)) return;
         uint32_t def = e.b, n = e.a;
         if (c.V().node(n).flags & NF_PS_PRESENT) {
             fail(c, K10S_PANIC_DUPLICATE_NODE);
@@ -2568,6 +2598,7 @@ K10S_WARM void on_ps(Ctx& c, K10S_EVARG) {
         break;
     }
     case K10S_EV_PS_NODE_ADDED: {
+        if (K10S_RUN(c, K10S_EV_PS_NODE_ADDED)) return;
         uint32_t n = e.a;
         if (!(c.V().node(n).flags & NF_PS_PRESENT)) {
             fail(c, K10S_PANIC_MISSING_NODE);
@@ -2578,6 +2609,7 @@ K10S_WARM void on_ps(Ctx& c, K10S_EVARG) {
         break;
     }
     case K10S_EV_PS_CREATE_POD_REQ: {
+        if (K10S_RUN(c, K10S_EV_PS_CREATE_POD_REQ)) return;
         uint32_t p = e.a;
         const uint8_t pf = c.V().pod(p).flags;
         if (pf & PF_IN_PS) {
@@ -2701,10 +2733,6 @@ K10S_WARM void on_ps(Ctx& c, K10S_EVARG) {
     case K10S_EV_PS_NODE_REMOVED:
         emit(c, K10S_EV_S_REMOVE_NODE, pr->ps_to_sched_network_delay, -1, e.a, 0, 0.0, FQ_PS_TO_SCHED);
         break;
-    case K10S_EV_PS_CA_REQ:
-        ca_decide(c);
-        emit(c, K10S_EV_AS_CA_RESP, pr->as_to_ps_network_delay, -1, 0, 0, 0.0, FQ_AS_TO_PS);
-        break;
     case K10S_EV_PS_REMOVE_POD_REQ: {
         uint32_t p = e.a;
         if (!(c.V().pod(p).flags & PF_IN_PS)) {
@@ -2737,6 +2765,16 @@ K10S_WARM void on_ps(Ctx& c, K10S_EVARG) {
     }
 }
 
+// Storage's ClusterAutoscalerRequest (persistent_storage.rs:381-412): the CA decision.  Its own
+// out-of-line handler, not a case of on_ps: the registers ca_decide clobbers then do not count against
+// on_ps, whose call the event loop makes four times per pod (with the decision inside, the loop saved
+// and restored 20 SGPRs around every on_ps call: 40 VALU lane moves).
+K10S_COLD void on_ps_ca(Ctx& c, K10S_EVARG) {
+    (void)ep;
+    ca_decide(c);
+    emit(c, K10S_EV_AS_CA_RESP, c.P().as_to_ps_network_delay, -1, 0, 0, 0.0, FQ_AS_TO_PS);
+}
+
 // The api server's removal set (names with a removal in flight, api_server.rs:343, 285-305) as a
 // uid bitset with its population count in the header.
 K10S_HD void pend_rm_set(Ctx& c, uint32_t uid) {
@@ -2760,6 +2798,7 @@ K10S_WARM void on_api_server(Ctx& c, K10S_EVARG) {
     const Scenario* sc = &c.S();
     switch (e.kind) {
     case K10S_EV_AS_CREATE_NODE_REQ: {
+        if (K10S_RUN(c, K10S_EV_AS_CREATE_NODE_REQ)) return;
         uint32_t def = e.b;
         uint32_t n = sc->def_node[def];
         h->g_cur_nodes += 1;  // api_server.rs:133-137
@@ -2768,6 +2807,7 @@ K10S_WARM void on_api_server(Ctx& c, K10S_EVARG) {
         break;
     }
     case K10S_EV_AS_CREATE_NODE_RESP: {  // handle_create_node (96-115)
+        if (K10S_RUN(c, K10S_EV_AS_CREATE_NODE_RESP)) return;
         uint32_t n = e.a;
         int32_t def = c.V().node(n).pend_def;
         if (def < 0) {
@@ -2798,6 +2838,7 @@ K10S_WARM void on_api_server(Ctx& c, K10S_EVARG) {
         break;
     }
     case K10S_EV_AS_CREATE_POD_REQ:
+        if (K10S_RUN(c, K10S_EV_AS_CREATE_POD_REQ)) return;
         h->g_cur_pods += 1;  // api_server.rs:151-155
         emit(c, K10S_EV_PS_CREATE_POD_REQ, pr->as_to_ps_network_delay, -1, e.a, 0, 0.0, FQ_AS_TO_PS);
         break;
@@ -3254,11 +3295,18 @@ K10S_HD void dispatch(Ctx& c, EvRef ep, uint32_t k) {
     k = uniform_u32(k);   // wave-uniform by construction: scalar branches (see run_replica)
     if (k <= K10S_EV_M_GAUGE_TICK) on_metrics(c, ep);
     else if (k <= K10S_EV_AS_CREATE_GROUP_REQ) on_api_server(c, ep);
-    else if (k <= K10S_EV_PS_POD_REMOVED) on_ps(c, ep);
+    else if (k <= K10S_EV_PS_POD_REMOVED) {
+        if (k == K10S_EV_PS_CA_REQ) on_ps_ca(c, ep);
+        else on_ps(c, ep);
+    }
     else if (k <= K10S_EV_S_REMOVE_POD) {
-        HeapEv e = *ep;
-        uniform_event(e);
-        on_scheduler(c, e);
+        if ((K10S_RUNS & 2) && (k == K10S_EV_S_POD_SCHEDULE_REQ || k == K10S_EV_S_ADD_NODE)) {
+            on_sched_run(c, ep);
+        } else {
+            HeapEv e = *ep;
+            uniform_event(e);
+            on_scheduler(c, e);
+        }
     } else if (k <= K10S_EV_N_REMOVE_POD) on_node(c, ep);
     else if (k <= K10S_EV_CA_RESP) on_ca(c, ep);
     else on_hpa(c, ep);
@@ -3561,6 +3609,7 @@ K10S_HD void fq_refill(Ctx& c, int cls, uint32_t hd) {
 // Remove the head event of source src (sl[0]) and move the source's entry in the source list to
 // its new head; a FIFO takes its next head from its window.  When the new
 // head still precedes sl[1], only sl[0]'s key is rewritten (tuning knob, semantics-neutral).
+K10S_HD void sl_after_consume(Ctx& c, int src, bool has, int64_t key, uint32_t seq);
 K10S_HD void consume_source(Ctx& c, int src, uint32_t ntr) {
     src = (int)uniform_u32((uint32_t)src);   // wave-uniform by construction: scalar branches (see run_replica)
     RepHdr& H = c.H();
@@ -3600,6 +3649,12 @@ K10S_HD void consume_source(Ctx& c, int src, uint32_t ntr) {
             seq = t.seq;
         }
     }
+    sl_after_consume(c, src, has, key, seq);
+}
+
+// The consumed source src (sl[0]) has its new head (key, seq), or is empty (!has): reposition it.
+K10S_HD void sl_after_consume(Ctx& c, int src, bool has, int64_t key, uint32_t seq) {
+    RepHdr& H = c.H();
     key = (int64_t)uniform_u64((uint64_t)key);
     seq = uniform_u32(seq);
     // src is sl[0]: while its new head still precedes the second source (47 % of the events at C3,
@@ -3735,6 +3790,396 @@ K10S_HD_NOINL void drop_stale_head(Ctx& c, uint32_t ntr) {
     heap_pop(c);
     sl_refresh(c, SRC_HEAP, ntr);
 }
+// ---- runs of one event kind, handled together (round 5) -------------------------------------------
+// The C3 workload delivers many events in runs: the 13-14 pods of an integer-second arrival burst
+// pass the api server, storage and the scheduler's queue as three runs of 13-14 consecutive events of
+// one kind, from one source, at one time (AS_CREATE_POD_REQ from the trace, PS_CREATE_POD_REQ from the
+// as-to-ps ring, S_POD_SCHEDULE_REQ from the ps-to-sched ring: mean run 13.65), and the 4,096 nodes of
+// the trace are created at t = 0 as five runs of 4,096 (AS_CREATE_NODE_REQ, PS_CREATE_NODE_REQ,
+// AS_CREATE_NODE_RESP, PS_NODE_ADDED, S_ADD_NODE).  Handling a run event by event pays the
+// selection, the dispatch and the consume once per event; here they are paid once per run (of up to
+// 64 events) and the K handlers run as K lanes.
+//
+// Why it is exact.  The run is the next K events in dslab (time, id) order: consecutive heads of source
+// src, all of kind k and time t, all before the head of the second source in the source list (sl[1]),
+// so no other source delivers in between.  Every event a handler of the run emits has time t + d >= t
+// and an id larger than every pending id (ids are handed out in emission order), so it is ordered after
+// the whole run and cannot interleave with it.  The handlers of these kinds touch their own pod's or
+// node's line, header counters that commute, slots taken from the pool ring in event order, presence
+// bits set with atomics, and the emission sequence; the batch hands out ids next_seq + i in event order
+// (one emission per event, as the serial handlers do) and appends to the target ring in that order.
+// What the serial path would do differently is excluded before anything is written — a reference panic
+// (a pod already in storage, a node already present / not pending / missing, an empty node pool, or
+// one pod or node twice in the run), a full ring or a run that would break its ring's time order
+// (those emissions go to the heap), an id overflow, a full action queue, a cluster autoscaler or the
+// pruned scan's block bounds (their per-node upkeep), a non-empty unschedulable map (a node added with
+// pods waiting moves them) — and then the run is not batched: the loop takes its events one by one.
+// The termination rule cannot fire inside a run (none of these kinds terminates a pod), and the time
+// limit and event budget are checked for the run's time and length by the caller.
+#define K10S_RUN_MAX 64
+// i = the run event this lane handles: one pass of the lanes below K on the device, a loop on the host
+#if K10S_DEVICE
+#define K10S_FOR_RUN(i, K) for (uint32_t i = (uint32_t)lane_id(), i##_1 = 0; i##_1 == 0 && i < (K); i##_1 = 1)
+#else
+#define K10S_FOR_RUN(i, K) for (uint32_t i = 0; i < (K); i++)
+#endif
+K10S_HD bool run_kind(uint32_t k) {
+    return k == K10S_EV_AS_CREATE_POD_REQ || k == K10S_EV_PS_CREATE_POD_REQ || k == K10S_EV_S_POD_SCHEDULE_REQ ||
+           k == K10S_EV_AS_CREATE_NODE_REQ || k == K10S_EV_PS_CREATE_NODE_REQ || k == K10S_EV_AS_CREATE_NODE_RESP ||
+           k == K10S_EV_PS_NODE_ADDED || k == K10S_EV_S_ADD_NODE;
+}
+// Event i of a run at source src: FIFO position head + i (its LDS window below wend, the HBM ring
+// above), or trace position trace_cursor + i (a and b as the loop materializes a trace event).  ok =
+// false when it does not exist or is a workload event outside this replica's trace (its id would shift).
+struct RunEv {
+    double time, x;
+    uint32_t seq, kind, a, b;
+    bool ok;
+};
+K10S_HD RunEv run_ev(Ctx& c, int src, uint32_t i) {
+    const RepHdr& H = c.H();
+    RunEv r;
+    r.time = 0.0;
+    r.x = 0.0;
+    r.seq = 0;
+    r.kind = 0xFFFFu;
+    r.a = 0;
+    r.b = 0;
+    r.ok = false;
+    if (src == SRC_TRACE) {
+        const uint32_t cur = H.trace_cursor + i;
+        if (cur < c.S().n_trace) {
+            const TraceEv t = c.S().trace[cur];
+            const bool wl = t.wpos != K10S_TRACE_CLUSTER;
+            r.ok = !wl || t.wpos < H.trace_prefix;
+            r.time = t.time;
+            r.seq = t.seq - (wl ? H.tr_skip : 0u);
+            r.kind = t.kind;
+            r.a = t.arg;
+            if (t.kind == K10S_EV_AS_CREATE_NODE_REQ) {   // as run_replica materializes it
+                r.a = c.S().def_node[t.arg];
+                r.b = t.arg;
+            }
+        }
+    } else {
+        const uint32_t hd = H.fq[src].head, tl = H.fq[src].tail, we = H.fq[src].wend;
+        if (i < tl - hd) {
+            const uint32_t pos = hd + i;
+            HeapEv e;
+            if (pos - hd < we - hd) e = H.fq_win[(uint32_t)src * K10S_FQW + (pos & (K10S_FQW - 1))];
+            else e = c.V().fq()[(uint32_t)src * c.Ly().cap_fq + (pos & (c.Ly().cap_fq - 1))];
+            r.ok = true;
+            r.time = e.time;
+            r.x = e.x;
+            r.seq = e.seq;
+            r.kind = e.kind;
+            r.a = e.a;
+            r.b = e.b;
+        }
+    }
+    return r;
+}
+
+// Called by the handler of the current event (kind k, at the head of its source, which is sl[0]; the
+// clock is its time): handle the run it starts, K >= 2 events, and return K, or 0 when the events must
+// go one by one (nothing was written then).  On return the K handlers have run, events 1..K-1 are
+// logged and counted, and the source is advanced past events 0..K-2: the event loop's own consume of
+// the current event then removes the last one (the loop itself is unchanged: a call in its body would
+// re-spill its live registers around every event; round 5 measured that layout at -9.6 % on C3).
+K10S_HD_NOINL uint32_t run_batch(Ctx& c, uint32_t k) {
+    RepHdr& H = c.H();
+    k = uniform_u32(k);
+    const uint32_t fl = uniform_u32(H.run_flags);
+    // budgeted launches count events one by one; the termination rule is checked before every event
+    // (it cannot fire inside a run while pods are left, or in until-time mode)
+    if (!(fl & 1u) || (!(fl & 2u) && (int64_t)uniform_u64((uint64_t)H.pods_left) <= 0)) return 0;
+    const int src = (int)uniform_u32(H.sl[0].src);
+    if (src == SRC_HEAP) return 0;
+    const double t = uniform_f64(H.clock);
+    const uint32_t kmax = K10S_RUN_MAX;
+    const int64_t kt = total_key(t);
+    // the second source's head bounds the run
+    const uint32_t sn = uniform_u32(H.sl_n);
+    const int64_t k1 = sn >= 2 ? (int64_t)uniform_u64((uint64_t)H.sl[1].key) : 0x7FFFFFFFFFFFFFFFll;
+    const uint32_t s1 = sn >= 2 ? uniform_u32(H.sl[1].seq) : 0xFFFFFFFFu;
+    const uint32_t lim = kmax < K10S_RUN_MAX ? kmax : K10S_RUN_MAX;
+    // ---- the run's length: the leading events that are of kind k, at time t, before sl[1]
+    uint32_t K = 0;
+#if K10S_DEVICE
+    {
+        const uint32_t lane = (uint32_t)lane_id();
+        bool in = false;
+        if (lane < lim) {
+            const RunEv r = run_ev(c, src, lane);
+            in = r.ok && r.kind == k && total_key(r.time) == kt && sl_less(kt, r.seq, k1, s1);
+        }
+        const uint64_t m = ~__ballot(in);
+        K = m ? (uint32_t)__builtin_ctzll(m) : 64u;
+    }
+#else
+    while (K < lim) {
+        const RunEv r = run_ev(c, src, K);
+        if (!(r.ok && r.kind == k && total_key(r.time) == kt && sl_less(kt, r.seq, k1, s1))) break;
+        K++;
+    }
+#endif
+    K = uniform_u32(K);
+    if (K < 2) return 0;
+    K10S_HSTAT(HS_RUN_REFUSED);   // (taken back below once the run is handled)
+    // ---- everything the serial path would do differently: then no batch
+    const uint32_t seq0 = uniform_u32(H.next_seq);
+    if ((uint64_t)seq0 + K > 0xFFFFFFFFull) return 0;   // an id would reach 2^32 - 1 (K10S_ERR_SEQ_OVERFLOW)
+    const Params& pr = c.P();
+    const Scenario& S = c.S();
+    int cls = -1;     // the emissions' delay class
+    double d = 0.0;
+    uint32_t ek = 0;  // and kind
+    bool uniq = false;   // the run's pods / nodes must be distinct
+    switch (k) {
+    case K10S_EV_AS_CREATE_POD_REQ:
+        cls = FQ_AS_TO_PS, d = pr.as_to_ps_network_delay, ek = K10S_EV_PS_CREATE_POD_REQ;
+        break;
+    case K10S_EV_PS_CREATE_POD_REQ:
+        cls = FQ_PS_TO_SCHED, d = pr.ps_to_sched_network_delay, ek = K10S_EV_S_POD_SCHEDULE_REQ, uniq = true;
+        break;
+    case K10S_EV_S_POD_SCHEDULE_REQ:
+        if (uniform_u32(H.aq_size) + K > c.Ly().cap_aq) return 0;
+        break;
+    case K10S_EV_AS_CREATE_NODE_REQ:
+        cls = FQ_AS_TO_PS, d = pr.as_to_ps_network_delay, ek = K10S_EV_PS_CREATE_NODE_REQ, uniq = true;
+        break;
+    case K10S_EV_PS_CREATE_NODE_REQ:
+        if (S.ca_enabled) return 0;   // CA-origin nodes: shared bitmap words, assignment lists
+        cls = FQ_AS_TO_PS, d = pr.as_to_ps_network_delay, ek = K10S_EV_AS_CREATE_NODE_RESP, uniq = true;
+        break;
+    case K10S_EV_AS_CREATE_NODE_RESP:
+        if (uniform_u32(H.pool_count) < K) return 0;   // node_component_pool.rs:56-59
+        cls = FQ_AS_TO_PS, d = pr.as_to_ps_network_delay, ek = K10S_EV_PS_NODE_ADDED, uniq = true;
+        break;
+    case K10S_EV_PS_NODE_ADDED:
+        cls = FQ_PS_TO_SCHED, d = pr.ps_to_sched_network_delay, ek = K10S_EV_S_ADD_NODE;
+        break;
+    default:   // K10S_EV_S_ADD_NODE
+        // with pods in the unschedulable map each addition moves some (scheduler.rs:391-405); the wide
+        // layout keeps capacities and (pruned scan) block bounds per node
+        if (uniform_u32(H.uq_size) != 0 || !nc_packed(c) || c.Ly().pruned) return 0;
+        uniq = true;
+        break;
+    }
+    const uint32_t cap = c.Ly().cap_fq;
+    const double te = t + d;
+    uint32_t fhd = 0, ftl = 0, fwe = 0;
+    if (cls >= 0) {
+        fhd = uniform_u32(H.fq[cls].head);
+        ftl = uniform_u32(H.fq[cls].tail);
+        fwe = uniform_u32(H.fq[cls].wend);
+        const double last = uniform_f64(H.fq[cls].last);
+#if !K10S_TIME_KEY_ID
+        if (!(d >= 0.0)) return 0;   // a negative delay panics in emit (signed-time kernel copy)
+#endif
+        // room: the run's own slots count when it is consumed from the target ring itself (storage's
+        // node creation answers the api server on the ring that brought the request) — each lane reads
+        // its run event before any lane writes, and emission i lands on run event i - free's slot, so
+        // the overlap is safe; at t = 0 that ring holds all 4,096 node requests, which the serial path
+        // answers through the heap
+        const uint32_t room = cap - (ftl - fhd) + (src == cls ? K : 0u);
+        if (!cap || room < K || (ftl != fhd && total_key(te) < total_key(last))) return 0;
+    }
+    {
+        bool bad = false;
+        K10S_FOR_RUN(i, K) {
+            const RunEv r = run_ev(c, src, i);
+            if (k == K10S_EV_PS_CREATE_POD_REQ) {
+                bad |= (c.V().pod(r.a).flags & PF_IN_PS) != 0;   // persistent_storage.rs:89-94
+            } else if (k == K10S_EV_PS_CREATE_NODE_REQ) {
+                bad |= (c.V().node(r.a).flags & NF_PS_PRESENT) != 0;   // persistent_storage.rs:76-81
+            } else if (k == K10S_EV_AS_CREATE_NODE_RESP) {
+                const NodeState& N = c.V().node(r.a);   // api_server.rs:98-101, 73-78
+                bad |= N.pend_def < 0 || N.as_slot >= 0;
+            } else if (k == K10S_EV_PS_NODE_ADDED) {
+                bad |= (c.V().node(r.a).flags & NF_PS_PRESENT) == 0;
+            }
+            if (uniq) {   // one pod / node twice: the serial path would see the first one's writes
+#if K10S_DEVICE
+                for (uint32_t j = 0; j < K; j++) bad |= j < i && (uint32_t)__builtin_amdgcn_readlane((int)r.a, (int)j) == r.a;
+#else
+                for (uint32_t j = 0; j < i; j++) bad |= run_ev(c, src, j).a == r.a;
+#endif
+            }
+        }
+        if (wave_any(bad)) return 0;
+    }
+    // ---- the K handlers, one per lane
+    const uint32_t cap_log = c.Ly().cap_log;
+    const uint32_t log0 = uniform_u32(H.log_n) - 1u;   // event 0 was logged by the event loop
+    const uint32_t pool_head = uniform_u32(H.pool_head);
+    uint32_t cnt = 0;   // per lane: PF_UNSCHED pods (PS_CREATE_POD_REQ) / newly present nodes (S_ADD_NODE)
+    K10S_FOR_RUN(i, K) {
+        const RunEv r = run_ev(c, src, i);
+        const bool node_kind = k != K10S_EV_AS_CREATE_POD_REQ && k != K10S_EV_PS_CREATE_POD_REQ &&
+                               k != K10S_EV_S_POD_SCHEDULE_REQ;
+        if (cap_log && i > 0 && log0 + i < cap_log) {
+            k10s_log_entry le;
+            le.time = r.time;
+            le.seq = r.seq;
+            le.kind = (uint16_t)k;
+            le.slot = -1;
+            le.pod = node_kind ? -1 : (int32_t)r.a;
+            le.node = node_kind ? (int32_t)r.a : -1;
+            c.V().log()[log0 + i] = le;
+        }
+        uint32_t eb = 0;   // the emission's b and x
+        double ex = 0.0;
+        switch (k) {
+        case K10S_EV_PS_CREATE_POD_REQ: {
+            PodState& P = c.V().pod(r.a);
+            const uint8_t pf = P.flags;
+            P.flags = (uint8_t)(pf | PF_IN_PS);
+            cnt += (pf & PF_UNSCHED) ? 1u : 0u;
+            P.ps_assigned = -1;
+            if (c.V().prec()) c.V().prec()[r.a].state = 1;
+            break;
+        }
+        case K10S_EV_S_POD_SCHEDULE_REQ:
+            c.V().pod(r.a).sflag = PF_IN_S;
+            c.V().pod(r.a).s_assigned = -1;
+            break;
+        case K10S_EV_AS_CREATE_NODE_REQ:   // api_server.rs:132-137
+            c.V().node(r.a).pend_def = (int32_t)r.b;
+            eb = r.b;
+            break;
+        case K10S_EV_PS_CREATE_NODE_REQ: {   // persistent_storage.rs:188-195 (no CA)
+            NodeState& N = c.V().node(r.a);
+            N.flags = (uint8_t)((N.flags & ~NF_CA_ORIGIN) | NF_PS_PRESENT);
+            N.ps_def = r.b;
+            N.ps_cpu = S.def_cpu[r.b];
+            N.ps_ram = S.def_ram[r.b];
+            N.ps_epoch += 1;
+            break;
+        }
+        case K10S_EV_AS_CREATE_NODE_RESP: {   // handle_create_node (api_server.rs:96-115): slots in event order
+            NodeState& N = c.V().node(r.a);
+            const uint32_t def = (uint32_t)N.pend_def;
+            N.pend_def = -1;
+            const uint32_t slot = c.V().pool_ring()[(pool_head + i) % S.n_slots];
+            c.V().slot((int32_t)slot).node = (int32_t)r.a;
+            c.V().slot((int32_t)slot).def = def;
+            N.as_slot = (int32_t)slot;
+            if (c.Ly().cap_gauge) {
+                c.V().g_cpu()[slot] = S.def_cpu[def];
+                c.V().g_ram()[slot] = S.def_ram[def];
+            }
+            ex = r.time;
+            break;
+        }
+        case K10S_EV_PS_NODE_ADDED:   // persistent_storage.rs:197-210
+            eb = c.V().node(r.a).ps_cpu;
+            ex = u2f(c.V().node(r.a).ps_ram);
+            break;
+        case K10S_EV_S_ADD_NODE: {   // scheduler.rs:391-405 (packed cache, empty unschedulable map)
+            const NcEnt ent = {r.b, f2u(r.x)};
+            nc_put(c, r.a, ent);
+            const uint64_t bit = 1ull << (r.a & 63u);
+#if K10S_DEVICE
+            const uint64_t old = atomicOr((unsigned long long*)&c.V().s_present()[r.a >> 6], (unsigned long long)bit);
+#else
+            const uint64_t old = c.V().s_present()[r.a >> 6];
+            c.V().s_present()[r.a >> 6] = old | bit;
+#endif
+            cnt += (old & bit) ? 0u : 1u;
+            break;
+        }
+        default:
+            break;
+        }
+        if (cls >= 0) {   // its one emission: id seq0 + i, ring position ftl + i
+            HeapEv e;
+            e.time = te;
+            e.seq = seq0 + i;
+            e.kind = (uint16_t)ek;
+            e.slot = -1;
+            e.a = r.a;
+            e.b = eb;
+            e.x = ex;
+            c.V().fq()[(uint32_t)cls * cap + ((ftl + i) & (cap - 1))] = e;
+            // the window holds the whole ring and has room: the first entries go there as well
+            if (fwe == ftl && (ftl - fhd) + i < K10S_FQW) H.fq_win[(uint32_t)cls * K10S_FQW + ((ftl + i) & (K10S_FQW - 1))] = e;
+        }
+    }
+    wave_sync();
+    if (cap_log) {   // (the loop logged event 0 at log0, or flagged the overflow)
+        if (log0 + K <= cap_log) H.log_n = log0 + K;
+        else {
+            H.log_n = log0 + 1u < cap_log ? cap_log : log0 + 1u;
+            H.flags |= 1u;
+        }
+    }
+    switch (k) {
+    case K10S_EV_AS_CREATE_POD_REQ: H.g_cur_pods += K; break;   // api_server.rs:151-155
+    case K10S_EV_PS_CREATE_POD_REQ: H.unsched_missing -= wave_sum_u32(cnt); break;
+    case K10S_EV_AS_CREATE_NODE_REQ: H.g_cur_nodes += K; break;
+    case K10S_EV_PS_CREATE_NODE_REQ: H.ps_node_count += K; break;
+    case K10S_EV_AS_CREATE_NODE_RESP:
+        H.pool_head = (pool_head + K) % S.n_slots;
+        H.pool_count -= K;
+        H.as_node_count += K;
+        break;
+    case K10S_EV_PS_NODE_ADDED: H.counters[K10S_C_PROCESSED_NODES] += K; break;
+    case K10S_EV_S_ADD_NODE: H.s_node_count += wave_sum_u32(cnt); break;
+    default: break;
+    }
+    if (cls >= 0) {
+        if (fwe == ftl && ftl - fhd < K10S_FQW) {
+            const uint32_t room = K10S_FQW - (ftl - fhd);
+            H.fq[cls].wend = ftl + (K < room ? K : room);
+        }
+        if (ftl == fhd) sl_mark(H, (uint32_t)cls);   // the ring was empty: a new head (source list)
+        H.fq[cls].tail = ftl + K;
+        H.fq[cls].last = te;
+        H.next_seq = seq0 + K;
+    }
+    if (k == K10S_EV_S_POD_SCHEDULE_REQ) {
+        // the K pushes in event order (the Rust BinaryHeap's sifts depend on the order)
+#if K10S_DEVICE
+        const uint32_t lane_a = (uint32_t)lane_id() < K ? run_ev(c, src, (uint32_t)lane_id()).a : 0u;
+#endif
+        for (uint32_t i = 0; i < K; i++) {
+#if K10S_DEVICE
+            const uint32_t p = (uint32_t)__builtin_amdgcn_readlane((int)lane_a, (int)i);
+#else
+            const uint32_t p = run_ev(c, src, i).a;
+#endif
+            QInfo q;
+            q.timestamp = t;
+            q.initial = t;
+            q.attempts = 1;
+            q.pod = p;
+            aq_push(c, q);
+        }
+    }
+    // ---- advance the source past events 0..K-2 (the loop's consume removes event K-1)
+    if (src == SRC_TRACE) {
+        H.trace_cursor = uniform_u32(H.trace_cursor) + (K - 1u);   // no skipped entry inside a run
+    } else {
+        const uint32_t hd = uniform_u32(H.fq[src].head) + (K - 1u);
+        const uint32_t we = uniform_u32(H.fq[src].wend);
+        H.fq[src].head = hd;
+        // the loop's consume refills the window when the head reaches its end: keep the head inside it
+        if ((int32_t)(hd - we) >= 0) fq_refill(c, src, hd);
+    }
+    H.counters[K10S_C_EVENTS] += K - 1u;
+#if K10S_PROF
+    H.prof[K10S_PROF_KIND0 + K10S_EV_NUM_KINDS + k] += K - 1u;
+#endif
+#if !K10S_DEVICE && defined(K10S_HOST_STATS)
+    k10s_host_stats[HS_RUN_REFUSED] -= 1;
+    k10s_host_stats[HS_RUNS] += 1;
+    k10s_host_stats[HS_RUN_EVENTS] += K;
+    k10s_host_stats[HS_EVENTS] += K - 1;
+#endif
+    return K;
+}
+
 // Returns 1 if the replica still has work (event budget exhausted), else 0.  The working header
 // c.H() is LDS on the device (staged by the kernel) and the replica's header in place on the host.
 K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, uint64_t budget) {
@@ -3755,6 +4200,7 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
     uint32_t status = K10S_REPLICA_RUNNING;
     const uint64_t t_loop = prof_now();
     sl_rebuild(c, ntr);  // the sorted source list, from the sources' heads
+    h->run_flags = (budget == 0 ? 1u : 0u) | (until_mode0 ? 2u : 0u);   // run_batch
     [[maybe_unused]] uint32_t it_stale = 0;
 #if !K10S_DEVICE && defined(K10S_HOST_STATS)
     uint32_t hs_next_before = 0xFFFFFFFFu;

@@ -52,6 +52,7 @@ def main():
                       "refills_per_fifo_pop": round(v["refill"] / max(v["fifo_pop"], 1), 4),
                       "rings": per_ring, "aq_pops": int(st[29]), "aq_hbm_reads": int(st[28]),
                       "sl_insert_pos_0_1_2_3plus": [int(st[32 + i]) for i in range(4)],
+                      "runs": int(st[38]), "run_events": int(st[39]), "runs_refused": int(st[40]),
                       "next_event_emitted_by_previous": round(int(st[36]) / ev, 4),
                       "next_event_emitted_by_previous_fifo": round(int(st[37]) / ev, 4)}, indent=1))
 
