@@ -243,17 +243,12 @@ K10S_HD void fail(Ctx& c, uint32_t code) {
 
 // Runs of one event kind handled together (defined with the event queue below); called by the
 // handlers of the run kinds.
-// (tuning knob, semantics-neutral: bit 0 the api-server / storage kinds, bit 1 the scheduler's)
+// (tuning knob, semantics-neutral: 0 = every event one by one)
 #ifndef K10S_RUNS
-#define K10S_RUNS 3
+#define K10S_RUNS 1
 #endif
 K10S_HD_NOINL uint32_t run_batch(Ctx& c, uint32_t k);
 #define K10S_RUN_CALL(c, k) (uniform_u32(run_batch((c), (k))) != 0u)
-#if K10S_RUNS & 1
-#define K10S_RUN(c, k) K10S_RUN_CALL(c, k)
-#else
-#define K10S_RUN(c, k) false
-#endif
 
 // ---- the scheduler's node cache (allocatable per node in name order: the scan target) -----------
 // Two layouts of the same values (Layout.packed, chosen per engine by make_layout):
@@ -2092,16 +2087,6 @@ K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
 // 4.6 % at C3, profiles/r02_v4_score_plugins_ab.json).
 K10S_HD void run_scheduling_cycle_plugins(Ctx& c, double t) { run_scheduling_cycle_t<true>(c, t); }
 
-K10S_HD void on_scheduler(Ctx& c, const HeapEv& e);
-// PodScheduleRequest and AddNodeToCache, out of line: both come in runs (run_batch), whose call stays
-// out of the event loop's body this way.
-K10S_WARM void on_sched_run(Ctx& c, K10S_EVARG) {
-    K10S_EV_PROLOGUE;
-    if (K10S_RUN_CALL(c, (uint32_t)e.kind)) return;
-    HeapEv ev = *ep;
-    uniform_event(ev);
-    on_scheduler(c, ev);
-}
 K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
     RepHdr* h = &c.H();
     switch (e.kind) {
@@ -2576,7 +2561,6 @@ K10S_WARM void on_ps(Ctx& c, K10S_EVARG) {
     const Params* pr = &c.P();
     switch (e.kind) {
     case K10S_EV_PS_CREATE_NODE_REQ: {
-        if (K10S_RUN(c, K10S_EV_PS_CREATE_NODE_REQ)) return;
         uint32_t def = e.b, n = e.a;
         if (c.V().node(n).flags & NF_PS_PRESENT) {
             fail(c, K10S_PANIC_DUPLICATE_NODE);
@@ -2598,7 +2582,6 @@ K10S_WARM void on_ps(Ctx& c, K10S_EVARG) {
         break;
     }
     case K10S_EV_PS_NODE_ADDED: {
-        if (K10S_RUN(c, K10S_EV_PS_NODE_ADDED)) return;
         uint32_t n = e.a;
         if (!(c.V().node(n).flags & NF_PS_PRESENT)) {
             fail(c, K10S_PANIC_MISSING_NODE);
@@ -2609,7 +2592,6 @@ K10S_WARM void on_ps(Ctx& c, K10S_EVARG) {
         break;
     }
     case K10S_EV_PS_CREATE_POD_REQ: {
-        if (K10S_RUN(c, K10S_EV_PS_CREATE_POD_REQ)) return;
         uint32_t p = e.a;
         const uint8_t pf = c.V().pod(p).flags;
         if (pf & PF_IN_PS) {
@@ -2798,7 +2780,6 @@ K10S_WARM void on_api_server(Ctx& c, K10S_EVARG) {
     const Scenario* sc = &c.S();
     switch (e.kind) {
     case K10S_EV_AS_CREATE_NODE_REQ: {
-        if (K10S_RUN(c, K10S_EV_AS_CREATE_NODE_REQ)) return;
         uint32_t def = e.b;
         uint32_t n = sc->def_node[def];
         h->g_cur_nodes += 1;  // api_server.rs:133-137
@@ -2807,7 +2788,6 @@ K10S_WARM void on_api_server(Ctx& c, K10S_EVARG) {
         break;
     }
     case K10S_EV_AS_CREATE_NODE_RESP: {  // handle_create_node (96-115)
-        if (K10S_RUN(c, K10S_EV_AS_CREATE_NODE_RESP)) return;
         uint32_t n = e.a;
         int32_t def = c.V().node(n).pend_def;
         if (def < 0) {
@@ -2838,7 +2818,6 @@ K10S_WARM void on_api_server(Ctx& c, K10S_EVARG) {
         break;
     }
     case K10S_EV_AS_CREATE_POD_REQ:
-        if (K10S_RUN(c, K10S_EV_AS_CREATE_POD_REQ)) return;
         h->g_cur_pods += 1;  // api_server.rs:151-155
         emit(c, K10S_EV_PS_CREATE_POD_REQ, pr->as_to_ps_network_delay, -1, e.a, 0, 0.0, FQ_AS_TO_PS);
         break;
@@ -3290,23 +3269,41 @@ K10S_COLD void on_metrics(Ctx& c, K10S_EVARG) {
 
 // (Round 2 inlined the api server's forwarding cases here, K10S_FAST_DISPATCH: VGPR spills 20 -> 77,
 // -3 % at C3, profiles/r02_v14_fast_dispatch_ab.json; not kept.)
+// The kinds that come in runs (run_batch) go through their own out-of-line entry: it tries the run
+// and otherwise calls the kind's handler.  The handlers themselves stay leaf functions (a call inside
+// on_api_server / on_ps made them save their return address and a VGPR to scratch on every event),
+// and the event loop pays one scalar mask test per event.
+#define K10S_RUN_KINDS ((1ull << K10S_EV_AS_CREATE_POD_REQ) | (1ull << K10S_EV_PS_CREATE_POD_REQ) |      \
+                        (1ull << K10S_EV_S_POD_SCHEDULE_REQ) | (1ull << K10S_EV_AS_CREATE_NODE_REQ) |    \
+                        (1ull << K10S_EV_PS_CREATE_NODE_REQ) | (1ull << K10S_EV_AS_CREATE_NODE_RESP) |   \
+                        (1ull << K10S_EV_PS_NODE_ADDED) | (1ull << K10S_EV_S_ADD_NODE))
+K10S_WARM void on_run_kind(Ctx& c, EvRef ep, uint32_t k) {
+    k = uniform_u32(k);
+    if (K10S_RUN_CALL(c, k)) return;
+    if (k <= K10S_EV_AS_CREATE_GROUP_REQ) {
+        on_api_server(c, ep);
+    } else if (k <= K10S_EV_PS_POD_REMOVED) {
+        on_ps(c, ep);
+    } else {
+        HeapEv e = *ep;
+        uniform_event(e);
+        on_scheduler(c, e);
+    }
+}
 K10S_HD void dispatch(Ctx& c, EvRef ep, uint32_t k) {
     if (!K10S_FULL_WAVE(XG_DISPATCH)) return;
     k = uniform_u32(k);   // wave-uniform by construction: scalar branches (see run_replica)
-    if (k <= K10S_EV_M_GAUGE_TICK) on_metrics(c, ep);
+    if (K10S_RUNS && ((K10S_RUN_KINDS >> k) & 1ull)) on_run_kind(c, ep, k);
+    else if (k <= K10S_EV_M_GAUGE_TICK) on_metrics(c, ep);
     else if (k <= K10S_EV_AS_CREATE_GROUP_REQ) on_api_server(c, ep);
     else if (k <= K10S_EV_PS_POD_REMOVED) {
         if (k == K10S_EV_PS_CA_REQ) on_ps_ca(c, ep);
         else on_ps(c, ep);
     }
     else if (k <= K10S_EV_S_REMOVE_POD) {
-        if ((K10S_RUNS & 2) && (k == K10S_EV_S_POD_SCHEDULE_REQ || k == K10S_EV_S_ADD_NODE)) {
-            on_sched_run(c, ep);
-        } else {
-            HeapEv e = *ep;
-            uniform_event(e);
-            on_scheduler(c, e);
-        }
+        HeapEv e = *ep;
+        uniform_event(e);
+        on_scheduler(c, e);
     } else if (k <= K10S_EV_N_REMOVE_POD) on_node(c, ep);
     else if (k <= K10S_EV_CA_RESP) on_ca(c, ep);
     else on_hpa(c, ep);
@@ -4139,7 +4136,32 @@ K10S_HD_NOINL uint32_t run_batch(Ctx& c, uint32_t k) {
         H.next_seq = seq0 + K;
     }
     if (k == K10S_EV_S_POD_SCHEDULE_REQ) {
-        // the K pushes in event order (the Rust BinaryHeap's sifts depend on the order)
+        // The K pushes in event order (the Rust BinaryHeap's sifts depend on the order).  Push i puts its
+        // entry (key t) at position n + i and sift_up stops at once when its parent's timestamp is <= t
+        // (queue.rs:29-33: `elem <= parent`); a parent inside the run has key t itself.  When that holds
+        // for every push whose parent is an older entry, the K pushes are K appends: one lane each, the
+        // parents read in one round trip instead of one dependent round trip per push.
+        const uint32_t n0 = uniform_u32(H.aq_size);
+        bool moves = false;
+        K10S_FOR_RUN(i, K) {
+            const uint32_t pos = n0 + i;
+            if (pos > 0 && (pos - 1u) / 2u < n0) moves |= total_key(aq_raw(c, (pos - 1u) / 2u).timestamp) > kt;
+        }
+        if (!wave_any(moves)) {
+            K10S_FOR_RUN(i, K) {
+                QInfo q;
+                q.timestamp = t;
+                q.initial = t;
+                q.attempts = 1;
+                q.pod = run_ev(c, src, i).a;
+                aq_put(c, n0 + i, q);
+            }
+            H.aq_size = n0 + K;
+            K = uniform_u32(K);
+            goto pushed;
+        }
+    }
+    if (k == K10S_EV_S_POD_SCHEDULE_REQ) {
 #if K10S_DEVICE
         const uint32_t lane_a = (uint32_t)lane_id() < K ? run_ev(c, src, (uint32_t)lane_id()).a : 0u;
 #endif
@@ -4157,6 +4179,7 @@ K10S_HD_NOINL uint32_t run_batch(Ctx& c, uint32_t k) {
             aq_push(c, q);
         }
     }
+pushed:
     // ---- advance the source past events 0..K-2 (the loop's consume removes event K-1)
     if (src == SRC_TRACE) {
         H.trace_cursor = uniform_u32(H.trace_cursor) + (K - 1u);   // no skipped entry inside a run
