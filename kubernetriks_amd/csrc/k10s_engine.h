@@ -248,6 +248,7 @@ K10S_HD void fail(Ctx& c, uint32_t code) {
 #define K10S_RUNS 1
 #endif
 K10S_HD_NOINL uint32_t run_batch(Ctx& c, uint32_t k);
+K10S_HD_NOINL uint32_t win_batch(Ctx& c);
 #define K10S_RUN_CALL(c, k) (uniform_u32(run_batch((c), (k))) != 0u)
 
 // ---- the scheduler's node cache (allocatable per node in name order: the scan target) -----------
@@ -533,7 +534,8 @@ extern "C" uint64_t k10s_host_stats[48];
 #endif
 enum { HS_EVENTS, HS_FIFO_POP, HS_REFILL, HS_HEAP_POP, HS_TRACE_POP, HS_SL_FAST, HS_SL_UPDATE, HS_EMIT_WIN,
        HS_EMIT_RING, HS_EMIT_HEAP, HS_SL_DIRTY, HS_SCANS, HS_REFILL_CLS0 = 12, HS_POP_CLS0 = 20, HS_AQ_HBM_GET = 28, HS_AQ_POP = 29, HS_SLPOS0 = 32,
-       HS_NEXT_EMITTED = 36, HS_NEXT_EMITTED_FIFO = 37, HS_RUNS = 38, HS_RUN_EVENTS = 39, HS_RUN_REFUSED = 40 };
+       HS_NEXT_EMITTED = 36, HS_NEXT_EMITTED_FIFO = 37, HS_RUNS = 38, HS_RUN_EVENTS = 39, HS_RUN_REFUSED = 40,
+       HS_WINDOWS = 41, HS_WIN_EVENTS = 42, HS_TILE_PICKS = 43, HS_TILE_RESCANS = 44 };
 // An emission changed source q's head: mark it for the source list.
 K10S_HD void sl_mark(RepHdr& H, uint32_t q) { H.sl_dirty |= 1u << q; }
 K10S_HD void pods_left_dec(RepHdr& H) { H.pods_left -= 1; }
@@ -1366,6 +1368,17 @@ K10S_D uint32_t screen_grp(const ScanGrp& g, uint32_t bits, uint32_t rc, uint64_
                          ((uint32_t)(l23.y > r23.y) << 3);
     return fit & ~out;
 }
+// The exact LeastAllocated score of a fitting node (scan_node_d's arithmetic; frc, frr: the request
+// as f64).
+K10S_D double la_exact(uint32_t ac, uint64_t ar, uint64_t rr, double frc, double frr) {
+    const double fac = (double)ac;
+    const double cs = div_rn((fac - frc) * 100.0, fac);
+    const uint2 w = __builtin_bit_cast(uint2, ar);
+    const double far = u64_f64(ar);
+    double dr = far - frr;
+    if (__builtin_expect(w.y >= (1u << 21), 0)) dr = u64_f64(ar - rr);
+    return (cs + div_rn(dr * 100.0, far)) * 0.5;
+}
 // A fitting node the screen did not rule out: the lane best's allocatables take the index (same
 // score), anything else is scored exactly (as scan_node_d).
 K10S_D void score_node_exact(uint32_t n, uint32_t ac, uint64_t ar, uint64_t rr, double frc, double frr, double& best_s,
@@ -1374,13 +1387,7 @@ K10S_D void score_node_exact(uint32_t n, uint32_t ac, uint64_t ar, uint64_t rr, 
         best_n = (int32_t)n;
         return;
     }
-    const double fac = (double)ac;
-    const double cs = div_rn((fac - frc) * 100.0, fac);
-    const uint2 w = __builtin_bit_cast(uint2, ar);
-    const double far = u64_f64(ar);
-    double dr = far - frr;
-    if (__builtin_expect(w.y >= (1u << 21), 0)) dr = u64_f64(ar - rr);
-    const double s = (cs + div_rn(dr * 100.0, far)) * 0.5;
+    const double s = la_exact(ac, ar, rr, frc, frr);
     if (s >= best_s) {
         best_s = s;
         best_n = (int32_t)n;
@@ -1864,6 +1871,216 @@ K10S_HD uint32_t fit_tile(const uint64_t* s_node, uint32_t n_nodes, const uint32
     return found;
 }
 
+// ---- best-node pass of a cycle tile (exact picks for the pods that fit) --------------------------
+// K10S_TILE_BEST=1: the tile's shared read also finds where each pod of the tile goes, and the pods
+// that fit are placed from it instead of by one full scan each.
+// Lanes: node n belongs to lane (n >> 2) & 63, the scans' layout (a lane's 4 consecutive nodes of
+// every 256-node step); S_L is lane L's share.  For every pod j of the tile and every lane L the pass
+// keeps b_jL, the (score, index) maximum over the nodes of S_L that fit j in the cache as it is when
+// the tile is formed (the snapshot).  Its screen (scan_screen) compares a node only with nodes the
+// same lane scored before, so b_jL is exactly that maximum.
+// Why the picks are the reference's: between the snapshot and pod j's turn the cycle changes the
+// cache only by reserve_node_resources on the nodes R that earlier pods of the tile were assigned
+// (scheduler.rs:118-123; nothing else runs inside a cycle, fit_tile above), so every node outside R
+// still has its snapshot entry.  The reference picks the (score, index) maximum over the nodes that
+// fit now (kube_scheduler.rs:140-148 over the name-ordered nodes, the last maximum), which is the
+// maximum over lanes of the maximum over S_L.  A lane whose share holds no node of R has all of its
+// nodes unchanged, so its maximum is b_jL.  Every other lane (at most |R| <= K10S_TILE - 1 of them)
+// rescans its own share under the current cache: n_nodes/64 entries per flagged lane, all flagged
+// lanes together.  The maximum of the lane values is the pick, and no lane value means no node fits
+// (NoSufficientResources).  A pod that fits no node of the snapshot fits none now (fit_tile above).
+// The pass costs one read of the cache per tile; a placement otherwise costs a full read of its own.
+// Measured and not kept (default 0, profiles/r05_ab5_tile_best.json): on the backlog line it cuts
+// the entries read per placement from 6,511 to 4,467 but takes 3,780 ms per launch instead of 2,290
+// (the pass's per-pod lane state spills at 64 VGPRs, 74 % of the picks need a rescan, and the
+// cycle's bookkeeping, not its reads, dominates that regime); C3 never runs tiles but lost 2.7 % to
+// the larger callee's register clobbers.  Kept as a knob with its parity tests
+// (tests/test_cycle_tile.py::test_tile_best_variant_host).
+#ifndef K10S_TILE_BEST
+#define K10S_TILE_BEST 0
+#endif
+// Tile pod j's request: rc, rr (> 0, within the packed fields), their f64 and f32 forms.
+struct TileReq {
+    K10S_GB(const PodState) P;   // the pod's line: the exact test reads the requests from it
+    float fa, fr;                // device: the request as f32 (the screen)
+};
+K10S_HD TileReq tile_req(K10S_GB(const PodState) P, uint32_t rc, uint64_t rr) {
+    TileReq q;
+#if K10S_DEVICE
+    // all wave-uniform: kept in SGPRs through the pass
+    q.P = P;
+    q.fa = __builtin_bit_cast(float, uniform_u32(__builtin_bit_cast(uint32_t, (float)rc)));
+    q.fr = __builtin_bit_cast(float, uniform_u32(__builtin_bit_cast(uint32_t, __builtin_fmaf((float)(uint32_t)(rr >> 32), 4294967296.0f, (float)(uint32_t)rr))));
+#else
+    q.P = P;
+    q.fa = q.fr = 0.0f;
+#endif
+    return q;
+}
+#if K10S_DEVICE
+// A lane's 4 consecutive packed entries at n0 (clamped address, as scan_load_pk) and, once for all
+// pods of the tile, their allocatables as f32 (the screen's A and R).  The f32 conversions are
+// monotone (R = fl(hi·2^32 + fl(lo)) rounds twice, both monotone; the request's fa, fr the same
+// way), so a node that fits (cpu >= rc, ram >= rr) has A >= fa and R >= fr: the f32 test keeps every
+// fitting node, and the survivors are tested exactly on the entry, reloaded.
+struct TileGrp {
+    f32x2 A01, A23, R01, R23;
+};
+typedef K10S_GB(const uint64_t) NodeCachePtr;   // the packed cache, global address space
+K10S_D void tile_load(ulonglong2 (&x)[2], NodeCachePtr s_node, uint32_t n_nodes, uint32_t n0) {
+    const uint32_t a = n0 < n_nodes ? n0 : 0u;
+    x[0] = *reinterpret_cast<K10S_GB(const ulonglong2)>(s_node + a);
+    x[1] = *reinterpret_cast<K10S_GB(const ulonglong2)>(s_node + a + 2);
+}
+K10S_D TileGrp tile_convert(const ulonglong2 (&x)[2]) {
+    const uint64_t e[4] = {x[0].x, x[0].y, x[1].x, x[1].y};
+    float A[4], R[4];
+    K10S_UNROLL
+    for (int k = 0; k < 4; k++) {
+        const uint32_t hi = (uint32_t)(e[k] >> 32);
+        A[k] = cvt_f32_u32(hi >> 8);
+        R[k] = __builtin_fmaf(cvt_f32_u32(hi & 0xFFu), 4294967296.0f, cvt_f32_u32((uint32_t)e[k]));
+    }
+    TileGrp g;
+    g.A01 = f32x2{A[0], A[1]};
+    g.A23 = f32x2{A[2], A[3]};
+    g.R01 = f32x2{R[0], R[1]};
+    g.R23 = f32x2{R[2], R[3]};
+    return g;
+}
+// One pod over a lane's group at n0 (bits: the nodes in range): the f32 fit test, the screen against
+// the lane's own best (scan_screen; T from its score, +inf before it has one), then the survivors in
+// ascending order: exact Fit on the reloaded entry (absent nodes hold 0 and fit nothing), the exact
+// score, ">=" keeping the last maximum.
+K10S_D void tile_best_grp(const TileGrp& g, uint32_t bits, NodeCachePtr s_node, uint32_t n0, const TileReq& q,
+                          double& bs, int32_t& bn) {
+    const float T = bn < 0 ? __builtin_inff() : screen_u(bs) + K10S_SCREEN_EPS;
+    const f32x2 va = {q.fa, q.fa}, vr = {q.fr, q.fr}, vT = {T, T};
+    const f32x2 l01 = __builtin_elementwise_fma(va, g.R01, vr * g.A01), l23 = __builtin_elementwise_fma(va, g.R23, vr * g.A23);
+    const f32x2 r01 = (g.A01 * g.R01) * vT, r23 = (g.A23 * g.R23) * vT;
+    const uint32_t keep = (uint32_t)(g.A01.x >= q.fa && g.R01.x >= q.fr && !(l01.x > r01.x)) |
+                          ((uint32_t)(g.A01.y >= q.fa && g.R01.y >= q.fr && !(l01.y > r01.y)) << 1) |
+                          ((uint32_t)(g.A23.x >= q.fa && g.R23.x >= q.fr && !(l23.x > r23.x)) << 2) |
+                          ((uint32_t)(g.A23.y >= q.fa && g.R23.y >= q.fr && !(l23.y > r23.y)) << 3);
+    uint32_t need = keep & bits;
+    // one exact test in the code (an innermost loop, no calls)
+    while (need) {
+        const uint32_t k = (uint32_t)__builtin_ctz(need);
+        need &= need - 1u;
+        const uint64_t x = s_node[n0 + k];
+        const uint32_t ac = (uint32_t)(x >> K10S_PK_SHIFT);
+        const uint64_t ar = x & K10S_PK_RAM;
+        const uint32_t rc = uniform_u32(q.P->req_cpu);
+        const uint64_t rr = uniform_u64(q.P->req_ram);
+        if (rc <= ac && rr <= ar) {
+            const double s = la_exact(ac, ar, rr, (double)rc, u64_f64(rr));
+            if (s >= bs) {
+                bs = s;
+                bn = (int32_t)(n0 + k);
+            }
+        }
+    }
+}
+K10S_D uint32_t tile_bits(uint32_t n0, uint32_t n_nodes) {
+    return n0 < n_nodes ? (n_nodes - n0 >= 4 ? 0xFu : (1u << (n_nodes - n0)) - 1u) : 0u;
+}
+// The pass: b_jL for every pod j of need (bs: score, bn: index, -1 none), one read of the cache,
+// one 256-node step per iteration with the next step's loads in flight.  Out of line (its own
+// registers: 8 pods' lane state, 24 VGPRs, beside the cycle's); the tile's pod j is the queue entry
+// at slot_top[-j], its requests read here.
+__device__ __attribute__((noinline)) void tile_best_pass(NodeCachePtr s_node, uint32_t n_nodes,
+                                                        K10S_GB(const QInfo) slot_top, K10S_GB(const PodState) pods,
+                                                        uint32_t need, double* bs, int32_t* bn) {
+    // (a callee's arguments arrive in VGPRs: say which are wave-uniform)
+    s_node = (NodeCachePtr)uniform_u64((uint64_t)s_node);
+    slot_top = (K10S_GB(const QInfo))uniform_u64((uint64_t)slot_top);
+    pods = (K10S_GB(const PodState))uniform_u64((uint64_t)pods);
+    n_nodes = uniform_u32(n_nodes);
+    need = uniform_u32(need);
+    const uint32_t l4 = 4u * (uint32_t)lane_id();
+    TileReq q[K10S_TILE];
+    K10S_UNROLL
+    for (int j = 0; j < K10S_TILE; j++) {
+        if ((need >> j) & 1u) {
+            const uint32_t p = uniform_u32(slot_top[-j].pod);
+            q[j] = tile_req(pods + p, pods[p].req_cpu, pods[p].req_ram);
+        } else {
+            q[j] = tile_req(pods, 0, 0);
+        }
+    }
+    K10S_UNROLL
+    for (int j = 0; j < K10S_TILE; j++) {
+        bs[j] = -__builtin_inf();
+        bn[j] = -1;
+    }
+    ulonglong2 x[2];
+    tile_load(x, s_node, n_nodes, l4);
+    for (uint32_t base = 0; base < n_nodes; base += 256) {
+        const TileGrp g = tile_convert(x);
+        tile_load(x, s_node, n_nodes, base + 256u + l4);
+        const uint32_t b = tile_bits(base + l4, n_nodes);
+        K10S_UNROLL
+        for (int j = 0; j < K10S_TILE; j++) {
+            if (!((need >> j) & 1u)) continue;   // wave-uniform
+            tile_best_grp(g, b, s_node, base + l4, q[j], bs[j], bn[j]);
+        }
+    }
+}
+// The rescan of the flagged lanes' shares for one pod under the current cache (the other lanes keep
+// their values); returns the entries read, summed over the wave.  Four 256-node steps per round trip.
+K10S_D uint32_t tile_lane_rescan(NodeCachePtr s_node, uint32_t n_nodes, bool flag, const TileReq& q, double& bs,
+                                 int32_t& bn) {
+    const uint32_t l4 = 4u * (uint32_t)lane_id();
+    uint32_t nread = 0;
+    if (flag) {
+        bs = -__builtin_inf();
+        bn = -1;
+    }
+    for (uint32_t base = 0; base < n_nodes; base += 1024) {
+        if (flag) {
+            ulonglong2 x[4][2];
+            K10S_UNROLL
+            for (int i = 0; i < 4; i++) tile_load(x[i], s_node, n_nodes, base + 256u * i + l4);
+            K10S_UNROLL
+            for (int i = 0; i < 4; i++) {
+                const uint32_t n0 = base + 256u * i + l4;
+                const uint32_t b = tile_bits(n0, n_nodes);
+                nread += (uint32_t)__builtin_popcount(b);
+                tile_best_grp(tile_convert(x[i]), b, s_node, n0, q, bs, bn);
+            }
+        }
+    }
+    return uniform_u32(wave_sum_u32(nread));
+}
+#else
+// Host form of the pass and the rescan, the 64 lanes simulated: for every lane L of lanes, (key, idx)
+// := the (score_key, index) maximum over the nodes of S_L that fit (rc, rr), idx -1 if none.
+// Returns the entries read (those of the lanes scanned).
+K10S_HD uint32_t tile_lanes_host(const uint64_t* s_node, uint32_t n_nodes, uint32_t rc, uint64_t rr, uint64_t lanes,
+                                 uint64_t* key, int32_t* idx) {
+    for (int L = 0; L < 64; L++)
+        if ((lanes >> L) & 1ull) {
+            key[L] = 0;
+            idx[L] = -1;
+        }
+    uint32_t nread = 0;
+    for (uint32_t n = 0; n < n_nodes; n++) {
+        const uint32_t L = (n >> 2) & 63u;
+        if (!((lanes >> L) & 1ull)) continue;
+        nread += 1;
+        const NcEnt v = nc_unpack(s_node[n]);
+        if (rc <= v.cpu && rr <= v.ram) {
+            const uint64_t k = score_key(la_score(v.cpu, v.ram, rc, rr));
+            if (k >= key[L] || idx[L] < 0) {
+                key[L] = k;
+                idx[L] = (int32_t)n;
+            }
+        }
+    }
+    return nread;
+}
+#endif
+
 // ---- scheduling cycle (scheduler.rs:246-334) ----------------------------------------------------
 // The cycle runs out of line on the device: it runs once per many events, and out of line its
 // attempt loop (the node scans, the queue pops) gets its own register allocation instead of sharing
@@ -1871,10 +2088,14 @@ K10S_HD uint32_t fit_tile(const uint64_t* s_node, uint32_t n_nodes, const uint32
 // on C3 and +16.7 % on the backlog workload, where cycles run many attempts
 // (profiles/r02_v5_knobs_ab.json).
 // One iteration of the cycle's loop (scheduler.rs:270-329) for a live pod q at cycle time t, with the
-// cycle's running duration and failure count; nofit: a tile's fit pass found no node for the pod
-// (its attempt then fails exactly as the scan would).
+// cycle's running duration and failure count.  pick: K10S_PICK_SCAN (scan the cache), K10S_PICK_NOFIT
+// (a tile found no node for the pod: its attempt fails exactly as the scan would), or the node a
+// tile resolved for it (exactly the scan's choice; the tile counted its reads).  Returns the node
+// the pod was assigned, or -1.
+#define K10S_PICK_SCAN (-1)
+#define K10S_PICK_NOFIT (-2)
 template <bool PLUG>
-K10S_HD void cycle_attempt(Ctx& c, double t, QInfo q, bool nofit, double& cycle_dur, uint32_t& fails) {
+K10S_HD int32_t cycle_attempt(Ctx& c, double t, QInfo q, int32_t pick, double& cycle_dur, uint32_t& fails) {
     RepHdr* h = &c.H();
     const double w = c.P().score_weight;
     const uint32_t p = q.pod;
@@ -1896,8 +2117,11 @@ K10S_HD void cycle_attempt(Ctx& c, double t, QInfo q, bool nofit, double& cycle_
         st = -1;
         uint32_t nread = 0;
         const uint64_t t_scan = prof_now();
-        if (nofit) {
-            st = K10S_SCHED_NO_SUFFICIENT_RESOURCES;   // (the tile's fit pass counted its reads)
+        if (pick == K10S_PICK_NOFIT) {
+            st = K10S_SCHED_NO_SUFFICIENT_RESOURCES;   // (the tile's pass counted its reads)
+        } else if (pick >= 0) {
+            st = K10S_SCHED_OK;
+            chosen = pick;
         } else if (PLUG) {
             st = schedule_scan_plugins(c, rc, rr, &chosen);
             nread = c.S().n_nodes;
@@ -1922,7 +2146,7 @@ K10S_HD void cycle_attempt(Ctx& c, double t, QInfo q, bool nofit, double& cycle_
         q.timestamp = t + cycle_dur;
         uq_insert(c, q);
         emit(c, K10S_EV_AS_POD_NOT_SCHEDULED, c.P().sched_to_as_network_delay, -1, p, 0, t + cycle_dur, FQ_SCHED_TO_AS);
-        return;
+        return -1;
     }
     const uint32_t n = (uint32_t)chosen;
     nc_reserve(c, n, rc, rr);  // reserve_node_resources (118-123)
@@ -1944,6 +2168,7 @@ K10S_HD void cycle_attempt(Ctx& c, double t, QInfo q, bool nofit, double& cycle_
     }
     est_add(h->est[K10S_EST_POD_SCHEDULE_TIME], sched_time);
     est_add(h->est[K10S_EST_POD_QUEUE_TIME], queue_t);
+    return (int32_t)n;
 }
 // The end of a cycle: the next one after max(its duration, the interval) (scheduler.rs:331-333).
 K10S_HD void cycle_end(Ctx& c, double cycle_dur, uint32_t fails) {
@@ -1963,7 +2188,7 @@ K10S_HD_NOINL void run_scheduling_cycle_t(Ctx& c, double t) {
         const QInfo q = aq_pop(c);
         K10S_PROF_ADD(c, PROF_AQPOP, t_aq);
         if (!pod_in_s(c, q.pod)) continue;   // removed from the cache (scheduler.rs:263-269)
-        cycle_attempt<PLUG>(c, t, q, false, cycle_dur, fails);
+        cycle_attempt<PLUG>(c, t, q, K10S_PICK_SCAN, cycle_dur, fails);
     }
     cycle_end(c, cycle_dur, fails);
 }
@@ -1974,6 +2199,9 @@ K10S_HD_NOINL void run_scheduling_cycle_t(Ctx& c, double t) {
 // same pops the loop would make) and kept in the queue array slots their pops vacated (slot top-1-j
 // for the j-th: the array only shrinks during a cycle; HBM part), a removed pod marked and later
 // skipped like the loop's `continue`; their fit is tested together, then each is attempted in order.
+// Error state: a capacity error (QUEUE_FULL / HEAP_FULL) mid-tile drops the tile's unattempted
+// entries, so aq_size / active_len of an errored replica is unspecified (the serial cycle would stop
+// popping one entry earlier); an errored replica's results are refused anyway.
 K10S_HD_NOINL void run_scheduling_cycle_tiles(Ctx& c, double t) {
     if (!K10S_FULL_WAVE(XG_CYCLE)) return;
     double cycle_dur = 0.0;
@@ -2019,14 +2247,47 @@ K10S_HD_NOINL void run_scheduling_cycle_tiles(Ctx& c, double t) {
             }
         }
         uint32_t found = 0;
+        const uint64_t* s_node = c.V().s_node();
+        const uint32_t N = c.S().n_nodes;
+#if K10S_TILE_BEST
+        // b_jL of every pod of need (device: lane L's own registers; host: the lanes simulated)
+#if K10S_DEVICE
+        double tbs[K10S_TILE];
+        int32_t tbn[K10S_TILE];
+#else
+        uint64_t tbk[K10S_TILE][64];
+        int32_t tbn[K10S_TILE][64];
+#endif
+        if (need && h->s_node_count > 0) {
+            const uint64_t t_fit = prof_now();
+#if K10S_DEVICE
+            tile_best_pass((NodeCachePtr)s_node, N, (K10S_GB(const QInfo))(slot + (top - 1)),
+                           (K10S_GB(const PodState))&c.V().pod(0), need, tbs, tbn);
+            K10S_UNROLL
+            for (int j = 0; j < K10S_TILE; j++)
+                if (__ballot(tbn[j] >= 0)) found |= 1u << j;
+#else
+            for (int j = 0; j < K10S_TILE; j++) {   // (one shared read on the device)
+                if (!((need >> j) & 1u)) continue;
+                tile_lanes_host(s_node, N, rc8[j] >> 8, rrq[j], ~0ull, tbk[j], tbn[j]);
+                for (int L = 0; L < 64; L++)
+                    if (tbn[j][L] >= 0) found |= 1u << j;
+            }
+#endif
+            h->counters[K10S_C_NODES_READ] += N;
+            K10S_PROF_ADD(c, PROF_SCAN, t_fit);
+        }
+#else
         if (need && h->s_node_count > 0) {
             uint32_t nread = 0;
             const uint64_t t_fit = prof_now();
-            found = fit_tile(c.V().s_node(), c.S().n_nodes, rc8, rrq, need, &nread);
+            found = fit_tile(s_node, N, rc8, rrq, need, &nread);
             h->counters[K10S_C_NODES_READ] += nread;
             K10S_PROF_ADD(c, PROF_SCAN, t_fit);
         }
+#endif
         const uint32_t nofit = (need & ~found) | never;
+        uint64_t rlanes = 0;   // lanes whose share holds a node reserved by this tile
         for (uint32_t j = 0; j < nt && !c.H().error_code; j++) {
             const QInfo q = slot[top - 1 - j];
             if (uniform_u32(q.pod) == 0xFFFFFFFFu) continue;
@@ -2035,7 +2296,60 @@ K10S_HD_NOINL void run_scheduling_cycle_tiles(Ctx& c, double t) {
             u.initial = uniform_f64(q.initial);
             u.attempts = uniform_u32(q.attempts);
             u.pod = uniform_u32(q.pod);
-            cycle_attempt<false>(c, t, u, (nofit >> j) & 1u, cycle_dur, fails);
+            int32_t pick = (nofit >> j) & 1u ? K10S_PICK_NOFIT : K10S_PICK_SCAN;
+#if K10S_TILE_BEST
+            if ((found >> j) & 1u) {   // fits some node of the snapshot: resolve from the lane values
+                const uint64_t t_pick = prof_now();
+                const uint32_t rc = uniform_u32(c.V().pod(u.pod).req_cpu);
+                const uint64_t rr = uniform_u64(c.V().pod(u.pod).req_ram);
+#if K10S_DEVICE
+                double s = tbs[j];
+                int32_t n = tbn[j];
+                if (rlanes) {
+                    const bool flag = (rlanes >> lane_id()) & 1ull;
+                    h->counters[K10S_C_NODES_READ] += tile_lane_rescan((NodeCachePtr)s_node, N, flag,
+                                                                   tile_req((K10S_GB(const PodState))&c.V().pod(u.pod), rc, rr), s, n);
+                }
+                uint64_t key = n >= 0 ? score_key(s) : 0;
+                wave_argmax(key, n);
+                n = (int32_t)uniform_u32((uint32_t)n);
+#else
+                if (rlanes) h->counters[K10S_C_NODES_READ] += tile_lanes_host(s_node, N, rc, rr, rlanes, tbk[j], tbn[j]);
+                uint64_t key = 0;
+                int32_t n = -1;
+                for (int L = 0; L < 64; L++)
+                    if (tbn[j][L] >= 0 && (tbk[j][L] > key || (tbk[j][L] == key && tbn[j][L] > n))) {
+                        key = tbk[j][L];
+                        n = tbn[j][L];
+                    }
+                K10S_HSTAT(HS_TILE_PICKS);
+                if (rlanes) K10S_HSTAT(HS_TILE_RESCANS);
+#endif
+                pick = n >= 0 ? n : K10S_PICK_NOFIT;
+#if !K10S_DEVICE && defined(K10S_TILE_DEBUG)
+                {
+                    int32_t ch = -1;
+                    const int st = schedule_scan<true, true>(nullptr, s_node, c.V().s_present(), N, rc, rr, 1.0, &ch);
+                    const int32_t want = st == K10S_SCHED_OK ? ch : K10S_PICK_NOFIT;
+                    if (want != pick) {
+                        fprintf(stderr, "TILE MISMATCH t=%.6f pod=%u j=%u pick=%d scan=%d rlanes=%llx nt=%u\n", t, u.pod, j, pick, want,
+                                (unsigned long long)rlanes, nt);
+                        for (uint32_t m = 0; m < N; m++) {
+                            const NcEnt v = nc_unpack(s_node[m]);
+                            fprintf(stderr, "  node %u cpu=%u ram=%llu pres=%d\n", m, v.cpu, (unsigned long long)v.ram,
+                                    (int)((c.V().s_present()[m >> 6] >> (m & 63)) & 1));
+                        }
+                        fprintf(stderr, "  rc=%u rr=%llu\n", rc, (unsigned long long)rr);
+                    }
+                }
+#endif
+                K10S_PROF_ADD(c, PROF_SCAN, t_pick);
+            }
+#endif
+            // every assignment of the tile marks its lane (a pod outside need, e.g. one zero
+            // request, is placed by the scan and changes the cache too)
+            const int32_t placed = cycle_attempt<false>(c, t, u, pick, cycle_dur, fails);
+            if (placed >= 0) rlanes |= 1ull << (((uint32_t)placed >> 2) & 63u);
         }
     }
     cycle_end(c, cycle_dur, fails);
@@ -2078,8 +2392,13 @@ K10S_HD void s_release(Ctx& c, uint32_t p) {  // release_node_resources (153-162
     node_bound_changed(c, (uint32_t)n);
 }
 
+// K10S_TILE_ALWAYS=1: every LeastAllocated-only cycle on the packed cache runs in tiles (A/B knob).
+#ifndef K10S_TILE_ALWAYS
+#define K10S_TILE_ALWAYS 0
+#endif
 K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
-    if (nc_packed(c) && c.P().score_weight == 1.0 && c.H().cyc_fails != 0) run_scheduling_cycle_tiles(c, t);
+    if (nc_packed(c) && c.P().score_weight == 1.0 && (K10S_TILE_ALWAYS || c.H().cyc_fails != 0))
+        run_scheduling_cycle_tiles(c, t);
     else run_scheduling_cycle_t<false>(c, t);
 }
 // A replica whose profile is not LeastAllocated alone (K10S_SCORE_PLUGINS builds only: the host
@@ -3277,23 +3596,40 @@ K10S_COLD void on_metrics(Ctx& c, K10S_EVARG) {
                         (1ull << K10S_EV_S_POD_SCHEDULE_REQ) | (1ull << K10S_EV_AS_CREATE_NODE_REQ) |    \
                         (1ull << K10S_EV_PS_CREATE_NODE_REQ) | (1ull << K10S_EV_AS_CREATE_NODE_RESP) |   \
                         (1ull << K10S_EV_PS_NODE_ADDED) | (1ull << K10S_EV_S_ADD_NODE))
+#ifndef K10S_WINDOWS
+#define K10S_WINDOWS 1
+#endif
+#define K10S_WIN_KINDS ((1ull << K10S_EV_AS_ASSIGN_REQ) | (1ull << K10S_EV_PS_ASSIGN_REQ) |                 \
+                        (1ull << K10S_EV_AS_ASSIGN_RESP) | (1ull << K10S_EV_N_BIND) |                       \
+                        (1ull << K10S_EV_AS_POD_STARTED) | (1ull << K10S_EV_PS_POD_STARTED))
+#define K10S_BATCH_KINDS (K10S_RUN_KINDS | (K10S_WINDOWS ? K10S_WIN_KINDS : 0ull))
+// the scheduler's handler out of line, for on_run_kind's fallback (the event loop inlines it)
+K10S_WARM void on_scheduler_ool(Ctx& c, EvRef ep) {
+    HeapEv e = *ep;
+    uniform_event(e);
+    on_scheduler(c, e);
+}
 K10S_WARM void on_run_kind(Ctx& c, EvRef ep, uint32_t k) {
     k = uniform_u32(k);
-    if (K10S_RUN_CALL(c, k)) return;
+    if ((K10S_RUN_KINDS >> k) & 1ull) {
+        if (K10S_RUN_CALL(c, k)) return;
+    } else {
+        if (uniform_u32(win_batch(c)) != 0u) return;
+    }
     if (k <= K10S_EV_AS_CREATE_GROUP_REQ) {
         on_api_server(c, ep);
     } else if (k <= K10S_EV_PS_POD_REMOVED) {
         on_ps(c, ep);
+    } else if (k <= K10S_EV_S_REMOVE_POD) {
+        on_scheduler_ool(c, ep);
     } else {
-        HeapEv e = *ep;
-        uniform_event(e);
-        on_scheduler(c, e);
+        on_node(c, ep);
     }
 }
 K10S_HD void dispatch(Ctx& c, EvRef ep, uint32_t k) {
     if (!K10S_FULL_WAVE(XG_DISPATCH)) return;
     k = uniform_u32(k);   // wave-uniform by construction: scalar branches (see run_replica)
-    if (K10S_RUNS && ((K10S_RUN_KINDS >> k) & 1ull)) on_run_kind(c, ep, k);
+    if (K10S_RUNS && ((K10S_BATCH_KINDS >> k) & 1ull)) on_run_kind(c, ep, k);
     else if (k <= K10S_EV_M_GAUGE_TICK) on_metrics(c, ep);
     else if (k <= K10S_EV_AS_CREATE_GROUP_REQ) on_api_server(c, ep);
     else if (k <= K10S_EV_PS_POD_REMOVED) {
@@ -4203,6 +4539,611 @@ pushed:
     return K;
 }
 
+// ---- windows of the assignment pipeline, handled together (round 5) -------------------------------
+// After a scheduling cycle places its pods, each placed pod p goes through six events at fixed offsets
+// from its assignment time T_p = t + (cycle duration so far) + sched_to_as (the offsets are the network
+// delays): AS_ASSIGN_REQ, PS_ASSIGN_REQ (+as_to_ps), AS_ASSIGN_RESP (+as_to_ps), N_BIND (+as_to_node),
+// AS_POD_STARTED (+as_to_node), PS_POD_STARTED (+as_to_ps).  The pods of a cycle are 4 us apart, so in
+// dslab order the six kinds interleave event by event: no two consecutive events share a kind (no run),
+// yet within any as_to_ps-long stretch (50 ms at C3) they are independent.  A window is such a stretch:
+// the next W events in dslab order, taken from the delay-class rings (their first 16 entries each, the
+// first four rings of the source list), handled as W lanes at once.
+//
+// Why it is exact.  (1) The window is a prefix of dslab's order: the rings' candidates are merged by
+// (time, id) (ranks by binary search), and the window stops before the first event that is not a
+// candidate — a later source's head, a ring's 16th entry, an event past the time limit — or not one
+// of the six kinds.  (2) Nothing a window event emits can precede a later window event: every
+// emission of these kinds is at least min(as_to_ps, as_to_node) after its event (the finish of N_BIND
+// adds the pod's duration >= 0), every window event is at most that far after the first one, and an
+// emission at an equal time has a larger id.  (3) The handlers commute inside a window: each writes
+// only its own pod's line (two events of one pod never share a window), storage's copy of its node
+// (PS_ASSIGN_REQ: two assignments to one node never share a window), its node component's slot
+// (N_BIND: likewise per slot), commutative header counters and the group's running count (an atomic
+// add), and it reads nothing the others write.  Emissions get the ids a serial run would hand out
+// (next_seq plus the emission counts of the earlier window events, N_BIND's finish before its start)
+// and are appended to their rings in that order (one delay per ring: times stay sorted); the finishes
+// go into the event heap one by one.  Every reference panic of these handlers, a full ring or heap,
+// the cluster autoscaler (storage's assignment lists) or signed event times end the window before the
+// event (or refuse it), and the serial path then handles that event.
+#define K10S_WIN_PER_SRC 16
+struct WinEv {
+    double time, x;
+    uint32_t seq, kind, a, b, src;
+    int32_t slot;
+};
+// What a window event's handler needs of the replica's state (loaded once, checked, then applied).
+struct WinSt {
+    uint32_t rc, pf, nf, nep, ncpu, srun, removed, sflags, emits;
+    uint64_t rr, nram;
+    int32_t as_slot, snode, prs, g;
+    double dur;
+    bool pending;
+};
+// Entry i (< count) of ring q as the event loop would see it (LDS window below wend, else HBM).
+K10S_HD HeapEv win_ring_entry(Ctx& c, uint32_t q, uint32_t i) {
+    const RepHdr& H = c.H();
+    const uint32_t hd = H.fq[q].head, we = H.fq[q].wend, pos = hd + i;
+    if (pos - hd < we - hd) return H.fq_win[q * K10S_FQW + (pos & (K10S_FQW - 1))];
+    return c.V().fq()[q * c.Ly().cap_fq + (pos & (c.Ly().cap_fq - 1))];
+}
+K10S_HD WinSt win_load(Ctx& c, const WinEv& e) {
+    WinSt s;
+    s.rc = s.pf = s.nf = s.nep = s.ncpu = s.srun = s.removed = s.sflags = s.emits = 0;
+    s.rr = s.nram = 0;
+    s.as_slot = s.snode = s.prs = s.g = -1;
+    s.dur = 0.0;
+    s.pending = false;
+    switch (e.kind) {
+    case K10S_EV_AS_ASSIGN_REQ:   // api_server.rs:163-192
+        s.as_slot = c.V().node(e.b).as_slot;
+        s.pending = c.H().pend_rm_n != 0 && bit_test(c.V().pend_rm(), c.S().node_uid[e.b]);
+        s.emits = (s.pending || s.as_slot < 0) ? 0u : 1u;
+        break;
+    case K10S_EV_PS_ASSIGN_REQ: {   // persistent_storage.rs:250-294
+        const PodState& P = c.V().pod(e.a);
+        const NodeState& N = c.V().node(e.b);
+        s.pf = P.flags;
+        s.rc = P.req_cpu;
+        s.rr = P.req_ram;
+        s.nf = N.flags;
+        s.nep = N.ps_epoch;
+        s.ncpu = N.ps_cpu;
+        s.nram = N.ps_ram;
+        s.emits = 1;
+        break;
+    }
+    case K10S_EV_AS_ASSIGN_RESP:   // api_server.rs:194-217
+        s.as_slot = c.V().node(e.b).as_slot;
+        s.emits = 1;
+        break;
+    case K10S_EV_N_BIND: {   // node_component.rs:181-202, 114-175
+        const SlotState& SL = c.V().slot(e.slot);
+        const PodState& P = c.V().pod(e.a);
+        s.removed = SL.removed;
+        s.snode = SL.node;
+        s.srun = (uint32_t)SL.running;
+        s.prs = P.run_slot;
+        s.dur = P.dur;
+        s.rc = P.req_cpu;
+        s.rr = P.req_ram;
+        s.sflags = c.S().pod_flags[e.a];
+        s.g = c.S().pod_group[e.a];
+        s.emits = (s.sflags & POD_HAS_DUR) ? 2u : 1u;
+        break;
+    }
+    case K10S_EV_AS_POD_STARTED:   // api_server.rs:233-245
+        s.emits = 1;
+        break;
+    default:   // K10S_EV_PS_POD_STARTED (persistent_storage.rs:309-314): no emission
+        s.pf = c.V().pod(e.a).flags;
+        break;
+    }
+    return s;
+}
+// Would the serial handler panic (or do what the window does not model)?  Then the window ends here.
+K10S_HD bool win_bad(Ctx& c, const WinEv& e, const WinSt& s) {
+    switch (e.kind) {
+    case K10S_EV_PS_ASSIGN_REQ: return !(s.pf & PF_IN_PS) || !(s.nf & NF_PS_PRESENT) || (s.nf & NF_CA_ORIGIN);
+    case K10S_EV_AS_ASSIGN_RESP: return s.as_slot < 0;
+    case K10S_EV_N_BIND: return s.removed != 0 || s.snode != (int32_t)e.b || s.prs >= 0;
+    case K10S_EV_PS_POD_STARTED: return (!K10S_TIME_KEY_ID || c.H().ps_rm_n != 0) && !(s.pf & PF_IN_PS);
+    default: return false;
+    }
+}
+// The state writes of one window event (its emissions are written by the caller).  fseq: the id of
+// N_BIND's finish self-event.
+K10S_HD void win_apply(Ctx& c, const WinEv& e, const WinSt& s, uint32_t fseq) {
+    switch (e.kind) {
+    case K10S_EV_PS_ASSIGN_REQ: {
+        PodState& P = c.V().pod(e.a);
+        NodeState& N = c.V().node(e.b);
+        P.ps_assigned = (int32_t)e.b;
+        if (s.pf & PF_UNSCHED) P.flags = (uint8_t)(s.pf & ~PF_UNSCHED);
+        N.ps_cpu = s.ncpu - s.rc;
+        N.ps_ram = s.nram - s.rr;
+        P.ps_aepoch = s.nep;
+        break;
+    }
+    case K10S_EV_N_BIND: {
+        c.V().slot(e.slot).running = (int32_t)s.srun + 1;
+        PodState& P = c.V().pod(e.a);
+        P.run_slot = e.slot;
+        P.finish_seq = fseq;
+        if (c.Ly().cap_gauge) {
+            c.V().g_cpu()[e.slot] -= s.rc;
+            c.V().g_ram()[e.slot] -= s.rr;
+        }
+        if (s.g >= 0) {
+#if K10S_DEVICE
+            atomicAdd(&c.V().grp()[s.g].running, 1u);
+#else
+            c.V().grp()[s.g].running += 1;
+#endif
+        }
+        break;
+    }
+    case K10S_EV_PS_POD_STARTED:
+        if (c.V().prec()) c.V().prec()[e.a].t_running = e.x;
+        break;
+    default:
+        break;
+    }
+}
+// The ring emission of a window event (AS_TO_PS or AS_TO_NODE class), id seq.
+K10S_HD HeapEv win_ring_emission(const Params& pr, const WinEv& e, uint32_t seq) {
+    HeapEv o;
+    o.seq = seq;
+    o.slot = -1;
+    o.a = e.a;
+    o.b = 0;
+    o.x = 0.0;
+    switch (e.kind) {
+    case K10S_EV_AS_ASSIGN_REQ:
+        o.kind = K10S_EV_PS_ASSIGN_REQ, o.time = e.time + pr.as_to_ps_network_delay, o.b = e.b, o.x = e.x;
+        break;
+    case K10S_EV_PS_ASSIGN_REQ:
+        o.kind = K10S_EV_AS_ASSIGN_RESP, o.time = e.time + pr.as_to_ps_network_delay, o.b = e.b;
+        break;
+    case K10S_EV_AS_ASSIGN_RESP:   // the slot found by win_load is the event's (e.slot is set by the caller)
+        o.kind = K10S_EV_N_BIND, o.time = e.time + pr.as_to_node_network_delay, o.b = e.b, o.slot = e.slot;
+        break;
+    case K10S_EV_N_BIND:
+        o.kind = K10S_EV_AS_POD_STARTED, o.time = e.time + pr.as_to_node_network_delay, o.x = e.time;
+        break;
+    default:   // K10S_EV_AS_POD_STARTED
+        o.kind = K10S_EV_PS_POD_STARTED, o.time = e.time + pr.as_to_ps_network_delay, o.x = e.x;
+        break;
+    }
+    return o;
+}
+K10S_HD uint32_t win_ring_of(uint32_t kind) {   // the emission's delay class (N_BIND: its start)
+    return (kind == K10S_EV_AS_ASSIGN_RESP || kind == K10S_EV_N_BIND) ? (uint32_t)FQ_AS_TO_NODE : (uint32_t)FQ_AS_TO_PS;
+}
+// One event into the dslab heap (emit's heap path with a given id; capacity checked by the caller).
+K10S_HD void heap_insert(Ctx& c, const HeapEv& e) {
+    RepHdr& H = c.H();
+    const int64_t k = total_key(e.time);
+    uint32_t pos = uniform_u32(H.heap_size);
+    H.heap_size = pos + 1;
+    [[maybe_unused]] uint32_t it = 0;
+    while (pos > 0) {
+        if (K10S_LOOP_CAP(it, 12, XG_LOOP_EMIT)) break;
+        const uint32_t parent = (pos - 1) / K10S_HEAP_D;
+        HeapEv p = heap_get(c, parent);
+        uniform_event(p);
+        const int64_t kp = total_key(p.time);
+        if (!(k < kp || (k == kp && e.seq < p.seq))) break;
+        heap_put(c, pos, p);
+        pos = parent;
+    }
+    heap_put(c, pos, e);
+    if (pos == 0) {
+        H.heap_top = e;
+        sl_mark(H, SRC_HEAP);
+    }
+}
+
+// Called by the handler entry of the current event (a window kind at the head of ring sl[0].src; the
+// clock is its time): handle the window it starts (W >= 2 events) and return W, or 0 (nothing written).
+// Like run_batch, events 1..W-1 are logged and counted here, the rings are advanced past every window
+// event except the current one (the event loop's consume removes it) and every ring touched is marked
+// for the source list.
+K10S_HD_NOINL uint32_t win_batch(Ctx& c) {
+    RepHdr& H = c.H();
+    const uint32_t fl = uniform_u32(H.run_flags);
+    if (!(fl & 1u) || (!(fl & 2u) && (int64_t)uniform_u64((uint64_t)H.pods_left) <= 0)) return 0;
+    if (!c.Ly().tnonneg || c.S().ca_enabled || !c.Ly().cap_fq) return 0;
+    const uint32_t src0 = uniform_u32(H.sl[0].src);
+    if (src0 >= (uint32_t)K10S_NFQ) return 0;
+    const Params& pr = c.P();
+    const double t0 = uniform_f64(H.clock), lim = uniform_f64(H.run_limit);
+    const double d_ps = pr.as_to_ps_network_delay, d_node = pr.as_to_node_network_delay;
+    const double tlook = t0 + (d_ps < d_node ? d_ps : d_node);
+    const int64_t kmax = total_key(tlook < lim ? tlook : lim);   // a candidate's time is at most this
+    // the first (up to) four rings of the source list; the first other source bounds the window
+    const uint32_t sn = uniform_u32(H.sl_n);
+    uint32_t srcs[4] = {0u, 0u, 0u, 0u};
+    uint32_t m = 0;
+    int64_t bk = 0x7FFFFFFFFFFFFFFFll;
+    uint32_t bs = 0xFFFFFFFFu;
+    for (uint32_t i = 0; i < sn; i++) {
+        const uint32_t s = uniform_u32(H.sl[i].src);
+        if (s < (uint32_t)K10S_NFQ && m < 4) {
+            if (m == 0) srcs[0] = s;
+            else if (m == 1) srcs[1] = s;
+            else if (m == 2) srcs[2] = s;
+            else srcs[3] = s;
+            m++;
+            continue;
+        }
+        bk = (int64_t)uniform_u64((uint64_t)H.sl[i].key);
+        bs = uniform_u32(H.sl[i].seq);
+        break;
+    }
+    // a ring holding more than K10S_WIN_PER_SRC entries: its 16th bounds the window (only 15 are used)
+    for (uint32_t j = 0; j < m; j++) {
+        const uint32_t q = j == 0 ? srcs[0] : j == 1 ? srcs[1] : j == 2 ? srcs[2] : srcs[3];
+        if (uniform_u32(H.fq[q].tail - H.fq[q].head) > K10S_WIN_PER_SRC) {
+            const HeapEv b = win_ring_entry(c, q, K10S_WIN_PER_SRC - 1);
+            const int64_t kb = (int64_t)uniform_u64((uint64_t)total_key(b.time));
+            const uint32_t sb = uniform_u32(b.seq);
+            if (sl_less(kb, sb, bk, bs)) bk = kb, bs = sb;
+        }
+    }
+    uint32_t W = 0, V = 0;
+#if K10S_DEVICE
+    // ---- candidates: lane 16j + i holds entry i of ring srcs[j]
+    const uint32_t lane = (uint32_t)lane_id();
+    const uint32_t grp = lane >> 4, gi = lane & 15u;
+    const uint32_t myq = grp == 0 ? srcs[0] : grp == 1 ? srcs[1] : grp == 2 ? srcs[2] : srcs[3];
+    WinEv ev;
+    ev.time = 0.0;
+    ev.x = 0.0;
+    ev.seq = 0xFFFFFFFFu;
+    ev.kind = 0xFFFFu;
+    ev.a = ev.b = 0;
+    ev.slot = -1;
+    ev.src = myq;
+    int64_t key = 0x7FFFFFFFFFFFFFFFll;
+    bool valid = false;
+    if (grp < m && gi < H.fq[myq].tail - H.fq[myq].head) {
+        const HeapEv h = win_ring_entry(c, myq, gi);
+        ev.time = h.time;
+        ev.x = h.x;
+        ev.seq = h.seq;
+        ev.kind = h.kind;
+        ev.slot = h.slot;
+        ev.a = h.a;
+        ev.b = h.b;
+        key = total_key(h.time);
+        valid = key <= kmax && sl_less(key, ev.seq, bk, bs);
+    }
+    // (the valid entries of a ring are a prefix of its 16: keys increase along a ring)
+    const uint64_t vm = __ballot(valid);
+    V = (uint32_t)__popcll(vm);
+    if (V < 2) return 0;
+    // ---- rank = position in the merged (time, id) order: own index + the other rings' entries below
+    uint32_t rank = gi;
+    const uint32_t klo = (uint32_t)(uint64_t)key, khi = (uint32_t)((uint64_t)key >> 32);
+    K10S_UNROLL
+    for (uint32_t j = 0; j < 4; j++) {
+        if (j >= m) break;
+        const uint32_t vj = (uint32_t)__popcll((vm >> (16u * j)) & 0xFFFFull);
+        uint32_t lo = 0, hi = grp == j ? 0u : vj;
+        K10S_UNROLL
+        for (int step = 0; step < 5; step++) {   // binary search over <= 16 sorted entries
+            const uint32_t mid = (lo + hi) >> 1;
+            const int addr = (int)((16u * j + (mid < 15u ? mid : 15u)) * 4u);
+            const uint32_t xl = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)klo);
+            const uint32_t xh = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)khi);
+            const uint32_t xs = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)ev.seq);
+            const bool less = lo < hi && sl_less((int64_t)(((uint64_t)xh << 32) | xl), xs, key, ev.seq);
+            const bool go = lo < hi;
+            lo = go && less ? mid + 1u : lo;
+            hi = go && !less ? mid : hi;
+        }
+        rank += lo;
+    }
+    {   // invalid lanes take the ranks after V, in lane order
+        const uint32_t below = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(vm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)vm, 0u));
+        if (!valid) rank = V + (lane - below);
+    }
+    // ---- lanes into (time, id) order: lane r holds the window's r-th event
+    {
+        const int addr = (int)(rank * 4u);
+        auto mv = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)v); };
+        const uint64_t tb = f2u(ev.time), xb = f2u(ev.x);
+        const uint32_t t_lo = mv((uint32_t)tb), t_hi = mv((uint32_t)(tb >> 32));
+        const uint32_t x_lo = mv((uint32_t)xb), x_hi = mv((uint32_t)(xb >> 32));
+        ev.seq = mv(ev.seq);
+        const uint32_t ks = mv(ev.kind | ((uint32_t)(uint16_t)ev.slot << 16));
+        ev.a = mv(ev.a);
+        ev.b = mv(ev.b);
+        ev.src = mv(ev.src);
+        ev.time = u2f(((uint64_t)t_hi << 32) | t_lo);
+        ev.x = u2f(((uint64_t)x_hi << 32) | x_lo);
+        ev.kind = ks & 0xFFFFu;
+        ev.slot = (int32_t)(int16_t)(ks >> 16);
+    }
+    const uint32_t r = lane;
+    const bool live = r < V;
+    const bool wk = live && ((K10S_WIN_KINDS >> (ev.kind & 63u)) & 1ull) != 0 && ev.kind < 64u;
+    WinSt st;
+    st.rc = st.pf = st.nf = st.nep = st.ncpu = st.srun = st.removed = st.sflags = st.emits = 0;
+    st.rr = st.nram = 0;
+    st.as_slot = st.snode = st.prs = st.g = -1;
+    st.dur = 0.0;
+    st.pending = false;
+    if (wk) st = win_load(c, ev);   // (only window events: another kind's fields index other tables)
+    if (wk && ev.kind == K10S_EV_AS_ASSIGN_RESP) ev.slot = st.as_slot;   // N_BIND's component
+    bool stop = !wk || win_bad(c, ev, st);
+    // two events of one pod, two assignments to one node, two binds on one component: only the first
+    {
+        const uint32_t writer = wk && (ev.kind == K10S_EV_PS_ASSIGN_REQ || ev.kind == K10S_EV_N_BIND ||
+                                       ev.kind == K10S_EV_PS_POD_STARTED) ? 1u : 0u;
+        uint64_t wm = __ballot(writer != 0u) & (V >= 64u ? ~0ull : ((1ull << V) - 1ull));
+        while (wm) {
+            const uint32_t b = (uint32_t)__builtin_ctzll(wm);
+            wm &= wm - 1;
+            const uint32_t bk2 = (uint32_t)__builtin_amdgcn_readlane((int)ev.kind, (int)b);
+            const uint32_t ba = (uint32_t)__builtin_amdgcn_readlane((int)ev.a, (int)b);
+            const uint32_t bb = (uint32_t)__builtin_amdgcn_readlane((int)ev.b, (int)b);
+            const int32_t bsl = __builtin_amdgcn_readlane(ev.slot, (int)b);
+            stop |= r > b && (ev.a == ba || (ev.kind == bk2 && ((bk2 == K10S_EV_PS_ASSIGN_REQ && ev.b == bb) ||
+                                                                 (bk2 == K10S_EV_N_BIND && ev.slot == bsl))));
+        }
+    }
+    {
+        const uint64_t sm = __ballot(stop);
+        W = sm ? (uint32_t)__builtin_ctzll(sm) : 64u;
+    }
+    W = uniform_u32(W);
+    if (W < 2) return 0;
+    const bool in = r < W;
+    // ---- emissions: ids and ring positions in window order
+    const uint32_t ne = in ? st.emits : 0u;
+    const bool e_heap = in && ev.kind == K10S_EV_N_BIND && (st.sflags & POD_HAS_DUR);
+    const bool e_ring = ne > (e_heap ? 1u : 0u);
+    const uint32_t e_q = win_ring_of(ev.kind);
+    const bool e_ps = e_ring && e_q == (uint32_t)FQ_AS_TO_PS, e_node = e_ring && e_q == (uint32_t)FQ_AS_TO_NODE;
+    const uint64_t m1 = __ballot(ne >= 1u), m2 = __ballot(ne >= 2u), mps = __ballot(e_ps), mnd = __ballot(e_node);
+    const uint64_t mhp = __ballot(e_heap);
+    auto below = [&](uint64_t mk) {
+        return (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+    };
+    const uint32_t n_total = (uint32_t)__popcll(m1) + (uint32_t)__popcll(m2);
+    const uint32_t n_ps = (uint32_t)__popcll(mps), n_node = (uint32_t)__popcll(mnd), n_heap = (uint32_t)__popcll(mhp);
+    const uint32_t id0 = uniform_u32(H.next_seq) + below(m1) + below(m2);
+    // events consumed per ring (room for emissions into a ring that is also consumed)
+    uint32_t used[4];
+    K10S_UNROLL
+    for (uint32_t j = 0; j < 4; j++) used[j] = j < m ? (uint32_t)__popcll(__ballot(in && ev.src == (j == 0 ? srcs[0] : j == 1 ? srcs[1] : j == 2 ? srcs[2] : srcs[3]))) : 0u;
+#else
+    // ---- host: the merge of the rings, event by event
+    WinEv evs[64];
+    WinSt sts[64];
+    {
+        uint32_t cur[4] = {0u, 0u, 0u, 0u};
+        while (V < 64) {
+            int best = -1;
+            int64_t kbest = 0;
+            uint32_t sbest = 0;
+            HeapEv hb{};
+            for (uint32_t j = 0; j < m; j++) {
+                const uint32_t q = srcs[j];
+                if (cur[j] >= K10S_WIN_PER_SRC || cur[j] >= H.fq[q].tail - H.fq[q].head) continue;
+                const HeapEv h = win_ring_entry(c, q, cur[j]);
+                const int64_t kh = total_key(h.time);
+                if (best < 0 || sl_less(kh, h.seq, kbest, sbest)) best = (int)j, kbest = kh, sbest = h.seq, hb = h;
+            }
+            if (best < 0 || kbest > kmax || !sl_less(kbest, sbest, bk, bs)) break;
+            cur[best]++;
+            WinEv& e = evs[V++];
+            e.time = hb.time;
+            e.x = hb.x;
+            e.seq = hb.seq;
+            e.kind = hb.kind;
+            e.slot = hb.slot;
+            e.a = hb.a;
+            e.b = hb.b;
+            e.src = srcs[best];
+        }
+    }
+    if (V < 2) return 0;
+    for (W = 0; W < V; W++) {
+        WinEv& e = evs[W];
+        if (!((K10S_WIN_KINDS >> (e.kind & 63u)) & 1ull) || e.kind >= 64u) break;
+        sts[W] = win_load(c, e);
+        if (e.kind == K10S_EV_AS_ASSIGN_RESP) e.slot = sts[W].as_slot;
+        if (win_bad(c, e, sts[W])) break;
+        bool conf = false;
+        for (uint32_t b = 0; b < W; b++) {
+            const WinEv& o = evs[b];
+            const bool writer = o.kind == K10S_EV_PS_ASSIGN_REQ || o.kind == K10S_EV_N_BIND || o.kind == K10S_EV_PS_POD_STARTED;
+            conf |= writer && (e.a == o.a || (e.kind == o.kind && ((o.kind == K10S_EV_PS_ASSIGN_REQ && e.b == o.b) ||
+                                                                     (o.kind == K10S_EV_N_BIND && e.slot == o.slot))));
+        }
+        if (conf) break;
+    }
+    if (W < 2) return 0;
+    uint32_t n_total = 0, n_ps = 0, n_node = 0, n_heap = 0;
+    uint32_t used[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t r = 0; r < W; r++) {
+        const WinSt& s = sts[r];
+        const bool hp = evs[r].kind == K10S_EV_N_BIND && (s.sflags & POD_HAS_DUR);
+        n_total += s.emits;
+        n_heap += hp ? 1u : 0u;
+        if (s.emits > (hp ? 1u : 0u)) {
+            if (win_ring_of(evs[r].kind) == (uint32_t)FQ_AS_TO_PS) n_ps++;
+            else n_node++;
+        }
+        for (uint32_t j = 0; j < m; j++) used[j] += evs[r].src == srcs[j] ? 1u : 0u;
+    }
+#endif
+    // ---- what the serial path would place differently: then no window
+    const uint32_t seq0 = uniform_u32(H.next_seq);
+    if ((uint64_t)seq0 + n_total > 0xFFFFFFFFull) return 0;
+    if (n_heap && uniform_u32(H.heap_size) + n_heap > c.Ly().cap_heap) return 0;
+    const uint32_t cap = c.Ly().cap_fq;
+    uint32_t rhd[2], rtl[2], rwe[2];
+    for (uint32_t z = 0; z < 2; z++) {
+        const uint32_t q = z == 0 ? (uint32_t)FQ_AS_TO_PS : (uint32_t)FQ_AS_TO_NODE;
+        const uint32_t n = z == 0 ? n_ps : n_node;
+        rhd[z] = uniform_u32(H.fq[q].head);
+        rtl[z] = uniform_u32(H.fq[q].tail);
+        rwe[z] = uniform_u32(H.fq[q].wend);
+        if (!n) continue;
+        uint32_t consumed = 0;
+        for (uint32_t j = 0; j < m; j++) consumed += (j == 0 ? srcs[0] : j == 1 ? srcs[1] : j == 2 ? srcs[2] : srcs[3]) == q ? used[j] : 0u;
+        if (cap - (rtl[z] - rhd[z]) + consumed < n) return 0;
+        // the ring stays sorted: its first new entry is not before its newest one
+        const double d = z == 0 ? d_ps : d_node;
+        if (rtl[z] != rhd[z] && total_key(t0 + d) < total_key(uniform_f64(H.fq[q].last))) return 0;
+    }
+    const uint32_t cap_log = c.Ly().cap_log;
+    const uint32_t log0 = uniform_u32(H.log_n) - 1u;   // event 0 was logged by the event loop
+    double last_ps = 0.0, last_node = 0.0, tW = t0;
+    uint32_t unsched = 0;
+#if K10S_DEVICE
+    {
+        const uint32_t fseq = e_heap ? id0 : 0u;   // N_BIND: its finish first (id0), then its start
+        if (in) {
+            win_apply(c, ev, st, fseq);
+            if (ev.kind == K10S_EV_PS_ASSIGN_REQ && (st.pf & PF_UNSCHED)) unsched = 1;
+            if (cap_log && r > 0 && log0 + r < cap_log) {
+                k10s_log_entry le;
+                le.time = ev.time;
+                le.seq = ev.seq;
+                le.kind = (uint16_t)ev.kind;
+                le.slot = (int16_t)(ev.kind == K10S_EV_N_BIND ? ev.slot : -1);
+                le.pod = (int32_t)ev.a;
+                le.node = (ev.kind == K10S_EV_AS_POD_STARTED || ev.kind == K10S_EV_PS_POD_STARTED) ? -1 : (int32_t)ev.b;
+                c.V().log()[log0 + r] = le;
+            }
+        }
+        if (e_ring) {
+            const uint32_t z = e_ps ? 0u : 1u;
+            const uint32_t q = e_ps ? (uint32_t)FQ_AS_TO_PS : (uint32_t)FQ_AS_TO_NODE;
+            const uint32_t idx = e_ps ? below(mps) : below(mnd);
+            const uint32_t tl = z == 0 ? rtl[0] : rtl[1], hd = z == 0 ? rhd[0] : rhd[1], we = z == 0 ? rwe[0] : rwe[1];
+            const HeapEv o = win_ring_emission(pr, ev, id0 + (e_heap ? 1u : 0u));
+            c.V().fq()[q * cap + ((tl + idx) & (cap - 1))] = o;
+            if (we == tl && (tl - hd) + idx < K10S_FQW) H.fq_win[q * K10S_FQW + ((tl + idx) & (K10S_FQW - 1))] = o;
+        }
+        // the rings' newest times and the last event's time (lane readlanes of the last writers)
+        if (n_ps) last_ps = uniform_f64(__shfl(ev.time, 63 - (int)__builtin_clzll(mps))) + d_ps;
+        if (n_node) last_node = uniform_f64(__shfl(ev.time, 63 - (int)__builtin_clzll(mnd))) + d_node;
+        tW = uniform_f64(__shfl(ev.time, (int)W - 1));
+        // the finishes into the heap, one by one in window order
+        uint64_t hm = mhp;
+        while (hm) {
+            const uint32_t b = (uint32_t)__builtin_ctzll(hm);
+            hm &= hm - 1;
+            HeapEv f;
+            f.time = uniform_f64(__shfl(ev.time + (st.dur + d_node), (int)b));   // clock + delay, as emit
+            f.seq = uniform_u32((uint32_t)__builtin_amdgcn_readlane((int)id0, (int)b));
+            f.kind = (uint16_t)K10S_EV_N_POD_FINISHED;
+            f.slot = (int16_t)__builtin_amdgcn_readlane(ev.slot, (int)b);
+            f.a = uniform_u32((uint32_t)__builtin_amdgcn_readlane((int)ev.a, (int)b));
+            f.b = uniform_u32((uint32_t)__builtin_amdgcn_readlane((int)ev.b, (int)b));
+            f.x = uniform_f64(__shfl(ev.time + st.dur, (int)b));
+            heap_insert(c, f);
+        }
+    }
+    unsched = wave_sum_u32(unsched);
+#else
+    {
+        uint32_t id = seq0, ips = 0, ind = 0;
+        for (uint32_t r = 0; r < W; r++) {
+            const WinEv& e = evs[r];
+            const WinSt& s = sts[r];
+            const bool hp = e.kind == K10S_EV_N_BIND && (s.sflags & POD_HAS_DUR);
+            win_apply(c, e, s, hp ? id : 0u);
+            if (e.kind == K10S_EV_PS_ASSIGN_REQ && (s.pf & PF_UNSCHED)) unsched++;
+            if (cap_log && r > 0 && log0 + r < cap_log) {
+                k10s_log_entry le;
+                le.time = e.time;
+                le.seq = e.seq;
+                le.kind = (uint16_t)e.kind;
+                le.slot = (int16_t)(e.kind == K10S_EV_N_BIND ? e.slot : -1);
+                le.pod = (int32_t)e.a;
+                le.node = (e.kind == K10S_EV_AS_POD_STARTED || e.kind == K10S_EV_PS_POD_STARTED) ? -1 : (int32_t)e.b;
+                c.V().log()[log0 + r] = le;
+            }
+            if (hp) {
+                HeapEv f;
+                f.time = e.time + (s.dur + d_node);   // clock + delay, as emit
+                f.seq = id;
+                f.kind = (uint16_t)K10S_EV_N_POD_FINISHED;
+                f.slot = (int16_t)e.slot;
+                f.a = e.a;
+                f.b = e.b;
+                f.x = e.time + s.dur;
+                heap_insert(c, f);
+            }
+            const bool ring = s.emits > (hp ? 1u : 0u);
+            if (ring) {
+                const bool ps = win_ring_of(e.kind) == (uint32_t)FQ_AS_TO_PS;
+                const uint32_t z = ps ? 0u : 1u, q = ps ? (uint32_t)FQ_AS_TO_PS : (uint32_t)FQ_AS_TO_NODE;
+                const uint32_t idx = ps ? ips++ : ind++;
+                const HeapEv o = win_ring_emission(pr, e, id + (hp ? 1u : 0u));
+                c.V().fq()[q * cap + ((rtl[z] + idx) & (cap - 1))] = o;
+                if (rwe[z] == rtl[z] && (rtl[z] - rhd[z]) + idx < K10S_FQW)
+                    H.fq_win[q * K10S_FQW + ((rtl[z] + idx) & (K10S_FQW - 1))] = o;
+                if (ps) last_ps = o.time;
+                else last_node = o.time;
+            }
+            id += s.emits;
+        }
+        tW = evs[W - 1].time;
+    }
+#endif
+    wave_sync();
+    // ---- header: logs, counters, rings, ids, clock
+    if (cap_log) {   // (the loop logged event 0 at log0, or flagged the overflow)
+        if (log0 + W <= cap_log) H.log_n = log0 + W;
+        else {
+            H.log_n = log0 + 1u < cap_log ? cap_log : log0 + 1u;
+            H.flags |= 1u;
+        }
+    }
+    H.unsched_cache_count -= unsched;
+    for (uint32_t z = 0; z < 2; z++) {
+        const uint32_t n = z == 0 ? n_ps : n_node;
+        if (!n) continue;
+        const uint32_t q = z == 0 ? (uint32_t)FQ_AS_TO_PS : (uint32_t)FQ_AS_TO_NODE;
+        if (rwe[z] == rtl[z] && rtl[z] - rhd[z] < K10S_FQW) {
+            const uint32_t room = K10S_FQW - (rtl[z] - rhd[z]);
+            H.fq[q].wend = rtl[z] + (n < room ? n : room);
+        }
+        H.fq[q].tail = rtl[z] + n;
+        H.fq[q].last = z == 0 ? last_ps : last_node;
+        sl_mark(H, q);
+    }
+    H.next_seq = seq0 + n_total;
+    H.clock = tW;
+    H.counters[K10S_C_EVENTS] += W - 1u;
+    // ---- advance the rings past the window's events (the current one stays for the loop's consume)
+    for (uint32_t j = 0; j < m; j++) {
+        const uint32_t q = j == 0 ? srcs[0] : j == 1 ? srcs[1] : j == 2 ? srcs[2] : srcs[3];
+        const uint32_t n = used[j] - (q == src0 ? 1u : 0u);
+        if (!n) continue;
+        const uint32_t hd = uniform_u32(H.fq[q].head) + n, tl = uniform_u32(H.fq[q].tail), we = uniform_u32(H.fq[q].wend);
+        H.fq[q].head = hd;
+        if ((int32_t)(hd - we) >= 0) {
+            if (hd != tl) fq_refill(c, (int)q, hd);
+            else H.fq[q].wend = hd;
+        }
+        if (q != src0) sl_mark(H, q);
+    }
+#if !K10S_DEVICE && defined(K10S_HOST_STATS)
+    k10s_host_stats[HS_WINDOWS] += 1;
+    k10s_host_stats[HS_WIN_EVENTS] += W;
+    k10s_host_stats[HS_EVENTS] += W - 1;
+#endif
+    return W;
+}
+
 // Returns 1 if the replica still has work (event budget exhausted), else 0.  The working header
 // c.H() is LDS on the device (staged by the kernel) and the replica's header in place on the host.
 K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, uint64_t budget) {
@@ -4223,7 +5164,8 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
     uint32_t status = K10S_REPLICA_RUNNING;
     const uint64_t t_loop = prof_now();
     sl_rebuild(c, ntr);  // the sorted source list, from the sources' heads
-    h->run_flags = (budget == 0 ? 1u : 0u) | (until_mode0 ? 2u : 0u);   // run_batch
+    h->run_flags = (budget == 0 ? 1u : 0u) | (until_mode0 ? 2u : 0u);   // run_batch, win_batch
+    h->run_limit = limit;
     [[maybe_unused]] uint32_t it_stale = 0;
 #if !K10S_DEVICE && defined(K10S_HOST_STATS)
     uint32_t hs_next_before = 0xFFFFFFFFu;

@@ -243,6 +243,7 @@ struct RepHdr {
     double tr_time;               // cached head of the shared trace stream (valid while
     uint32_t tr_seq;              // trace_cursor < n_trace)
     uint32_t run_flags;           // this launch: bit 0 runs allowed (no event budget), bit 1 until-time mode
+    double run_limit;             // this launch's time limit (until_time or max_time): window events stay below
     uint32_t trace_prefix;        // workload events at file positions >= this are not in this
                                   // replica's trace (k10s_replica_params.workload_prefix; ~0 = all)
     uint32_t tr_skip;             // workload events skipped so far: the replica's id of a later

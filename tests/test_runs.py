@@ -158,17 +158,30 @@ def test_bursty_stepping_matches_oracle(backend):
             assert parity.compare(od, eng, r=r) == [], (t, r)
 
 
+_STATS = {}
+
+
+def _stats_lib():
+    """The host build with event-path statistics (tools/host_stats.py's build), compiled once per
+    test process (per-process file name: pytest-xdist workers build side by side)."""
+    if "lib" not in _STATS:
+        tag = os.getpid()
+        out = os.path.join(REPO, "build", f"libk10s_hoststats_runs_{tag}.so")
+        defs = os.path.join(REPO, "build", f"hoststats_runs_defs_{tag}.cpp")
+        with open(defs, "w") as f:
+            f.write('#include <cstdint>\nextern "C" uint64_t k10s_host_stats[48];\nuint64_t k10s_host_stats[48];\n')
+        hc = os.path.join(REPO, "tests", "hostcheck")
+        subprocess.check_call(["g++", "-O1", "-std=c++17", "-fPIC", "-ffp-contract=off", "-DK10S_HOST_STATS", "-shared",
+                               "-o", out, os.path.join(hc, "hostcheck.cpp"),
+                               os.path.join(REPO, "kubernetriks_amd", "csrc", "k10s_builder.cpp"), defs])
+        os.unlink(defs)
+        _STATS["lib"] = out
+    return _STATS["lib"]
+
+
 def test_runs_cover_the_bursts():
-    """The host build with event-path statistics (tools/host_stats.py's build): on a bursty scenario
-    most events go through runs."""
-    out = os.path.join(REPO, "build", "libk10s_hoststats_runs.so")
-    defs = os.path.join(REPO, "build", "hoststats_runs_defs.cpp")
-    with open(defs, "w") as f:
-        f.write('#include <cstdint>\nextern "C" uint64_t k10s_host_stats[48];\nuint64_t k10s_host_stats[48];\n')
-    hc = os.path.join(REPO, "tests", "hostcheck")
-    subprocess.check_call(["g++", "-O1", "-std=c++17", "-fPIC", "-ffp-contract=off", "-DK10S_HOST_STATS", "-shared",
-                           "-o", out, os.path.join(hc, "hostcheck.cpp"),
-                           os.path.join(REPO, "kubernetriks_amd", "csrc", "k10s_builder.cpp"), defs])
+    """On a bursty scenario most events go through runs (host build with event statistics)."""
+    out = _stats_lib()
     L = ctypes.CDLL(out)
     import hostcheck_bridge as hb
     saved = (hb.LIB_PATH, hb._lib, hb.build)
@@ -180,6 +193,104 @@ def test_runs_cover_the_bursts():
         eng.run_until_all_finished(max_time=1e7)
         st = (ctypes.c_uint64 * 48).in_dll(L, "k10s_host_stats")
         events, runs, run_events = int(st[0]), int(st[38]), int(st[39])
+        for i in range(48):
+            st[i] = 0
     finally:
         hb.LIB_PATH, hb._lib, hb.build = saved
     assert runs > 100 and run_events > 0.2 * events, (events, runs, run_events)
+
+
+# ---- windows of the assignment pipeline (k10s_engine.h win_batch) -----------------------------------
+def pipeline_scenario(seed: int, n_pods: int = 300) -> str:
+    """Cycles that place many pods at once on few nodes: the six pipeline kinds interleave, several
+    assignments per node and binds per component fall inside one window (the window must stop
+    there), with zero and equal network delays (windows of equal-time events only), pod groups (the
+    group's running count), pod removals (the api server's removal set), node removals while
+    assignments are in flight (binds on removed nodes panic in the reference), tiny rings."""
+    rng = random.Random(seed)
+    cfg = test_simulation_config()
+    cfg.scheduling_cycle_interval = rng.choice([5.0, 10.0, 30.0])
+    d = rng.choice([0.0, 0.001, 0.05, 0.15])
+    cfg.as_to_ps_network_delay = d if rng.random() < 0.5 else rng.choice([0.0, 0.02, 0.05])
+    cfg.as_to_node_network_delay = d if rng.random() < 0.5 else rng.choice([0.0, 0.03, 0.15])
+    cfg.sched_to_as_network_delay = rng.choice([0.0, 0.02])
+    cfg.ps_to_sched_network_delay = rng.choice([0.0, 0.01, 0.089])
+    cfg.enable_unscheduled_pods_conditional_move = rng.random() < 0.3
+    cluster = GenericClusterTrace()
+    n_nodes = rng.randint(1, 6)
+    for i in range(n_nodes):
+        cluster.create_node(0.0, Node(f"node_{i}", 64000, 256 << 30))
+    if rng.random() < 0.5:   # a node removed (and maybe re-created) while pods are being bound to it
+        t = float(rng.choice([10, 20, 30, 60])) + rng.choice([0.0, 0.02, 0.05, 0.1])
+        cluster.remove_node(t, "node_0")
+        if rng.random() < 0.5:
+            cluster.create_node(t + 7.0, Node("node_0", 64000, 256 << 30))
+    workload = GenericWorkloadTrace()
+    names = []
+    for i in range(n_pods):
+        t = float(rng.randint(0, 120))
+        name = f"pod_{i:04d}"
+        workload.create_pod(t, Pod(name, rng.choice([100, 500, 1000]), rng.choice([1 << 28, 1 << 30]),
+                                   float(rng.randint(0, 200)) if rng.random() < 0.9 else None))
+        names.append(name)
+    for name in names:
+        if rng.random() < 0.04:
+            workload.remove_pod(float(rng.randint(0, 150)) + rng.choice([0.0, 0.02, 0.05]), name)
+    if rng.random() < 0.4:
+        cfg.hpa_enabled = True
+        cfg.hpa_scan_interval = 30.0
+        g = PodGroup("group_0", rng.randint(3, 10), 30, Pod("group_0", 100, 100 << 20, None), 0.6, None,
+                     UsageModel("pod_group", units=[(100.0, 8.0), (50.0, 1.0)]), None)
+        workload.events.append(WorkloadEvent(float(rng.randint(0, 60)), "create_pod_group", pod_group=g))
+    return scenario_text(cfg, cluster, workload)
+
+
+PIPE_SEEDS = list(range(30))
+
+
+def _pipe(backend, seed, fifo=0, gauges=0):
+    scn = pipeline_scenario(seed)
+    mode = _mode(scn)
+    o = ob.OracleSim(scn, log=True, gauges=gauges or parity.GAUGE_ROWS)
+    st = o.run_until_all_finished(20000.0) if mode == RUN_UNTIL_ALL_FINISHED else o.step_until_time(1000.0)
+    od = o.result(placements=True, log=True)
+    od["status_name"] = parity.ORACLE_STATUS[st] if not od["panicked"] else "error"
+    caps = parity.parity_caps(True, fifo=fifo, gauges=gauges or parity.GAUGE_ROWS)
+    eng = engine_cls(backend)(scn, 1, caps=caps)
+    if mode == RUN_UNTIL_ALL_FINISHED:
+        eng.run_until_all_finished(20000.0)
+    else:
+        eng.step_until_time(1000.0)
+    assert parity.compare(od, eng) == [], (seed, fifo)
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+@pytest.mark.parametrize("seed", PIPE_SEEDS)
+def test_pipeline_windows_match_oracle(backend, seed):
+    _pipe(backend, seed)
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+@pytest.mark.parametrize("seed,fifo", [(s, f) for s in (0, 3, 8) for f in (2, 4, 16)])
+def test_pipeline_windows_small_rings(backend, seed, fifo):
+    _pipe(backend, seed, fifo=fifo)
+
+
+def test_windows_cover_the_pipeline():
+    """On the C3 shape the six pipeline kinds go through windows (host build with event statistics)."""
+    out = _stats_lib()
+    L = ctypes.CDLL(out)
+    import hostcheck_bridge as hb
+    saved = (hb.LIB_PATH, hb._lib, hb.build)
+    try:
+        hb.LIB_PATH, hb._lib, hb.build = out, None, (lambda: None)
+        from kubernetriks_amd import workloads as wl
+        st = (ctypes.c_uint64 * 48).in_dll(L, "k10s_host_stats")
+        before = [int(st[i]) for i in (0, 41, 42)]
+        cluster, workload = wl.c3_traces(n_nodes=256, n_pods=1024, arrival_window=100.0, seed=4)
+        eng = hb.HostEngine(scenario_text(SimulationConfig(), cluster, workload), 1)
+        eng.run_until_all_finished(max_time=1e7)
+        events, wins, win_events = (int(st[i]) - b for i, b in zip((0, 41, 42), before))
+    finally:
+        hb.LIB_PATH, hb._lib, hb.build = saved
+    assert wins > 20 and win_events > 0.25 * events, (events, wins, win_events)
