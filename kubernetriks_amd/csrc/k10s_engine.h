@@ -535,7 +535,7 @@ extern "C" uint64_t k10s_host_stats[48];
 enum { HS_EVENTS, HS_FIFO_POP, HS_REFILL, HS_HEAP_POP, HS_TRACE_POP, HS_SL_FAST, HS_SL_UPDATE, HS_EMIT_WIN,
        HS_EMIT_RING, HS_EMIT_HEAP, HS_SL_DIRTY, HS_SCANS, HS_REFILL_CLS0 = 12, HS_POP_CLS0 = 20, HS_AQ_HBM_GET = 28, HS_AQ_POP = 29, HS_SLPOS0 = 32,
        HS_NEXT_EMITTED = 36, HS_NEXT_EMITTED_FIFO = 37, HS_RUNS = 38, HS_RUN_EVENTS = 39, HS_RUN_REFUSED = 40,
-       HS_WINDOWS = 41, HS_WIN_EVENTS = 42, HS_TILE_PICKS = 43, HS_TILE_RESCANS = 44 };
+       HS_WINDOWS = 41, HS_WIN_EVENTS = 42, HS_TILE_PICKS = 43, HS_TILE_RESCANS = 44, HS_FUSED_FINISH = 45 };
 // An emission changed source q's head: mark it for the source list.
 K10S_HD void sl_mark(RepHdr& H, uint32_t q) { H.sl_dirty |= 1u << q; }
 K10S_HD void pods_left_dec(RepHdr& H) { H.pods_left -= 1; }
@@ -1890,7 +1890,7 @@ K10S_HD uint32_t fit_tile(const uint64_t* s_node, uint32_t n_nodes, const uint32
 // lanes together.  The maximum of the lane values is the pick, and no lane value means no node fits
 // (NoSufficientResources).  A pod that fits no node of the snapshot fits none now (fit_tile above).
 // The pass costs one read of the cache per tile; a placement otherwise costs a full read of its own.
-// Measured and not kept (default 0, profiles/r05_ab5_tile_best.json): on the backlog line it cuts
+// Measured and not kept (default 0, profiles/r05_ab5_windows_tile_best.json): on the backlog line it cuts
 // the entries read per placement from 6,511 to 4,467 but takes 3,780 ms per launch instead of 2,290
 // (the pass's per-pod lane state spills at 64 VGPRs, 74 % of the picks need a rescan, and the
 // cycle's bookkeeping, not its reads, dominates that regime); C3 never runs tiles but lost 2.7 % to
@@ -3091,6 +3091,84 @@ K10S_HD void pend_rm_clear(Ctx& c, uint32_t uid) {
     }
 }
 
+// ---- the finish relay handled with the finish (round 5) -------------------------------------------
+// A node component's PodFinishedRunning self-event at time T emits the api server's
+// PodFinishedRunning with emit_now (node_component.rs:227-245): the relay gets time T and the next id,
+// so it is the very next event exactly when no other pending event has a time <= T (one at T has a
+// smaller id and goes first; no later-emitted event can precede it).  Then the finish handler handles
+// the relay itself (api_server.rs:247-276: counters, pods left, a PS_POD_FINISHED after as_to_ps)
+// with the id the relay would have had, logged and counted as an event, instead of a round through
+// the FIFO of delay 0 and the event loop.  Pending events: the other sources' heads (the source
+// list's second entry is the smallest) and the heap below its root, which is the finish itself (the
+// root's children hold the heap's second-smallest entry: one LDS read of the top level, a canceled
+// finish counting like a live one).  Not fused: a budgeted launch (the loop may stop between the
+// two), a launch the termination rule would end before the relay (pods_left <= 0 at a multiple of
+// 1,000 s), an id overflow.
+#ifndef K10S_FUSE_FINISH
+#define K10S_FUSE_FINISH 1
+#endif
+// api_server.rs:247-276 (PodFinishedRunning): the serial handler and the fused relay
+K10S_HD void as_pod_finished(Ctx& c, uint32_t a, uint32_t b, double x) {
+    RepHdr* h = &c.H();
+    h->counters[K10S_C_TERMINATED_PODS] += 1;
+    pods_left_dec(*h);
+    h->counters[K10S_C_PODS_SUCCEEDED] += 1;
+    h->g_cur_pods -= 1;  // api_server.rs:262-265
+    emit(c, K10S_EV_PS_POD_FINISHED, c.P().as_to_ps_network_delay, -1, a, b, x, FQ_AS_TO_PS);
+}
+// Is the relay of a finish at time T (the heap root) the next event?
+K10S_HD bool finish_relay_next(Ctx& c, double T) {
+    if (!K10S_FUSE_FINISH) return false;
+    RepHdr& H = c.H();
+    const uint32_t fl = uniform_u32(H.run_flags);
+    if (!(fl & 1u)) return false;
+    if (!(fl & 2u) && (int64_t)uniform_u64((uint64_t)H.pods_left) <= 0 && is_multiple_of_1000(T)) return false;
+    if (uniform_u32(H.next_seq) >= 0xFFFFFFFEu) return false;
+    if (uniform_u32(H.sl[0].src) != (uint32_t)SRC_HEAP) return false;
+    const int64_t kT = total_key(T);
+    if (uniform_u32(H.sl_n) > 1 && (int64_t)uniform_u64((uint64_t)H.sl[1].key) <= kT) return false;
+    const uint32_t n = uniform_u32(H.heap_size);
+    static_assert(K10S_HEAP_TOP >= 1 + K10S_HEAP_D, "the root's children are in the LDS top level");
+#if K10S_DEVICE
+    const uint32_t i = 1u + (uint32_t)lane_id();
+    const bool early = i < n && i <= (uint32_t)K10S_HEAP_D && total_key(H.heap_lds[i < K10S_HEAP_TOP ? i : 0].time) <= kT;
+    return __ballot(early) == 0;
+#else
+    for (uint32_t i = 1; i < n && i <= (uint32_t)K10S_HEAP_D; i++)
+        if (total_key(H.heap_lds[i].time) <= kT) return false;
+    return true;
+#endif
+}
+// The fused relay: the id, the log entry and the event count the loop would give it, then its handler.
+K10S_HD void as_pod_finished_fused(Ctx& c, uint32_t a, uint32_t b, double x, double T) {
+    RepHdr& H = c.H();
+    const uint32_t seq = uniform_u32(H.next_seq);
+    H.next_seq = seq + 1u;
+    const uint32_t cap_log = c.Ly().cap_log;
+    if (cap_log) {
+        const uint32_t k = uniform_u32(H.log_n);
+        if (k < cap_log) {
+            k10s_log_entry le;
+            le.time = T;
+            le.seq = seq;
+            le.kind = (uint16_t)K10S_EV_AS_POD_FINISHED;
+            le.slot = -1;
+            le.pod = (int32_t)a;
+            le.node = (int32_t)b;
+            c.V().log()[k] = le;
+            H.log_n = k + 1u;
+        } else {
+            H.flags |= 1u;
+        }
+    }
+    H.counters[K10S_C_EVENTS] += 1;
+#if K10S_PROF
+    H.prof[K10S_PROF_KIND0 + K10S_EV_NUM_KINDS + K10S_EV_AS_POD_FINISHED] += 1;
+#endif
+    K10S_HSTAT(HS_FUSED_FINISH);
+    as_pod_finished(c, a, b, x);
+}
+
 // ---- api server (api_server.rs:127-457) --------------------------------------------------------
 K10S_WARM void on_api_server(Ctx& c, K10S_EVARG) {
     K10S_EV_PROLOGUE;
@@ -3165,11 +3243,7 @@ K10S_WARM void on_api_server(Ctx& c, K10S_EVARG) {
         emit(c, K10S_EV_PS_POD_STARTED, pr->as_to_ps_network_delay, -1, e.a, 0, e.x, FQ_AS_TO_PS);
         break;
     case K10S_EV_AS_POD_FINISHED:
-        h->counters[K10S_C_TERMINATED_PODS] += 1;
-        pods_left_dec(*h);
-        h->counters[K10S_C_PODS_SUCCEEDED] += 1;
-        h->g_cur_pods -= 1;  // api_server.rs:262-265
-        emit(c, K10S_EV_PS_POD_FINISHED, pr->as_to_ps_network_delay, -1, e.a, e.b, e.x, FQ_AS_TO_PS);
+        as_pod_finished(c, e.a, e.b, e.x);
         break;
     case K10S_EV_AS_REMOVE_NODE_REQ:
         pend_rm_set(c, sc->node_uid[e.a]);
@@ -3322,7 +3396,8 @@ K10S_WARM void on_node(Ctx& c, K10S_EVARG) {
             return;
         }
         run_remove_at(c, p, slot, fs, srun, g);
-        emit(c, K10S_EV_AS_POD_FINISHED, 0.0, -1, p, e.b, e.x, FQ_NOW);  // emit_now
+        if (finish_relay_next(c, e.time)) as_pod_finished_fused(c, p, e.b, e.x, e.time);
+        else emit(c, K10S_EV_AS_POD_FINISHED, 0.0, -1, p, e.b, e.x, FQ_NOW);  // emit_now
         break;
     }
     case K10S_EV_N_REMOVE_NODE: {

@@ -54,7 +54,7 @@ def main():
                       "sl_insert_pos_0_1_2_3plus": [int(st[32 + i]) for i in range(4)],
                       "runs": int(st[38]), "run_events": int(st[39]), "runs_refused": int(st[40]),
                       "windows": int(st[41]), "window_events": int(st[42]),
-                      "tile_picks": int(st[43]), "tile_picks_with_rescan": int(st[44]),
+                      "tile_picks": int(st[43]), "tile_picks_with_rescan": int(st[44]), "fused_finish_relays": int(st[45]),
                       "next_event_emitted_by_previous": round(int(st[36]) / ev, 4),
                       "next_event_emitted_by_previous_fifo": round(int(st[37]) / ev, 4)}, indent=1))
 
