@@ -532,6 +532,16 @@ extern "C" uint64_t k10s_host_stats[48];
 #else
 #define K10S_HSTAT(i) ((void)0)
 #endif
+// Host-only memory-touch model (tooling: tools/traffic_model.py builds the host engine with
+// -DK10S_TRAFFIC_MODEL and compiler load/store tracing; the runtime attributes every touched line of
+// the replica's HBM sections to the kind of the event the loop is handling); compiled out elsewhere.
+#if !K10S_DEVICE && defined(K10S_TRAFFIC_MODEL)
+extern "C" void k10s_tm_replica(const void* base, const void* layout);
+extern "C" void k10s_tm_event(uint32_t kind);
+#define K10S_TM_EVENT(k) k10s_tm_event(k)
+#else
+#define K10S_TM_EVENT(k) ((void)0)
+#endif
 enum { HS_EVENTS, HS_FIFO_POP, HS_REFILL, HS_HEAP_POP, HS_TRACE_POP, HS_SL_FAST, HS_SL_UPDATE, HS_EMIT_WIN,
        HS_EMIT_RING, HS_EMIT_HEAP, HS_SL_DIRTY, HS_SCANS, HS_REFILL_CLS0 = 12, HS_POP_CLS0 = 20, HS_AQ_HBM_GET = 28, HS_AQ_POP = 29, HS_SLPOS0 = 32,
        HS_NEXT_EMITTED = 36, HS_NEXT_EMITTED_FIFO = 37, HS_RUNS = 38, HS_RUN_EVENTS = 39, HS_RUN_REFUSED = 40,
@@ -2406,6 +2416,40 @@ K10S_HD void run_scheduling_cycle(Ctx& c, double t) {
 // 4.6 % at C3, profiles/r02_v4_score_plugins_ab.json).
 K10S_HD void run_scheduling_cycle_plugins(Ctx& c, double t) { run_scheduling_cycle_t<true>(c, t); }
 
+// AddNodeToCache (scheduler.rs:391-405)
+K10S_HD void s_add_node(Ctx& c, const HeapEv& e) {
+    RepHdr* h = &c.H();
+    uint32_t n = e.a;
+    uint32_t ac = e.b;
+    uint64_t ar = f2u(e.x);
+    const NcEnt cap = {ac, ar};
+    nc_put(c, n, cap);
+    // the stored node's capacity: a node reaches the scheduler straight from its creation,
+    // allocatable = capacity (node.rs:60-66); only MostAllocated reads it (wide layout)
+    if (!nc_packed(c)) {
+        c.V().s_ccpu()[n] = ac;
+        c.V().s_cram()[n] = ar;
+    }
+    if (!bit_test(c.V().s_present(), n)) {
+        bit_set(c.V().s_present(), n);
+        h->s_node_count += 1;
+    }
+    node_bound_changed(c, n);
+    if (c.P().enable_unscheduled_pods_conditional_move) s_move(c, 3, 0.0, ac, ar);
+    else s_move(c, 0, 0.0, 0, 0);
+}
+// PodScheduleRequest (scheduler.rs:411-420)
+K10S_HD void s_pod_schedule_req(Ctx& c, const HeapEv& e) {
+    uint32_t p = e.a;
+    c.V().pod(p).sflag = PF_IN_S;   // a store: no read of the pod line on this event
+    c.V().pod(p).s_assigned = -1;
+    QInfo q;
+    q.timestamp = e.time;
+    q.initial = e.time;
+    q.attempts = 1;
+    q.pod = p;
+    aq_push(c, q);
+}
 K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
     RepHdr* h = &c.H();
     switch (e.kind) {
@@ -2420,39 +2464,12 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
         s_move(c, 1, e.time, 0, 0);
         emit0(c, K10S_EV_S_FLUSH, 30.0);  // POD_FLUSH_INTERVAL (queue.rs:11)
         break;
-    case K10S_EV_S_ADD_NODE: {
-        uint32_t n = e.a;
-        uint32_t ac = e.b;
-        uint64_t ar = f2u(e.x);
-        const NcEnt cap = {ac, ar};
-        nc_put(c, n, cap);
-        // the stored node's capacity: a node reaches the scheduler straight from its creation,
-        // allocatable = capacity (node.rs:60-66); only MostAllocated reads it (wide layout)
-        if (!nc_packed(c)) {
-            c.V().s_ccpu()[n] = ac;
-            c.V().s_cram()[n] = ar;
-        }
-        if (!bit_test(c.V().s_present(), n)) {
-            bit_set(c.V().s_present(), n);
-            h->s_node_count += 1;
-        }
-        node_bound_changed(c, n);
-        if (c.P().enable_unscheduled_pods_conditional_move) s_move(c, 3, 0.0, ac, ar);
-        else s_move(c, 0, 0.0, 0, 0);
+    case K10S_EV_S_ADD_NODE:
+        s_add_node(c, e);
         break;
-    }
-    case K10S_EV_S_POD_SCHEDULE_REQ: {
-        uint32_t p = e.a;
-        c.V().pod(p).sflag = PF_IN_S;   // a store: no read of the pod line on this event
-        c.V().pod(p).s_assigned = -1;
-        QInfo q;
-        q.timestamp = e.time;
-        q.initial = e.time;
-        q.attempts = 1;
-        q.pod = p;
-        aq_push(c, q);
+    case K10S_EV_S_POD_SCHEDULE_REQ:
+        s_pod_schedule_req(c, e);
         break;
-    }
     case K10S_EV_S_POD_FINISHED: {
         uint32_t p = e.a, n = e.b;
         // one batch of loads: the pod's fields, the event node's flags, and the scheduler-cache entry
@@ -3678,12 +3695,18 @@ K10S_COLD void on_metrics(Ctx& c, K10S_EVARG) {
                         (1ull << K10S_EV_AS_ASSIGN_RESP) | (1ull << K10S_EV_N_BIND) |                       \
                         (1ull << K10S_EV_AS_POD_STARTED) | (1ull << K10S_EV_PS_POD_STARTED))
 #define K10S_BATCH_KINDS (K10S_RUN_KINDS | (K10S_WINDOWS ? K10S_WIN_KINDS : 0ull))
-// the scheduler's handler out of line, for on_run_kind's fallback (the event loop inlines it)
-K10S_WARM void on_scheduler_ool(Ctx& c, EvRef ep) {
+// The scheduler's run kinds for on_run_kind's fallback: not on_scheduler itself, whose scheduling
+// cycle (64 VGPRs) would make every call of on_run_kind clobber the event loop's live VGPRs (six
+// 64-bit values spilled to scratch and reloaded around each call).
+K10S_HD void on_scheduler_run_kind(Ctx& c, EvRef ep, uint32_t k) {
     HeapEv e = *ep;
     uniform_event(e);
-    on_scheduler(c, e);
+    if (k == K10S_EV_S_ADD_NODE) s_add_node(c, e);
+    else s_pod_schedule_req(c, e);
 }
+static_assert((K10S_BATCH_KINDS & (((1ull << (K10S_EV_S_REMOVE_POD + 1)) - 1ull) & ~((1ull << K10S_EV_S_RUN_CYCLE) - 1ull))) ==
+                  ((1ull << K10S_EV_S_POD_SCHEDULE_REQ) | (1ull << K10S_EV_S_ADD_NODE)),
+              "on_scheduler_run_kind handles every scheduler kind a batch entry can fall back to");
 K10S_WARM void on_run_kind(Ctx& c, EvRef ep, uint32_t k) {
     k = uniform_u32(k);
     if ((K10S_RUN_KINDS >> k) & 1ull) {
@@ -3696,7 +3719,7 @@ K10S_WARM void on_run_kind(Ctx& c, EvRef ep, uint32_t k) {
     } else if (k <= K10S_EV_PS_POD_REMOVED) {
         on_ps(c, ep);
     } else if (k <= K10S_EV_S_REMOVE_POD) {
-        on_scheduler_ool(c, ep);
+        on_scheduler_run_kind(c, ep, k);   // (S_POD_SCHEDULE_REQ, S_ADD_NODE: the only scheduler run kinds)
     } else {
         on_node(c, ep);
     }
@@ -5240,6 +5263,9 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
     const uint64_t t_loop = prof_now();
     sl_rebuild(c, ntr);  // the sorted source list, from the sources' heads
     h->run_flags = (budget == 0 ? 1u : 0u) | (until_mode0 ? 2u : 0u);   // run_batch, win_batch
+#if !K10S_DEVICE && defined(K10S_TRAFFIC_MODEL)
+    k10s_tm_replica(c.V().b, &c.Ly());
+#endif
     h->run_limit = limit;
     [[maybe_unused]] uint32_t it_stale = 0;
 #if !K10S_DEVICE && defined(K10S_HOST_STATS)
@@ -5383,6 +5409,7 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
         }
 #endif
         const uint64_t t_dis = prof_now();
+        K10S_TM_EVENT(e.kind);
         dispatch(c, ep, e.kind);
         {   // the event stayed at the head of its source during the handler (an emission lands after
             // it: larger id, time >= clock); remove it now
@@ -5402,6 +5429,7 @@ K10S_HD int run_replica(Ctx& c, int mode, double until_time, double max_time, ui
         }
     }
     K10S_PROF_ADD(c, PROF_LOOP, t_loop);
+    K10S_TM_EVENT(0xFFFFu);
 #if K10S_DEVICE && K10S_BEACON
     if (lane_id() == 0)   // word 12: the loop has exited (1 + launch-local event count)
         __hip_atomic_store(k10s_beacon + (uint64_t)blockIdx.x * K10S_BEACON_WORDS + 12, (uint32_t)done + 1u,
