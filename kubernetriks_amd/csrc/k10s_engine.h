@@ -3691,9 +3691,14 @@ K10S_COLD void on_metrics(Ctx& c, K10S_EVARG) {
 #ifndef K10S_WINDOWS
 #define K10S_WINDOWS 1
 #endif
+#ifndef K10S_WIN_NOTSCHED
+#define K10S_WIN_NOTSCHED 1   // the failed attempts' relays in windows (A/B knob)
+#endif
 #define K10S_WIN_KINDS ((1ull << K10S_EV_AS_ASSIGN_REQ) | (1ull << K10S_EV_PS_ASSIGN_REQ) |                 \
                         (1ull << K10S_EV_AS_ASSIGN_RESP) | (1ull << K10S_EV_N_BIND) |                       \
-                        (1ull << K10S_EV_AS_POD_STARTED) | (1ull << K10S_EV_PS_POD_STARTED))
+                        (1ull << K10S_EV_AS_POD_STARTED) | (1ull << K10S_EV_PS_POD_STARTED) |               \
+                        (K10S_WIN_NOTSCHED ? (1ull << K10S_EV_AS_POD_NOT_SCHEDULED) |                        \
+                                                 (1ull << K10S_EV_PS_POD_NOT_SCHEDULED) : 0ull))
 #define K10S_BATCH_KINDS (K10S_RUN_KINDS | (K10S_WINDOWS ? K10S_WIN_KINDS : 0ull))
 // The scheduler's run kinds for on_run_kind's fallback: not on_scheduler itself, whose scheduling
 // cycle (64 VGPRs) would make every call of on_run_kind clobber the event loop's live VGPRs (six
@@ -4645,7 +4650,10 @@ pushed:
 // dslab order the six kinds interleave event by event: no two consecutive events share a kind (no run),
 // yet within any as_to_ps-long stretch (50 ms at C3) they are independent.  A window is such a stretch:
 // the next W events in dslab order, taken from the delay-class rings (their first 16 entries each, the
-// first four rings of the source list), handled as W lanes at once.
+// first four rings of the source list), handled as W lanes at once.  The backlog regime adds a second
+// pipeline of the same shape: a cycle's failed attempts are 4.1 ms apart (the per-node scheduling
+// time) and each relays AS_POD_NOT_SCHEDULED -> PS_POD_NOT_SCHEDULED (+as_to_ps, no emission after
+// that), so those two kinds are window kinds as well.
 //
 // Why it is exact.  (1) The window is a prefix of dslab's order: the rings' candidates are merged by
 // (time, id) (ranks by binary search), and the window stops before the first event that is not a
@@ -4656,8 +4664,8 @@ pushed:
 // emission at an equal time has a larger id.  (3) The handlers commute inside a window: each writes
 // only its own pod's line (two events of one pod never share a window), storage's copy of its node
 // (PS_ASSIGN_REQ: two assignments to one node never share a window), its node component's slot
-// (N_BIND: likewise per slot), commutative header counters and the group's running count (an atomic
-// add), and it reads nothing the others write.  Emissions get the ids a serial run would hand out
+// (N_BIND: likewise per slot), commutative header counters (storage's unscheduled count as a sum of
+// +1 / -1) and the group's running count (an atomic add), and it reads nothing the others write.  Emissions get the ids a serial run would hand out
 // (next_seq plus the emission counts of the earlier window events, N_BIND's finish before its start)
 // and are appended to their rings in that order (one delay per ring: times stay sorted); the finishes
 // go into the event heap one by one.  Every reference panic of these handlers, a full ring or heap,
@@ -4729,10 +4737,12 @@ K10S_HD WinSt win_load(Ctx& c, const WinEv& e) {
         s.emits = (s.sflags & POD_HAS_DUR) ? 2u : 1u;
         break;
     }
-    case K10S_EV_AS_POD_STARTED:   // api_server.rs:233-245
+    case K10S_EV_AS_POD_STARTED:         // api_server.rs:233-245
+    case K10S_EV_AS_POD_NOT_SCHEDULED:   // api_server.rs:219-231
         s.emits = 1;
         break;
-    default:   // K10S_EV_PS_POD_STARTED (persistent_storage.rs:309-314): no emission
+    default:   // K10S_EV_PS_POD_STARTED (persistent_storage.rs:309-314), K10S_EV_PS_POD_NOT_SCHEDULED
+               // (296-307): no emission
         s.pf = c.V().pod(e.a).flags;
         break;
     }
@@ -4745,6 +4755,7 @@ K10S_HD bool win_bad(Ctx& c, const WinEv& e, const WinSt& s) {
     case K10S_EV_AS_ASSIGN_RESP: return s.as_slot < 0;
     case K10S_EV_N_BIND: return s.removed != 0 || s.snode != (int32_t)e.b || s.prs >= 0;
     case K10S_EV_PS_POD_STARTED: return (!K10S_TIME_KEY_ID || c.H().ps_rm_n != 0) && !(s.pf & PF_IN_PS);
+    case K10S_EV_PS_POD_NOT_SCHEDULED: return !(s.pf & PF_IN_PS);
     default: return false;
     }
 }
@@ -4783,9 +4794,18 @@ K10S_HD void win_apply(Ctx& c, const WinEv& e, const WinSt& s, uint32_t fseq) {
     case K10S_EV_PS_POD_STARTED:
         if (c.V().prec()) c.V().prec()[e.a].t_running = e.x;
         break;
+    case K10S_EV_PS_POD_NOT_SCHEDULED:   // (the unscheduled count is summed by the caller)
+        if (!(s.pf & PF_UNSCHED)) c.V().pod(e.a).flags = (uint8_t)(s.pf | PF_UNSCHED);
+        break;
     default:
         break;
     }
+}
+// The window event's change of storage's unscheduled-pod count.
+K10S_HD int32_t win_unsched_delta(const WinEv& e, const WinSt& s) {
+    if (e.kind == K10S_EV_PS_ASSIGN_REQ) return (s.pf & PF_UNSCHED) ? -1 : 0;
+    if (e.kind == K10S_EV_PS_POD_NOT_SCHEDULED) return (s.pf & PF_UNSCHED) ? 0 : 1;
+    return 0;
 }
 // The ring emission of a window event (AS_TO_PS or AS_TO_NODE class), id seq.
 K10S_HD HeapEv win_ring_emission(const Params& pr, const WinEv& e, uint32_t seq) {
@@ -4807,6 +4827,9 @@ K10S_HD HeapEv win_ring_emission(const Params& pr, const WinEv& e, uint32_t seq)
         break;
     case K10S_EV_N_BIND:
         o.kind = K10S_EV_AS_POD_STARTED, o.time = e.time + pr.as_to_node_network_delay, o.x = e.time;
+        break;
+    case K10S_EV_AS_POD_NOT_SCHEDULED:
+        o.kind = K10S_EV_PS_POD_NOT_SCHEDULED, o.time = e.time + pr.as_to_ps_network_delay, o.x = e.x;
         break;
     default:   // K10S_EV_AS_POD_STARTED
         o.kind = K10S_EV_PS_POD_STARTED, o.time = e.time + pr.as_to_ps_network_delay, o.x = e.x;
@@ -4978,7 +5001,7 @@ K10S_HD_NOINL uint32_t win_batch(Ctx& c) {
     // two events of one pod, two assignments to one node, two binds on one component: only the first
     {
         const uint32_t writer = wk && (ev.kind == K10S_EV_PS_ASSIGN_REQ || ev.kind == K10S_EV_N_BIND ||
-                                       ev.kind == K10S_EV_PS_POD_STARTED) ? 1u : 0u;
+                                       ev.kind == K10S_EV_PS_POD_STARTED || ev.kind == K10S_EV_PS_POD_NOT_SCHEDULED) ? 1u : 0u;
         uint64_t wm = __ballot(writer != 0u) & (V >= 64u ? ~0ull : ((1ull << V) - 1ull));
         while (wm) {
             const uint32_t b = (uint32_t)__builtin_ctzll(wm);
@@ -5057,7 +5080,8 @@ K10S_HD_NOINL uint32_t win_batch(Ctx& c) {
         bool conf = false;
         for (uint32_t b = 0; b < W; b++) {
             const WinEv& o = evs[b];
-            const bool writer = o.kind == K10S_EV_PS_ASSIGN_REQ || o.kind == K10S_EV_N_BIND || o.kind == K10S_EV_PS_POD_STARTED;
+            const bool writer = o.kind == K10S_EV_PS_ASSIGN_REQ || o.kind == K10S_EV_N_BIND || o.kind == K10S_EV_PS_POD_STARTED ||
+                                o.kind == K10S_EV_PS_POD_NOT_SCHEDULED;
             conf |= writer && (e.a == o.a || (e.kind == o.kind && ((o.kind == K10S_EV_PS_ASSIGN_REQ && e.b == o.b) ||
                                                                      (o.kind == K10S_EV_N_BIND && e.slot == o.slot))));
         }
@@ -5107,7 +5131,7 @@ K10S_HD_NOINL uint32_t win_batch(Ctx& c) {
         const uint32_t fseq = e_heap ? id0 : 0u;   // N_BIND: its finish first (id0), then its start
         if (in) {
             win_apply(c, ev, st, fseq);
-            if (ev.kind == K10S_EV_PS_ASSIGN_REQ && (st.pf & PF_UNSCHED)) unsched = 1;
+            unsched = (uint32_t)win_unsched_delta(ev, st);
             if (cap_log && r > 0 && log0 + r < cap_log) {
                 k10s_log_entry le;
                 le.time = ev.time;
@@ -5115,7 +5139,8 @@ K10S_HD_NOINL uint32_t win_batch(Ctx& c) {
                 le.kind = (uint16_t)ev.kind;
                 le.slot = (int16_t)(ev.kind == K10S_EV_N_BIND ? ev.slot : -1);
                 le.pod = (int32_t)ev.a;
-                le.node = (ev.kind == K10S_EV_AS_POD_STARTED || ev.kind == K10S_EV_PS_POD_STARTED) ? -1 : (int32_t)ev.b;
+                le.node = (ev.kind == K10S_EV_AS_POD_STARTED || ev.kind == K10S_EV_PS_POD_STARTED ||
+                           ev.kind == K10S_EV_AS_POD_NOT_SCHEDULED || ev.kind == K10S_EV_PS_POD_NOT_SCHEDULED) ? -1 : (int32_t)ev.b;
                 c.V().log()[log0 + r] = le;
             }
         }
@@ -5157,7 +5182,7 @@ K10S_HD_NOINL uint32_t win_batch(Ctx& c) {
             const WinSt& s = sts[r];
             const bool hp = e.kind == K10S_EV_N_BIND && (s.sflags & POD_HAS_DUR);
             win_apply(c, e, s, hp ? id : 0u);
-            if (e.kind == K10S_EV_PS_ASSIGN_REQ && (s.pf & PF_UNSCHED)) unsched++;
+            unsched += (uint32_t)win_unsched_delta(e, s);
             if (cap_log && r > 0 && log0 + r < cap_log) {
                 k10s_log_entry le;
                 le.time = e.time;
@@ -5165,7 +5190,8 @@ K10S_HD_NOINL uint32_t win_batch(Ctx& c) {
                 le.kind = (uint16_t)e.kind;
                 le.slot = (int16_t)(e.kind == K10S_EV_N_BIND ? e.slot : -1);
                 le.pod = (int32_t)e.a;
-                le.node = (e.kind == K10S_EV_AS_POD_STARTED || e.kind == K10S_EV_PS_POD_STARTED) ? -1 : (int32_t)e.b;
+                le.node = (e.kind == K10S_EV_AS_POD_STARTED || e.kind == K10S_EV_PS_POD_STARTED ||
+                           e.kind == K10S_EV_AS_POD_NOT_SCHEDULED || e.kind == K10S_EV_PS_POD_NOT_SCHEDULED) ? -1 : (int32_t)e.b;
                 c.V().log()[log0 + r] = le;
             }
             if (hp) {
@@ -5205,7 +5231,7 @@ K10S_HD_NOINL uint32_t win_batch(Ctx& c) {
             H.flags |= 1u;
         }
     }
-    H.unsched_cache_count -= unsched;
+    H.unsched_cache_count += unsched;   // (a wrapping sum of the events' +1 / -1)
     for (uint32_t z = 0; z < 2; z++) {
         const uint32_t n = z == 0 ? n_ps : n_node;
         if (!n) continue;

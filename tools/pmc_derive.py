@@ -55,12 +55,17 @@ def main():
         # memory-side read requests of the L2 that target DRAM (HBM or the Infinity Cache in front of
         # it: the MALL sits on the memory side, so the L2 counters cannot split its hits from HBM)
         der["dram_share_of_l2_read_requests"] = per.get("TCC_EA0_RDREQ_DRAM_sum", 0.0) / per["TCC_EA0_RDREQ_sum"]
-    if "FETCH_SIZE" in per:
-        der["memory_read_bytes_fetch_x2"] = 2.0 * per["FETCH_SIZE"] * 1024.0   # gfx950: FETCH_SIZE is half
-    if "WRITE_SIZE" in per:
+    if "TCC_EA0_RDREQ_128B_sum" in per:   # exact request sizes (tools/pmc_summary.py; round 5)
+        der["memory_read_bytes"] = (32.0 * per.get("TCC_EA0_RDREQ_32B_sum", 0.0) + 64.0 * per.get("TCC_EA0_RDREQ_64B_sum", 0.0)
+                                    + 128.0 * per["TCC_EA0_RDREQ_128B_sum"])
+    elif "FETCH_SIZE" in per:
+        der["memory_read_bytes"] = 2.0 * per["FETCH_SIZE"] * 1024.0   # round 4: FETCH_SIZE doubled
+    if "TCC_EA0_WRREQ_64B_sum" in per and "TCC_EA0_WRREQ_sum" in per:
+        der["memory_write_bytes"] = 64.0 * per["TCC_EA0_WRREQ_64B_sum"] + 32.0 * (per["TCC_EA0_WRREQ_sum"] - per["TCC_EA0_WRREQ_64B_sum"])
+    elif "WRITE_SIZE" in per:
         der["memory_write_bytes"] = per["WRITE_SIZE"] * 1024.0
-    if "FETCH_SIZE" in per and "WRITE_SIZE" in per and kns:
-        tot = der["memory_read_bytes_fetch_x2"] + der["memory_write_bytes"]
+    if "memory_read_bytes" in der and "memory_write_bytes" in der and kns:
+        tot = der["memory_read_bytes"] + der["memory_write_bytes"]
         der["memory_bytes_per_launch"] = tot
         der["memory_TBps"] = tot / kns / 1e3
         der["memory_frac_of_8TBps"] = tot / kns / 8e3
