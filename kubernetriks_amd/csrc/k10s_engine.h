@@ -401,7 +401,7 @@ struct EvLazy {
 // s_memtime deltas per loop phase, accumulated in RepHdr::prof and read by k10s_engine_profile.
 enum : int { PROF_LOOP = 0, PROF_SELECT = 1, PROF_CONSUME = 2, PROF_DISPATCH = 3, PROF_CYCLE = 4, PROF_SCAN = 5,
              PROF_NSCAN = 6, PROF_BOUNDS = 7, PROF_AQPOP = 8, PROF_HEAPPOP = 9, PROF_NHEAPPOP = 10, PROF_EMIT = 11,
-             PROF_NEMIT = 12, PROF_AQPUSH = 13 };
+             PROF_NEMIT = 12, PROF_AQPUSH = 13, PROF_WFRONT = 14, PROF_WAPPLY = 15 };
 K10S_HD uint64_t prof_now() {
 #if K10S_PROF && K10S_DEVICE
     // an ordered read (volatile, memory clobber): the builtin's reads could move across the code they
@@ -4871,6 +4871,7 @@ K10S_HD void heap_insert(Ctx& c, const HeapEv& e) {
 // for the source list.
 K10S_HD_NOINL uint32_t win_batch(Ctx& c) {
     RepHdr& H = c.H();
+    [[maybe_unused]] const uint64_t t_front = prof_now();
     const uint32_t fl = uniform_u32(H.run_flags);
     if (!(fl & 1u) || (!(fl & 2u) && (int64_t)uniform_u64((uint64_t)H.pods_left) <= 0)) return 0;
     if (!c.Ly().tnonneg || c.S().ca_enabled || !c.Ly().cap_fq) return 0;
@@ -5019,6 +5020,7 @@ K10S_HD_NOINL uint32_t win_batch(Ctx& c) {
         W = sm ? (uint32_t)__builtin_ctzll(sm) : 64u;
     }
     W = uniform_u32(W);
+    K10S_PROF_ADD(c, PROF_WFRONT, t_front);
     if (W < 2) return 0;
     const bool in = r < W;
     // ---- emissions: ids and ring positions in window order
@@ -5103,6 +5105,7 @@ K10S_HD_NOINL uint32_t win_batch(Ctx& c) {
     }
 #endif
     // ---- what the serial path would place differently: then no window
+    [[maybe_unused]] const uint64_t t_apply = prof_now();
     const uint32_t seq0 = uniform_u32(H.next_seq);
     if ((uint64_t)seq0 + n_total > 0xFFFFFFFFull) return 0;
     if (n_heap && uniform_u32(H.heap_size) + n_heap > c.Ly().cap_heap) return 0;
@@ -5265,6 +5268,7 @@ K10S_HD_NOINL uint32_t win_batch(Ctx& c) {
     k10s_host_stats[HS_WIN_EVENTS] += W;
     k10s_host_stats[HS_EVENTS] += W - 1;
 #endif
+    K10S_PROF_ADD(c, PROF_WAPPLY, t_apply);
     return W;
 }
 

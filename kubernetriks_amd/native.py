@@ -401,11 +401,11 @@ class Engine(EngineBase):
         self._L.k10s_engine_profile.restype = ctypes.c_int32
         self._check(self._L.k10s_engine_profile(self._h, buf))
         keys = ["loop", "select", "consume", "dispatch", "cycle", "scan", "scans", "bounds", "aqpop", "heappop",
-                "nheappop", "emit", "nemit", "aqpush"]
+                "nheappop", "emit", "nemit", "aqpush", "win_front", "win_apply"]
         out = []
         for r in range(self.n_replicas):
             row = list(buf[r * w:(r + 1) * w])
-            d = dict(zip(keys, row[:min(w, 14)]))
+            d = dict(zip(keys, row[:min(w, 16)]))
             if w > 16:
                 nk = (w - 16) // 2
                 d["kind_cycles"] = row[16:16 + nk]

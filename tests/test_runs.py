@@ -176,6 +176,8 @@ def _stats_lib():
                                os.path.join(REPO, "kubernetriks_amd", "csrc", "k10s_builder.cpp"), defs])
         os.unlink(defs)
         _STATS["lib"] = out
+        import atexit
+        atexit.register(lambda: os.path.exists(out) and os.unlink(out))
     return _STATS["lib"]
 
 
@@ -294,3 +296,31 @@ def test_windows_cover_the_pipeline():
     finally:
         hb.LIB_PATH, hb._lib, hb.build = saved
     assert wins > 20 and win_events > 0.25 * events, (events, wins, win_events)
+
+
+def test_finish_relay_fused_and_refused():
+    """The finish relay (k10s_engine.h finish_relay_next) is handled inside the finish when it is the
+    next event, and left to the loop when another event shares or precedes its time.  Both happen on
+    the bursty scenarios (integer arrivals and durations: finishes tie in time), whose parity the
+    tests above check; here the host build with event statistics shows both branches ran."""
+    out = _stats_lib()
+    L = ctypes.CDLL(out)
+    import hostcheck_bridge as hb
+    saved = (hb.LIB_PATH, hb._lib, hb.build)
+    try:
+        hb.LIB_PATH, hb._lib, hb.build = out, None, (lambda: None)
+        st = (ctypes.c_uint64 * 48).in_dll(L, "k10s_host_stats")
+        before = int(st[45])
+        finished = 0
+        for seed in (0, 1, 2, 4, 5):
+            scn = bursty_scenario(seed)
+            eng = hb.HostEngine(scn, 1)
+            if _mode(scn) == RUN_UNTIL_TIME:
+                eng.step_until_time(2000.0)
+            else:
+                eng.run_until_all_finished(max_time=20000.0)
+            finished += eng.results()[0]["counters"]["pods_succeeded"]
+        fused = int(st[45]) - before
+    finally:
+        hb.LIB_PATH, hb._lib, hb.build = saved
+    assert 0 < fused < finished, (fused, finished)
