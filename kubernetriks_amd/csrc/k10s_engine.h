@@ -4655,22 +4655,31 @@ pushed:
 // time) and each relays AS_POD_NOT_SCHEDULED -> PS_POD_NOT_SCHEDULED (+as_to_ps, no emission after
 // that), so those two kinds are window kinds as well.
 //
-// Why it is exact.  (1) The window is a prefix of dslab's order: the rings' candidates are merged by
-// (time, id) (ranks by binary search), and the window stops before the first event that is not a
-// candidate — a later source's head, a ring's 16th entry, an event past the time limit — or not one
-// of the six kinds.  (2) Nothing a window event emits can precede a later window event: every
-// emission of these kinds is at least min(as_to_ps, as_to_node) after its event (the finish of N_BIND
-// adds the pod's duration >= 0), every window event is at most that far after the first one, and an
-// emission at an equal time has a larger id.  (3) The handlers commute inside a window: each writes
-// only its own pod's line (two events of one pod never share a window), storage's copy of its node
-// (PS_ASSIGN_REQ: two assignments to one node never share a window), its node component's slot
-// (N_BIND: likewise per slot), commutative header counters (storage's unscheduled count as a sum of
-// +1 / -1) and the group's running count (an atomic add), and it reads nothing the others write.  Emissions get the ids a serial run would hand out
-// (next_seq plus the emission counts of the earlier window events, N_BIND's finish before its start)
-// and are appended to their rings in that order (one delay per ring: times stay sorted); the finishes
-// go into the event heap one by one.  Every reference panic of these handlers, a full ring or heap,
-// the cluster autoscaler (storage's assignment lists) or signed event times end the window before the
-// event (or refuse it), and the serial path then handles that event.
+// Why it is exact.
+// (1) The window is a prefix of dslab's order.  The rings' candidates are merged by (time, id), with
+//     ranks by binary search.  The window stops before the first event that is not a candidate (a
+//     later source's head, a ring's 16th entry, an event past the time limit) or not a window kind.
+// (2) Nothing a window event emits can precede a later window event.  Every emission of these kinds
+//     is at least min(as_to_ps, as_to_node) after its event (the finish of N_BIND adds the pod's
+//     duration >= 0), every window event is at most that far after the first one, and an emission
+//     at an equal time has a larger id.
+// (3) The handlers commute inside a window.  Each writes only:
+//     * its own pod's line (two events of one pod never share a window);
+//     * storage's copy of its node (PS_ASSIGN_REQ: two assignments to one node never share a
+//       window) or its node component's slot (N_BIND: likewise per slot);
+//     * commutative header counters (storage's unscheduled count as a sum of +1 / -1) and the
+//       group's running count (an atomic add).
+//     It reads nothing the others write.
+// Emissions get the ids a serial run would hand out: next_seq plus the emission counts of the
+// earlier window events, N_BIND's finish before its start.  They are appended to their rings in that
+// order (one delay per ring: times stay sorted), and the finishes go into the event heap one by one.
+// A reference panic of these handlers, a full ring or heap, the cluster autoscaler (storage's
+// assignment lists) or signed event times end the window before the event (or refuse it); the
+// serial path then handles that event.
+// Measured and not kept: storage's and the scheduler's PodFinishedRunning as window kinds (+2.6 % at
+// C3, +2.4 % on the backlog; profiles/r05_ab9_win_finish.json): at C3 those windows hold about two
+// events, and the estimator's in-order update grew this function past the VGPRs the event loop
+// leaves free across the call.
 #define K10S_WIN_PER_SRC 16
 struct WinEv {
     double time, x;
