@@ -1359,24 +1359,66 @@ K10S_D float cvt_f32_u32(uint32_t v) {   // (float)v, correctly rounded, as the 
     asm("v_cvt_f32_u32 %0, %1" : "=v"(f) : "v"(v));
     return f;
 }
-// Bit k set: node k of the group is present, fits, and is not ruled out by the screen (scan_screen).
-K10S_D uint32_t screen_grp(const ScanGrp& g, uint32_t bits, uint32_t rc, uint64_t rr, float fa, float fr, float T) {
-    const uint32_t fit = bits & ((uint32_t)(rc <= g.cv.x && rr <= g.r01.x) | ((uint32_t)(rc <= g.cv.y && rr <= g.r01.y) << 1) |
-                                 ((uint32_t)(rc <= g.cv.z && rr <= g.r23.x) << 2) | ((uint32_t)(rc <= g.cv.w && rr <= g.r23.y) << 3));
+// nk: node k of the group is present, fits, and is not ruled out by the screen (scan_screen).  Kept
+// as four bools, the compares' lane masks combine on the scalar unit and gate the exact scores
+// directly; packed into a 4-bit integer they cost a v_cndmask / v_or / v_cmp each per node.
+struct Need4 {
+    bool n0, n1, n2, n3;
+};
+// The screen alone: nk is false when scan_screen rules node k out (A: cpu, H/L: ram's high and low
+// words, each converted to f32 exactly as one instruction).
+K10S_D Need4 screen_keep(f32x2 A01, f32x2 A23, f32x2 H01, f32x2 H23, f32x2 L01, f32x2 L23, float fa, float fr, float T) {
+    const f32x2 two32 = {4294967296.0f, 4294967296.0f};
+    const f32x2 R01 = __builtin_elementwise_fma(H01, two32, L01), R23 = __builtin_elementwise_fma(H23, two32, L23);
+    const f32x2 va = {fa, fa}, vr = {fr, fr}, vT = {T, T};
+    const f32x2 l01 = __builtin_elementwise_fma(va, R01, vr * A01), l23 = __builtin_elementwise_fma(va, R23, vr * A23);
+    const f32x2 r01 = (A01 * R01) * vT, r23 = (A23 * R23) * vT;
+    return {!(l01.x > r01.x), !(l01.y > r01.y), !(l23.x > r23.x), !(l23.y > r23.y)};
+}
+K10S_D Need4 screen_grp(const ScanGrp& g, uint32_t bits, uint32_t rc, uint64_t rr, float fa, float fr, float T) {
+    const bool f0 = (bits & 1u) && rc <= g.cv.x && rr <= g.r01.x;
+    const bool f1 = (bits & 2u) && rc <= g.cv.y && rr <= g.r01.y;
+    const bool f2 = (bits & 4u) && rc <= g.cv.z && rr <= g.r23.x;
+    const bool f3 = (bits & 8u) && rc <= g.cv.w && rr <= g.r23.y;
     const f32x2 A01 = {cvt_f32_u32(g.cv.x), cvt_f32_u32(g.cv.y)};
     const f32x2 A23 = {cvt_f32_u32(g.cv.z), cvt_f32_u32(g.cv.w)};
     const f32x2 H01 = {cvt_f32_u32((uint32_t)(g.r01.x >> 32)), cvt_f32_u32((uint32_t)(g.r01.y >> 32))};
     const f32x2 H23 = {cvt_f32_u32((uint32_t)(g.r23.x >> 32)), cvt_f32_u32((uint32_t)(g.r23.y >> 32))};
     const f32x2 L01 = {cvt_f32_u32((uint32_t)g.r01.x), cvt_f32_u32((uint32_t)g.r01.y)};
     const f32x2 L23 = {cvt_f32_u32((uint32_t)g.r23.x), cvt_f32_u32((uint32_t)g.r23.y)};
-    const f32x2 two32 = {4294967296.0f, 4294967296.0f};
-    const f32x2 R01 = __builtin_elementwise_fma(H01, two32, L01), R23 = __builtin_elementwise_fma(H23, two32, L23);
-    const f32x2 va = {fa, fa}, vr = {fr, fr}, vT = {T, T};
-    const f32x2 l01 = __builtin_elementwise_fma(va, R01, vr * A01), l23 = __builtin_elementwise_fma(va, R23, vr * A23);
-    const f32x2 r01 = (A01 * R01) * vT, r23 = (A23 * R23) * vT;
-    const uint32_t out = (uint32_t)(l01.x > r01.x) | ((uint32_t)(l01.y > r01.y) << 1) | ((uint32_t)(l23.x > r23.x) << 2) |
-                         ((uint32_t)(l23.y > r23.y) << 3);
-    return fit & ~out;
+    const Need4 k = screen_keep(A01, A23, H01, H23, L01, L23, fa, fr, T);
+    return {f0 && k.n0, f1 && k.n1, f2 && k.n2, f3 && k.n3};
+}
+// The packed cache's whole-block path: a lane's 4 entries as loaded, (lo, hi) words each (cpu =
+// hi >> 8, ram = (hi & 0xff)·2^32 + lo for K10S_PK_SHIFT 40).  The screen runs first on the raw
+// words — the ram's high byte converts with v_cvt_f32_ubyte0, so nothing is masked — and Fit only
+// for the nodes it keeps, which are few once the wave has a threshold: a node that does not fit
+// has u = rc/A + rr/R > 1, far above any scored node's.  Kept-and-fitting is exactly screen_grp's
+// set, so the same nodes are scored in the same order.
+static_assert(K10S_PK_SHIFT == 40, "pk_* helpers assume the ram's high word is the entry's low byte of hi");
+struct PkGrp {
+    uint2 w0, w1, w2, w3;
+};
+K10S_D PkGrp pk_load_full(const uint64_t* s_node, uint32_t n0) {
+    const uint4 a = *reinterpret_cast<const uint4*>(s_node + n0);
+    const uint4 b = *reinterpret_cast<const uint4*>(s_node + n0 + 2);
+    return {{a.x, a.y}, {a.z, a.w}, {b.x, b.y}, {b.z, b.w}};
+}
+K10S_D float cvt_f32_ubyte0(uint32_t v) {   // (float)(v & 0xff), as the one instruction
+    float f;
+    asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(f) : "v"(v));
+    return f;
+}
+K10S_D uint32_t pk_cpu(uint2 w) { return w.y >> (K10S_PK_SHIFT - 32); }
+K10S_D uint64_t pk_ram(uint2 w) { return ((uint64_t)(w.y & 0xffu) << 32) | w.x; }
+K10S_D Need4 screen_pk(const PkGrp& g, float fa, float fr, float T) {
+    const f32x2 A01 = {cvt_f32_u32(pk_cpu(g.w0)), cvt_f32_u32(pk_cpu(g.w1))};
+    const f32x2 A23 = {cvt_f32_u32(pk_cpu(g.w2)), cvt_f32_u32(pk_cpu(g.w3))};
+    const f32x2 H01 = {cvt_f32_ubyte0(g.w0.y), cvt_f32_ubyte0(g.w1.y)};
+    const f32x2 H23 = {cvt_f32_ubyte0(g.w2.y), cvt_f32_ubyte0(g.w3.y)};
+    const f32x2 L01 = {cvt_f32_u32(g.w0.x), cvt_f32_u32(g.w1.x)};
+    const f32x2 L23 = {cvt_f32_u32(g.w2.x), cvt_f32_u32(g.w3.x)};
+    return screen_keep(A01, A23, H01, H23, L01, L23, fa, fr, T);
 }
 // The exact LeastAllocated score of a fitting node (scan_node_d's arithmetic; frc, frr: the request
 // as f64).
@@ -1441,14 +1483,15 @@ K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, cons
     // one 256-node step of a lane's group g at n0 (screen, exact scores, threshold)
     auto step = [&](const ScanGrp& g, uint32_t n0, auto full) {
         const uint32_t bits = decltype(full)::value ? 0xFu : grp_bits(g, n0, n_nodes);
-        const uint32_t need = screen_grp(g, bits, rc, rr, fa, fr, T);
-        if (need) {
-            if (need & 1u) score_node_exact(n0, g.cv.x, g.r01.x, rr, frc, frr, best_s, best_n, la, lr, lu);
-            if (need & 2u) score_node_exact(n0 + 1, g.cv.y, g.r01.y, rr, frc, frr, best_s, best_n, la, lr, lu);
-            if (need & 4u) score_node_exact(n0 + 2, g.cv.z, g.r23.x, rr, frc, frr, best_s, best_n, la, lr, lu);
-            if (need & 8u) score_node_exact(n0 + 3, g.cv.w, g.r23.y, rr, frc, frr, best_s, best_n, la, lr, lu);
+        const Need4 need = screen_grp(g, bits, rc, rr, fa, fr, T);
+        const bool any = need.n0 | need.n1 | need.n2 | need.n3;
+        if (any) {
+            if (need.n0) score_node_exact(n0, g.cv.x, g.r01.x, rr, frc, frr, best_s, best_n, la, lr, lu);
+            if (need.n1) score_node_exact(n0 + 1, g.cv.y, g.r01.y, rr, frc, frr, best_s, best_n, la, lr, lu);
+            if (need.n2) score_node_exact(n0 + 2, g.cv.z, g.r23.x, rr, frc, frr, best_s, best_n, la, lr, lu);
+            if (need.n3) score_node_exact(n0 + 3, g.cv.w, g.r23.y, rr, frc, frr, best_s, best_n, la, lr, lu);
         }
-        if (__ballot(need != 0)) {
+        if (__ballot(any)) {
             const float thr = __builtin_bit_cast(float, uniform_u32(__builtin_bit_cast(uint32_t, wave_min_f32(lu))));
             T = thr + K10S_SCREEN_EPS;
         }
@@ -1461,11 +1504,34 @@ K10S_D void scan_lanes_screen(const uint32_t* s_cpu, const uint64_t* s_ram, cons
     if (PK && PIPE == 0) {
         uint32_t base = 0;
         if (NP) {
+            // one 256-node step on the raw packed words (screen_pk; Fit after the screen)
+            auto step_pk = [&](const PkGrp& g, uint32_t n0) {
+                const Need4 keep = screen_pk(g, fa, fr, T);
+                bool scored = false;
+                if (keep.n0 | keep.n1 | keep.n2 | keep.n3) {
+                    auto one = [&](bool kept, uint2 w, uint32_t n) {
+                        const uint32_t ac = pk_cpu(w);
+                        const uint64_t ar = pk_ram(w);
+                        if (kept && rc <= ac && rr <= ar) {
+                            score_node_exact(n, ac, ar, rr, frc, frr, best_s, best_n, la, lr, lu);
+                            scored = true;
+                        }
+                    };
+                    one(keep.n0, g.w0, n0);
+                    one(keep.n1, g.w1, n0 + 1);
+                    one(keep.n2, g.w2, n0 + 2);
+                    one(keep.n3, g.w3, n0 + 3);
+                }
+                if (__ballot(scored)) {
+                    const float thr = __builtin_bit_cast(float, uniform_u32(__builtin_bit_cast(uint32_t, wave_min_f32(lu))));
+                    T = thr + K10S_SCREEN_EPS;
+                }
+            };
             for (; base + 512u <= n_nodes; base += 512) {
-                const ScanGrp g0 = scan_load_pk_full(s_ram, base + l4);
-                const ScanGrp g1 = scan_load_pk_full(s_ram, base + 256u + l4);
-                step(g0, base + l4, std::true_type());
-                step(g1, base + 256u + l4, std::true_type());
+                const PkGrp g0 = pk_load_full(s_ram, base + l4);
+                const PkGrp g1 = pk_load_full(s_ram, base + 256u + l4);
+                step_pk(g0, base + l4);
+                step_pk(g1, base + 256u + l4);
             }
         }
         for (; base < n_nodes; base += 512) {
@@ -2297,7 +2363,7 @@ K10S_HD_NOINL void run_scheduling_cycle_tiles(Ctx& c, double t) {
         }
 #endif
         const uint32_t nofit = (need & ~found) | never;
-        uint64_t rlanes = 0;   // lanes whose share holds a node reserved by this tile
+        [[maybe_unused]] uint64_t rlanes = 0;   // lanes whose share holds a node reserved by this tile
         for (uint32_t j = 0; j < nt && !c.H().error_code; j++) {
             const QInfo q = slot[top - 1 - j];
             if (uniform_u32(q.pod) == 0xFFFFFFFFu) continue;
