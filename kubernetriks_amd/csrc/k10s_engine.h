@@ -486,12 +486,19 @@ K10S_D __amdgpu_buffer_rsrc_t heap_rsrc(Ctx& c) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)c.V().heap(), (short)0,
                                              (int)(K10S_DC.L.cap_heap * (uint32_t)sizeof(HeapEv)), 0x00020000);
 }
+// The HBM part is a structure of two arrays (round 5): position i's key half (time, id, kind|slot;
+// 16 B) at i·16 and its payload half (a, b, x; 16 B) at (cap_heap + i)·16, both in the heap section
+// (cap_heap · 32 B, as sized by the builder).  A pop's minimum over 64 children then reads only key
+// halves — 1 KB a level instead of 2 KB — and the chosen child's payload (heap_min_child_ev).
+// Device-only: the host engine's heap stays an array of HeapEv (no state crosses the two).
+static_assert(sizeof(HeapEv) == 32, "key and payload halves of 16 B");
+K10S_D int heap_key_off(uint32_t i) { return (int)(i * 16u); }
+K10S_D int heap_pay_off(uint32_t i) { return (int)((K10S_DC.L.cap_heap + i) * 16u); }
 K10S_D HeapEv heap_get(Ctx& c, uint32_t i) {
     if (i < K10S_HEAP_TOP) return k10s_hdr.heap_lds[i];
     const __amdgpu_buffer_rsrc_t rs = heap_rsrc(c);
-    const int off = (int)(i * (uint32_t)sizeof(HeapEv));
-    auto lo = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
-    auto hi = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0);
+    auto lo = __builtin_amdgcn_raw_buffer_load_b128(rs, heap_key_off(i), 0, 0);
+    auto hi = __builtin_amdgcn_raw_buffer_load_b128(rs, heap_pay_off(i), 0, 0);
     HeapEv e;
     e.time = u2f(((uint64_t)lo[1] << 32) | lo[0]);
     e.seq = lo[2];
@@ -508,13 +515,12 @@ K10S_D void heap_put(Ctx& c, uint32_t i, const HeapEv& e) {
         return;
     }
     const __amdgpu_buffer_rsrc_t rs = heap_rsrc(c);
-    const int off = (int)(i * (uint32_t)sizeof(HeapEv));
     const uint64_t tb = f2u(e.time), xb = f2u(e.x);
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     v4u lo = {(uint32_t)tb, (uint32_t)(tb >> 32), e.seq, (uint32_t)e.kind | ((uint32_t)(uint16_t)e.slot << 16)};
     v4u hi = {e.a, e.b, (uint32_t)xb, (uint32_t)(xb >> 32)};
-    __builtin_amdgcn_raw_buffer_store_b128(lo, rs, off, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b128(hi, rs, off + 16, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(lo, rs, heap_key_off(i), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(hi, rs, heap_pay_off(i), 0, 0);
 }
 #else
 K10S_HD HeapEv heap_get(Ctx& c, uint32_t i) { return i < K10S_HEAP_TOP ? c.H().heap_lds[i] : c.V().heap()[i]; }
@@ -655,7 +661,7 @@ K10S_HD uint32_t heap_min_child(Ctx& c, uint32_t first, uint32_t n, int64_t& kmi
             sq = k10s_hdr.heap_lds[i].seq;
         } else {
             const __amdgpu_buffer_rsrc_t rs = heap_rsrc(c);
-            auto lo = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * (uint32_t)sizeof(HeapEv)), 0, 0);
+            auto lo = __builtin_amdgcn_raw_buffer_load_b128(rs, heap_key_off(i), 0, 0);
             k = total_key(u2f(((uint64_t)lo[1] << 32) | lo[0]));
             sq = lo[2];
         }
@@ -694,9 +700,10 @@ K10S_HD uint32_t heap_min_child(Ctx& c, uint32_t first, uint32_t n, int64_t& kmi
 }
 
 #if K10S_DEVICE
-// The device's heap_pop: (a) the moved-up entry of a level in HBM taken from the lane that
-// loaded it (heap_min_child_ev loads the whole 32-B entries, so the chosen child needs no second
-// load), and (b) the last entry's load awaited only after the first level's minimum (LDS) is known.
+// The device's heap_pop: (a) the moved-up entry of a level in HBM: its key half taken from the
+// lane that loaded it (heap_min_child_ev loads the 64 children's key halves) and its payload half
+// loaded once the minimum is known, and (b) the last entry's load awaited only after the first
+// level's minimum (LDS) is known.
 // Same comparisons and moves.  Inlined into the event loop it lost 1.5 % to register pressure
 // (profiles/r03_k6_heap_pop_ab.json); the whole pop runs out of line on the device (+1.6 %,
 // profiles/r03_k11_heap_pop_call_ab.json).
@@ -717,11 +724,10 @@ K10S_D uint32_t heap_min_child_ev(Ctx& c, uint32_t first, uint32_t n, int64_t& k
     int64_t k = 0x7FFFFFFFFFFFFFFFll;
     uint32_t sq = 0xFFFFFFFFu;
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    v4u lo = {0u, 0u, 0u, 0u}, hi = {0u, 0u, 0u, 0u};
+    v4u lo = {0u, 0u, 0u, 0u};
+    const __amdgpu_buffer_rsrc_t rs = heap_rsrc(c);
     if (lane < K10S_HEAP_D && i < n) {
-        const __amdgpu_buffer_rsrc_t rs = heap_rsrc(c);
-        lo = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * (uint32_t)sizeof(HeapEv)), 0, 0);
-        hi = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * (uint32_t)sizeof(HeapEv)) + 16, 0, 0);
+        lo = __builtin_amdgcn_raw_buffer_load_b128(rs, heap_key_off(i), 0, 0);   // key halves only
         k = total_key(u2f(((uint64_t)lo[1] << 32) | lo[0]));
         sq = lo[2];
     }
@@ -736,16 +742,18 @@ K10S_D uint32_t heap_min_child_ev(Ctx& c, uint32_t first, uint32_t n, int64_t& k
     kmin = (int64_t)(klo | (khi << 32));
     smin = (uint32_t)__builtin_amdgcn_readfirstlane((int)sq);
     const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
-    const int src = (int)(m - first);   // the lane that loaded entry m
+    const v4u hi = __builtin_amdgcn_raw_buffer_load_b128(rs, heap_pay_off(m), 0, 0);   // m's payload half
+    const int src = (int)(m - first);   // the lane that loaded entry m's key half
     auto rl = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, src); };
+    auto rf = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
     ev.time = u2f(((uint64_t)rl(lo[1]) << 32) | rl(lo[0]));
     ev.seq = rl(lo[2]);
     const uint32_t ks = rl(lo[3]);
     ev.kind = (uint16_t)ks;
     ev.slot = (int16_t)(ks >> 16);
-    ev.a = rl(hi[0]);
-    ev.b = rl(hi[1]);
-    ev.x = u2f(((uint64_t)rl(hi[3]) << 32) | rl(hi[2]));
+    ev.a = rf(hi[0]);
+    ev.b = rf(hi[1]);
+    ev.x = u2f(((uint64_t)rf(hi[3]) << 32) | rf(hi[2]));
     return m;
 }
 #define K10S_HEAP_POP_ATTR __attribute__((noinline))
