@@ -19,7 +19,12 @@ _lib = None
 
 
 def build():
-    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "tests", "hostcheck")])
+    """make under a file lock: parallel test workers rebuild a stale library once, one at a time."""
+    import fcntl
+    os.makedirs(os.path.join(REPO, "build"), exist_ok=True)
+    with open(os.path.join(REPO, "build", ".hostcheck.lock"), "w") as f:
+        fcntl.flock(f, fcntl.LOCK_EX)
+        subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "tests", "hostcheck")])
 
 
 def lib():
