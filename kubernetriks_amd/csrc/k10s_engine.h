@@ -26,11 +26,11 @@ namespace k10s {
 // working replica header — clock, id counter, queue sizes, counters, estimators — is staged in LDS
 // (k10s_hdr) for the whole launch: one workgroup = one replica.  Host (test-only check build): the
 // same code reads them through the pointers held in Ctx.
-// The replica region of this workgroup and its most used sections as absolute addresses
-// (k10s_sec, LDS), written by the kernels before anything else: an access reads its section's
-// address with one ds_read_b64 (CSE'd within a function: the array is never written afterwards)
-// instead of re-deriving it through the opaque constant block (replica index x stride + section
-// offset: ~10 SALU + 3 SMEM per access, repeated at every access by design, see K10S_DC below).
+// The replica region of this workgroup and its most used sections: by default (K10S_SEC_SGPR, Rep
+// below) re-derived at each use from the workgroup id and the constant block (replica index x
+// stride + section offset, SALU and scalar loads); with K10S_SEC_SGPR=0 read as absolute addresses
+// from k10s_sec (LDS, written by the kernels before anything else) with one ds_read_b64 and two
+// v_readfirstlane.
 enum : int { SEC_BASE = 0, SEC_POD, SEC_NODE, SEC_SLOT, SEC_FQ, SEC_HEAP, SEC_SNODE, SEC_PRES, SEC_AQ, SEC_UQ,
              SEC_PARAMS, K10S_NSEC };   // SEC_PARAMS: this replica's k10s_replica_params (read-only)
 #if defined(__HIP__)
@@ -138,9 +138,34 @@ K10S_D DevConstPtr dc_ptr() {
 
 // Typed accessors over one replica's region; section bases are recomputed from the (constant)
 // layout at each use instead of being held live across the event loop.
+// K10S_SEC_SGPR=1 (default since round 5): a section base is the workgroup id (one replica per
+// workgroup) x the stride + the section's offset, from the constant block: scalar loads and SALU
+// only, where the LDS table costs a ds_read_b64 and two v_readfirstlane per use.  The handlers'
+// VALU falls 10-20 % statically for 20-30 % more SALU (C3 +0.9 %, backlog +1.8 %,
+// profiles/r05_ab13_sec_sgpr.json).  0: the LDS table k10s_sec.
+#ifndef K10S_SEC_SGPR
+#define K10S_SEC_SGPR 1
+#endif
 struct Rep {
 #if K10S_DEVICE
+#if K10S_SEC_SGPR
+    K10S_D static K10S_GB(uint8_t) sec(int i) {
+        const DevConst& D = K10S_DC;
+        // a callee receives the id in an SGPR, the kernel keeps it across its calls; the empty asm
+        // makes every use recompute the base instead of hoisting r x stride out of the event loop
+        // and keeping it live (in VGPRs) across the handler calls
+        uint32_t r = (uint32_t)__builtin_amdgcn_readfirstlane((int)__builtin_amdgcn_workgroup_id_x());
+        asm volatile("" : "+s"(r));
+        if (i == SEC_PARAMS) return (K10S_GB(uint8_t))(D.params + r);
+        const Layout& L = D.L;
+        const uint64_t off = i == SEC_POD ? L.pod : i == SEC_NODE ? L.node : i == SEC_SLOT ? L.slot : i == SEC_FQ ? L.fq
+                           : i == SEC_HEAP ? L.heap : i == SEC_SNODE ? L.s_node : i == SEC_PRES ? L.s_present
+                           : i == SEC_AQ ? L.aq : i == SEC_UQ ? L.uq : 0;
+        return (K10S_GB(uint8_t))((uint64_t)D.base + (uint64_t)r * L.stride + off);
+    }
+#else
     K10S_D static K10S_GB(uint8_t) sec(int i) { return (K10S_GB(uint8_t))uniform_u64(k10s_sec[i]); }
+#endif
     K10S_D const Layout& L() const { return K10S_DC.L; }
     template <typename T>
     K10S_D T* at(uint64_t off) const { return (T*)(sec(SEC_BASE) + off); }
@@ -208,7 +233,7 @@ inline Rep make_rep(uint8_t* base, const Layout& L, uint32_t r) {
 struct Ctx {
 #if K10S_DEVICE
     K10S_D const Scenario& S() const { return K10S_DC.sc; }
-    K10S_D const Params& P() const { return *(K10S_RO(Params))uniform_u64(k10s_sec[SEC_PARAMS]); }
+    K10S_D const Params& P() const { return *(K10S_RO(Params))Rep::sec(SEC_PARAMS); }
     K10S_D const Layout& Ly() const { return K10S_DC.L; }
     K10S_D RepHdr& H() const { return k10s_hdr; }
     K10S_D Rep V() const { return Rep(); }

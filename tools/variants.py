@@ -9,6 +9,9 @@ Live knobs (round 4 removed the measured-and-not-kept alternatives; their A/B hi
             (unit-surface scan loads N steps ahead); LOOP_SCAN_PIPE=N; qN -DK10S_FQW=N (FIFO window
             entries in LDS); hN -DK10S_HEAP_D=N (event-heap arity 8/16/32/64); AQ_TOP=N;
             FAIR_SHIFT=N, FAIR_BAND=N (wave priorities)
+  round 5   WINDOWS=0|1, WIN_NOTSCHED=0|1, FUSE_FINISH=0|1, RUNS=0|1 (events handled together);
+            SEC_SGPR=0|1 (section bases from the LDS table / from the workgroup id); TILE_BEST=1,
+            TILE_ALWAYS=1 (best-node tiles, measured and not kept)
   NAME=v    -DK10S_NAME=v (any of the above by name), parts joined by '+'
 Usage: tools/variants.py prof w8 s1 WAVES_PER_EU=8+FQW=4 ..."""
 import os
