@@ -1923,7 +1923,7 @@ K10S_HD int schedule_scan_pruned(Ctx& c, uint32_t rc, uint64_t rr, int32_t* chos
 // fits and the pass would only add reads; in the backlog regime most attempts fail and their node
 // scans become one shared read per tile.
 #ifndef K10S_TILE
-#define K10S_TILE 8
+#define K10S_TILE 32   // round 5: 8 -> 32, backlog -3 % and 6,511 -> 5,032 entries read per placement (r05_ab18)
 #endif
 static_assert(K10S_TILE >= 1 && K10S_TILE <= 32, "K10S_TILE");
 // Bit j set: pod j of the tile (need bit j: request rc8[j] = cpu << 8, rr[j] = ram, both > 0 and cpu

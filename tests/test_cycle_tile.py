@@ -1,5 +1,5 @@
 """The scheduling cycle's tiles (k10s_engine.h tile_best_pass / run_scheduling_cycle_tiles): after a
-cycle with a failed attempt, the cycle pops K10S_TILE (8) pods at a time and reads the packed node
+cycle with a failed attempt, the cycle pops K10S_TILE (32) pods at a time and reads the packed node
 cache once for all of them.  The read finds, per pod and per lane share of the nodes, the best fitting
 node of the cache as it is then.  Pods that fit nowhere fail without a scan (exact: nothing is pushed
 onto the action queue during a cycle, scheduler.rs:261-330, and a reservation only lowers a node's
