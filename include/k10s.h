@@ -81,11 +81,12 @@ extern "C" {
 #define K10S_PANIC_NEGATIVE_DELAY 15       /* dslab-core add_event: an event emitted with a negative (or NaN)
                                               delay, i.e. into the past (a negative pod duration, network
                                               delay or tick interval reaching an emission) */
-#define K10S_ERR_HEAP_FULL 100             /* engine capacity: event heap */
-#define K10S_ERR_QUEUE_FULL 101            /* engine capacity: scheduler queues */
-#define K10S_ERR_NAME_BOUND 102            /* engine capacity: generated-name universe bound */
+#define K10S_ERR_HEAP_FULL 100             /* engine capacity: event heap (regrown, k10s_engine_name_bounds) */
+#define K10S_ERR_QUEUE_FULL 101            /* engine capacity: scheduler queues (regrown) */
+#define K10S_ERR_NAME_BOUND 102            /* engine capacity: generated-name universe bound (regrown) */
 #define K10S_ERR_SEQ_OVERFLOW 103          /* engine capacity: 2^32 event ids in one replica */
-#define K10S_ERR_CA_BUFFER 104             /* engine capacity: CA action buffer */
+#define K10S_ERR_CA_BUFFER 104             /* CA action buffers: sized so no decision can fill them (an
+                                              invariant, k10s_host.cpp regrow), never regrown */
 #define K10S_ERR_NODE_CACHE_RANGE 105      /* engine capacity: a packed node-cache entry would exceed its
                                               field (allocatable cpu >= 2^24 or ram >= 2^40 after a
                                               release; cannot happen while allocatable <= capacity) */
@@ -358,14 +359,31 @@ int32_t k10s_engine_group_sizes(const k10s_engine* e, uint32_t replica, uint32_t
 /* Generated-name universes of the compiled batch: names per pod group ("{group}_{k}", the HPA's pods)
    and per CA node group ("{group}_{k}").  k10s_capacities.group_name_bound / ca_name_bound set the
    first universe (0 = derived from the scenario).  The reference bounds neither
-   (kube_horizontal_pod_autoscaler.rs:178-182, api_server.rs:421); when a replica would create a name
-   beyond its universe (K10S_ERR_NAME_BOUND), k10s_engine_run / k10s_engine_sync recompile the batch
-   with that universe doubled (up to 2^20 names) and replay every run call since the last
-   initialize, so results equal the reference's; the name tables below then describe the regrown
-   batch (re-read them after a run). */
+   (kube_horizontal_pod_autoscaler.rs:178-182, api_server.rs:421), nor its event queue and scheduler
+   queues (dslab-core's BinaryHeap, scheduler.rs:45, 49).  When a replica outgrows a universe
+   (K10S_ERR_NAME_BOUND), the event heap (K10S_ERR_HEAP_FULL) or the active queue / unschedulable
+   map (K10S_ERR_QUEUE_FULL), k10s_engine_run / k10s_engine_sync recompile the batch with every
+   exhausted capacity doubled (up to 2^20 names per universe, 2^30 heap or queue entries) and replay
+   every run and step call since the last initialize, so results equal the reference's.
+   * Memory: the regrown batch is allocated beside the current one if both fit, else in its place;
+     if neither fits, the call returns K10S_E_CAPACITY and the stopped results stay readable.  If the
+     regrow released the current state and then failed, every later call on the engine returns
+     K10S_E_CAPACITY (destroy it).
+   * Timing: elapsed_ms of k10s_engine_run includes the regrow and its replays (k10s_engine_capacities
+     reports how many regrows happened).
+   * Names: the name tables below then describe the regrown batch.  A pointer returned by
+     k10s_engine_node_name / k10s_engine_pod_name / k10s_engine_group_name before a run or sync is
+     invalid after one that regrew: re-read the names after every run. */
 int32_t k10s_engine_name_bounds(const k10s_engine* e, uint32_t* group_bound, uint32_t* ca_bound);
+/* The batch's effective capacities (after any regrow): event_heap, active_queue, unschedulable and
+   the two name bounds as compiled (derived values filled in), delay_fifo = entries per ring
+   (K10S_FIFO_OFF when off), the other fields as given at create.  *regrows (may be NULL) = batches
+   recompiled by regrow since create. */
+int32_t k10s_engine_capacities(const k10s_engine* e, k10s_capacities* out, uint32_t* regrows);
 
-/* Name tables of the compiled scenario (index -> name), for mapping logs back to names. */
+/* Name tables of the compiled scenario (index -> name), for mapping logs back to names.  The
+   returned strings belong to the engine and stay valid until the next run / sync that regrows the
+   batch (k10s_engine_name_bounds) or k10s_engine_destroy. */
 uint32_t k10s_engine_num_nodes(const k10s_engine* e);
 uint32_t k10s_engine_num_pods(const k10s_engine* e);
 uint32_t k10s_engine_num_groups(const k10s_engine* e);

@@ -17,6 +17,9 @@
 #pragma once
 
 #include "k10s_state.h"
+#if !defined(__HIP__) && defined(K10S_PRUNE_STUDY)
+#include <vector>
+#endif
 
 namespace k10s {
 
@@ -2201,6 +2204,136 @@ K10S_HD uint32_t tile_lanes_host(const uint64_t* s_node, uint32_t n_nodes, uint3
 // (a tile found no node for the pod: its attempt fails exactly as the scan would), or the node a
 // tile resolved for it (exactly the scan's choice; the tile counted its reads).  Returns the node
 // the pod was assigned, or -1.
+#if !K10S_DEVICE && defined(K10S_PRUNE_STUDY)
+// Tooling (tools/prune_study.py): how many entries an exact block-pruned scan would read, with tight
+// componentwise block bounds, best-first block order, for block sizes 16..512.  Slots: [2i] entries
+// read (bounds + blocks), [2i+1] blocks scanned; [12] scans.
+extern "C" uint64_t k10s_prune_stats[32];
+inline void k10s_prune_study(const uint64_t* s, uint32_t N, uint32_t rc, uint64_t rr) {
+    k10s_prune_stats[12] += 1;
+    for (int bi = 0; bi < 6; bi++) {
+        const uint32_t B = 16u << bi, NB = (N + B - 1) / B;
+        static uint64_t ub[1 << 12];
+        for (uint32_t b = 0; b < NB; b++) {
+            uint32_t mc = 0;
+            uint64_t mr = 0;
+            for (uint32_t n = b * B; n < N && n < (b + 1) * B; n++) {
+                const NcEnt v = nc_unpack(s[n]);
+                mc = v.cpu > mc ? v.cpu : mc;
+                mr = v.ram > mr ? v.ram : mr;
+            }
+            ub[b] = (mc >= rc && mr >= rr) ? score_key(la_score(mc, mr, rc, rr)) : 0;
+        }
+        uint64_t best_key = 0;
+        int64_t best_n = -1;
+        uint64_t reads = NB, blocks = 0;
+        for (;;) {
+            uint64_t k = 0;
+            int64_t b = -1;
+            for (uint32_t x = 0; x < NB; x++)
+                if (ub[x] && ub[x] >= k) {
+                    k = ub[x];
+                    b = x;
+                }
+            if (b < 0) break;
+            if (best_n >= 0 && (k < best_key || (k == best_key && (int64_t)((b + 1) * B) <= best_n))) break;
+            for (uint32_t n = (uint32_t)b * B; n < N && n < ((uint32_t)b + 1) * B; n++) {
+                const NcEnt v = nc_unpack(s[n]);
+                if (rc <= v.cpu && rr <= v.ram) {
+                    const uint64_t kk = score_key(la_score(v.cpu, v.ram, rc, rr));
+                    if (kk > best_key || (kk == best_key && (int64_t)n > best_n)) {
+                        best_key = kk;
+                        best_n = n;
+                    }
+                }
+            }
+            reads += B;
+            blocks += 1;
+            ub[b] = 0;
+        }
+        k10s_prune_stats[2 * bi] += reads;
+        k10s_prune_stats[2 * bi + 1] += blocks;
+    }
+    // near ties of the argmax: nodes with exactly its score, within 1e-5 of its u, within 1e-4
+    uint64_t bk = 0;
+    for (uint32_t n = 0; n < N; n++) {
+        const NcEnt v = nc_unpack(s[n]);
+        if (rc <= v.cpu && rr <= v.ram) {
+            const uint64_t k = score_key(la_score(v.cpu, v.ram, rc, rr));
+            bk = k > bk ? k : bk;
+        }
+    }
+    if (!bk) return;
+    double bs = 0;
+    for (uint32_t n = 0; n < N; n++) {
+        const NcEnt v = nc_unpack(s[n]);
+        if (rc <= v.cpu && rr <= v.ram && score_key(la_score(v.cpu, v.ram, rc, rr)) == bk) bs = la_score(v.cpu, v.ram, rc, rr);
+    }
+    for (uint32_t n = 0; n < N; n++) {
+        const NcEnt v = nc_unpack(s[n]);
+        if (!(rc <= v.cpu && rr <= v.ram)) continue;
+        const double sc = la_score(v.cpu, v.ram, rc, rr);
+        const double du = (bs - sc) * 0.02;
+        if (sc == bs) k10s_prune_stats[28] += 1;
+        if (du <= 1e-5) k10s_prune_stats[29] += 1;
+        if (du <= 1e-4) k10s_prune_stats[30] += 1;
+        if (du <= 1e-3) k10s_prune_stats[31] += 1;
+    }
+}
+// Cycle depth study: the cache at the cycle's start (snapshot) and the nodes reserved so far in
+// the cycle; for each attempt, d = 1 + the number of reserved nodes whose snapshot (score, index)
+// beats the pod's pick in the snapshot order — the depth a per-pod snapshot top-K list needs.
+// Histogram slots [16 + min(d, 15)]; [13] cycles, [14] attempts in cycles, [15] distinct reserved.
+struct PruneCyc {
+    std::vector<uint64_t> snap;
+    std::vector<uint32_t> rset;
+};
+inline PruneCyc& prune_cyc() {
+    static PruneCyc p;
+    return p;
+}
+inline void k10s_prune_cycle_start(const uint64_t* s, uint32_t N) {
+    PruneCyc& p = prune_cyc();
+    p.snap.assign(s, s + N);
+    p.rset.clear();
+    k10s_prune_stats[13] += 1;
+}
+inline void k10s_prune_cycle_pick(uint32_t rc, uint64_t rr, int32_t pick) {
+    PruneCyc& p = prune_cyc();
+    k10s_prune_stats[14] += 1;
+    if (pick < 0) return;
+    // pick's snapshot key
+    auto key = [&](uint32_t n) -> uint64_t {
+        const NcEnt v = nc_unpack(p.snap[n]);
+        return (rc <= v.cpu && rr <= v.ram) ? score_key(la_score(v.cpu, v.ram, rc, rr)) : 0;
+    };
+    // the best snapshot node outside the reserved set, then the reserved nodes above it
+    std::vector<char> inr(p.snap.size(), 0);
+    for (uint32_t n : p.rset) inr[n] = 1;
+    uint64_t kp = 0;
+    int64_t m = -1;
+    for (uint32_t n = 0; n < p.snap.size(); n++) {
+        if (inr[n]) continue;
+        const uint64_t k = key(n);
+        if (k && (k > kp || (k == kp && (int64_t)n > m))) {
+            kp = k;
+            m = n;
+        }
+    }
+    uint32_t d = 1;
+    for (uint32_t n : p.rset) {
+        const uint64_t k = key(n);
+        if (k > kp || (k == kp && (int64_t)n > m)) d++;
+    }
+    k10s_prune_stats[16 + (d < 15 ? d : 15)] += 1;
+    bool seen = false;
+    for (uint32_t n : p.rset) seen |= n == (uint32_t)pick;
+    if (!seen) {
+        p.rset.push_back((uint32_t)pick);
+        k10s_prune_stats[15] += 1;
+    }
+}
+#endif
 #define K10S_PICK_SCAN (-1)
 #define K10S_PICK_NOFIT (-2)
 template <bool PLUG>
@@ -2238,6 +2371,9 @@ K10S_HD int32_t cycle_attempt(Ctx& c, double t, QInfo q, int32_t pick, double& c
             st = schedule_scan_pruned(c, rc, rr, &chosen, &nread);
         }
         if (st < 0) {
+#if !K10S_DEVICE && defined(K10S_PRUNE_STUDY)
+            if (nc_packed(c) && w == 1.0 && rc > 0 && rr > 0) k10s_prune_study(c.V().s_node(), c.S().n_nodes, rc, rr);
+#endif
             if (nc_packed(c))
                 st = schedule_scan<true, true>(nullptr, c.V().s_node(), c.V().s_present(), c.S().n_nodes, rc, rr, w,
                                                &chosen);
@@ -2292,12 +2428,21 @@ K10S_HD_NOINL void run_scheduling_cycle_t(Ctx& c, double t) {
     uint32_t fails = 0;
     RepHdr* h = &c.H();
     h->g_pods_q = (uint64_t)h->aq_size + (uint64_t)h->uq_size;  // scheduler.rs:256-259
+#if !K10S_DEVICE && defined(K10S_PRUNE_STUDY)
+    if (nc_packed(c)) k10s_prune_cycle_start(c.V().s_node(), c.S().n_nodes);
+#endif
     while (c.H().aq_size > 0 && !c.H().error_code) {
         const uint64_t t_aq = prof_now();
         const QInfo q = aq_pop(c);
         K10S_PROF_ADD(c, PROF_AQPOP, t_aq);
         if (!pod_in_s(c, q.pod)) continue;   // removed from the cache (scheduler.rs:263-269)
+#if !K10S_DEVICE && defined(K10S_PRUNE_STUDY)
+        const int32_t placed =
+#endif
         cycle_attempt<PLUG>(c, t, q, K10S_PICK_SCAN, cycle_dur, fails);
+#if !K10S_DEVICE && defined(K10S_PRUNE_STUDY)
+        if (nc_packed(c)) k10s_prune_cycle_pick(c.V().pod(q.pod).req_cpu, c.V().pod(q.pod).req_ram, placed);
+#endif
     }
     cycle_end(c, cycle_dur, fails);
 }

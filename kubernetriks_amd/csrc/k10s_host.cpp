@@ -83,6 +83,7 @@ struct k10s_engine : EngineCore {
     std::vector<uint8_t> blob;
     k10s_capacities caps;
     std::vector<RunCall> history;
+    uint32_t regrows = 0;   // batches recompiled by regrow since create
 };
 
 // All engines of a device launch on one stream: the launch constants are one __constant__ block per
@@ -122,7 +123,15 @@ static void engine_free(k10s_engine* e) {
     delete e;
 }
 
+// A failed regrow that had to release the replaced batch's state leaves the engine without one.
+static int32_t live(const EngineCore& e) {
+    if (e.d_state) return K10S_OK;
+    return set_err(K10S_E_CAPACITY, "engine state was released by a regrow that then failed (device memory); "
+                                    "destroy the engine");
+}
+
 static int32_t core_init(EngineCore& e) {
+    if (int32_t rc = live(e)) return rc;
     HIPCHK(hipSetDevice(e.device));
     HIPCHK(hipMemsetAsync(e.d_active, 0, 8, e.stream));
     HIPCHK((e.wide ? k10s_launch_init_plugins : k10s_launch_init)(e.h_dc, e.R, e.stream));
@@ -133,9 +142,12 @@ static int32_t core_init(EngineCore& e) {
 // Compile the scenario and allocate + initialize the batch.  params: n_replicas entries, or NULL for
 // the scenario defaults.  Returns K10S_OK or an error code (message in g_err); on failure the core
 // holds nothing the caller must free beyond what core_free releases.
+// reclaim (a regrow only): the batch this one replaces.  When the new replica state does not fit
+// the free device memory beside reclaim's but fits in its place, reclaim's state is freed first
+// (reclaim->d_state becomes NULL: the caller's results are then lost if this create fails).
 static int32_t core_create(EngineCore& e, const char* text, const uint8_t* blob, uint64_t blob_len,
                            const k10s_replica_params* params, uint32_t n_replicas, const k10s_capacities& c,
-                           int32_t device) {
+                           int32_t device, EngineCore* reclaim = nullptr) {
     e.device = device;
     e.R = n_replicas;
     std::string err;
@@ -169,6 +181,9 @@ static int32_t core_create(EngineCore& e, const char* text, const uint8_t* blob,
     size_t bytes = (size_t)e.L.stride * n_replicas;
     size_t free_b = 0, total_b = 0;
     (void)hipMemGetInfo(&free_b, &total_b);
+    const size_t old_b = (reclaim && reclaim->d_state) ? (size_t)reclaim->L.stride * reclaim->R : 0;
+    const size_t here_b = free_b;   // free beside the batch being replaced
+    free_b += old_b;                // ... and in its place
     if (bytes + (64ull << 20) > free_b && c.delay_fifo == 0 && e.L.cap_fq > 512) {
         // the default rings grow with the node count (up to 8 x 8,192 x 32 B = 2 MiB per replica): when
         // that does not fit, fall back to 512-entry rings (a fuller ring only spills to the heap)
@@ -179,6 +194,10 @@ static int32_t core_create(EngineCore& e, const char* text, const uint8_t* blob,
     }
     if (bytes + (64ull << 20) > free_b)
         return set_err(K10S_E_CAPACITY, "replica state (" + std::to_string(bytes >> 20) + " MiB) exceeds free device memory");
+    if (old_b && bytes + (64ull << 20) > here_b) {   //  room only in the replaced batch's place
+        (void)hipFree(reclaim->d_state);
+        reclaim->d_state = nullptr;
+    }
     if (hipMalloc(&e.d_state, bytes) != hipSuccess) return set_err(K10S_E_HIP, "hipMalloc replica state");
     if (hipMalloc(&e.d_params, sizeof(Params) * n_replicas) != hipSuccess) return set_err(K10S_E_HIP, "hipMalloc params");
     if (hipMemcpy(e.d_params, e.params.data(), sizeof(Params) * n_replicas, hipMemcpyHostToDevice) != hipSuccess)
@@ -199,8 +218,9 @@ static int32_t core_create(EngineCore& e, const char* text, const uint8_t* blob,
 
 // One launch over every replica (no sync); h_active[0..1] receive the launch's flags when it is done.
 static int32_t core_launch(EngineCore& e, const RunCall& rc) {
+    if (int32_t r = live(e)) return r;
     HIPCHK(hipSetDevice(e.device));
-    HIPCHK(hipMemsetAsync(e.d_active, 0, 4, e.stream));   // word 1 (name bound) stays set until a regrow
+    HIPCHK(hipMemsetAsync(e.d_active, 0, 4, e.stream));   // word 1 (a growable stop) stays set until a regrow
     HIPCHK((e.wide ? k10s_launch_run_plugins : k10s_launch_run)(e.h_dc, e.R, rc.mode, rc.until_time, rc.max_time,
                                                                  rc.budget, e.d_active, e.stream));
     HIPCHK(hipMemcpyAsync(e.h_active, e.d_active, 8, hipMemcpyDeviceToHost, e.stream));
@@ -221,6 +241,7 @@ static int32_t core_call(EngineCore& e, const RunCall& rc) {
 // destination would be copied through a bounce buffer).  The caller holds e->hdr_mu across the fill
 // and its reads of h_hdr, so concurrent read-back calls on one engine do not interleave.
 static int32_t read_all_hdrs(EngineCore* e) {
+    if (int32_t rc = live(*e)) return rc;
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipMemcpy2DAsync(e->h_hdr, sizeof(RepHdr), e->d_state + e->L.hdr, e->L.stride, sizeof(RepHdr), e->R,
                             hipMemcpyDeviceToHost, e->stream));
@@ -228,58 +249,96 @@ static int32_t read_all_hdrs(EngineCore* e) {
     return K10S_OK;
 }
 
-// Generated names without a bound.  The reference names the HPA's pods "{group}_{total_created}"
+// Engine capacities the reference does not have.  The reference's containers grow without a bound:
+// the event queue (dslab-core's BinaryHeap), the active queue and the unschedulable map
+// (scheduler.rs:45, 49), and the generated names — the HPA's pods "{group}_{total_created}"
 // (kube_horizontal_pod_autoscaler.rs:178-182, api_server.rs:421) and the cluster autoscaler's nodes
-// "{group}_{k}" (kube_cluster_autoscaler.rs) with no limit; the engine ranks every name of the run
-// ahead of time (name rank = index), so it compiles a finite universe per group
-// (k10s_capacities.group_name_bound / ca_name_bound, derived from the scenario when 0) and a replica
-// that would create a name beyond it stops with K10S_ERR_NAME_BOUND.  The run kernel flags such a
-// stop (active word 1); this recompiles the batch with the exhausted universe doubled and replays
+// "{group}_{k}" (kube_cluster_autoscaler.rs).  The engine sizes each replica's state ahead of time
+// (name rank = index; k10s_capacities), and a replica that outgrows one of them stops
+// with K10S_ERR_HEAP_FULL, K10S_ERR_QUEUE_FULL or K10S_ERR_NAME_BOUND.  The run kernel flags such a
+// stop (active word 1); this recompiles the batch with every exhausted capacity doubled and replays
 // every call since the last initialize on it, until no replica stops there.  Every replica is
 // deterministic, so the others come out identical; the handle keeps its identity (name tables and
-// replica_bytes may grow).  A bound at K10S_NAME_BOUND_MAX is left as the error.
+// replica_bytes may grow).  A capacity at its maximum (2^20 names per universe, 2^30 heap or queue
+// entries) is left as the replica's error.
+// Memory: the regrown batch is allocated beside the current one when both fit, else in its place
+// (core_create's reclaim); if it fits neither way the engine keeps the stopped results and the run
+// returns K10S_E_CAPACITY.  K10S_ERR_CA_BUFFER is not regrown: its buffers are sized from the node
+// pool and the pod count (cap_act >= max(ca_max_node_count, N) + 16 actions per decision, cap_undo =
+// P + 16 moved pods), which no decision can exceed, so it marks a broken invariant, not a limit.
 #define K10S_NAME_BOUND_MAX (1u << 20)
+#define K10S_QUEUE_CAP_MAX (1u << 30)
+static uint32_t grow2(uint32_t cur, uint32_t floor_, uint32_t max_) {
+    return std::min<uint32_t>(2 * std::max<uint32_t>(cur, floor_), max_);
+}
 static int32_t regrow(k10s_engine* e) {
     for (;;) {
         if (e->h_active[1] == 0) return K10S_OK;
-        bool grow_ca = false, grow_group = false;
+        bool grow_ca = false, grow_group = false, grow_heap = false, grow_queue = false;
         {
             std::lock_guard<std::mutex> g(e->hdr_mu);
             int32_t rc = read_all_hdrs(e);
             if (rc != K10S_OK) return rc;
             for (uint32_t r = 0; r < e->R; r++) {
-                if (e->h_hdr[r].error_code != K10S_ERR_NAME_BOUND) continue;
-                if (e->h_hdr[r].error_kind == K10S_EV_PS_CA_REQ) grow_ca = true;
-                else grow_group = true;
+                const uint32_t code = e->h_hdr[r].error_code;
+                if (code == K10S_ERR_NAME_BOUND) {
+                    if (e->h_hdr[r].error_kind == K10S_EV_PS_CA_REQ) grow_ca = true;
+                    else grow_group = true;
+                } else if (code == K10S_ERR_HEAP_FULL) {
+                    grow_heap = true;
+                } else if (code == K10S_ERR_QUEUE_FULL) {
+                    grow_queue = true;
+                }
             }
         }
-        k10s_capacities c = e->caps;
+        k10s_capacities c = e->caps;   // the batch's effective capacities
         c.group_name_bound = e->hs.group_bound;
         c.ca_name_bound = e->hs.ca_bound;
+        c.event_heap = e->L.cap_heap;
+        c.active_queue = e->L.cap_aq;
+        c.unschedulable = e->L.cap_uq;
         bool grown = false;
         if (grow_group && c.group_name_bound < K10S_NAME_BOUND_MAX) {
-            c.group_name_bound = std::min<uint32_t>(2 * std::max<uint32_t>(c.group_name_bound, 32), K10S_NAME_BOUND_MAX);
+            c.group_name_bound = grow2(c.group_name_bound, 32, K10S_NAME_BOUND_MAX);
             grown = true;
         }
         if (grow_ca && c.ca_name_bound < K10S_NAME_BOUND_MAX) {
-            c.ca_name_bound = std::min<uint32_t>(2 * std::max<uint32_t>(c.ca_name_bound, 32), K10S_NAME_BOUND_MAX);
+            c.ca_name_bound = grow2(c.ca_name_bound, 32, K10S_NAME_BOUND_MAX);
             grown = true;
         }
-        if (!grown) {
+        if (grow_heap && c.event_heap < K10S_QUEUE_CAP_MAX) {
+            c.event_heap = grow2(c.event_heap, 64, K10S_QUEUE_CAP_MAX);
+            grown = true;
+        }
+        if (grow_queue && (c.active_queue < K10S_QUEUE_CAP_MAX || c.unschedulable < K10S_QUEUE_CAP_MAX)) {
+            c.active_queue = grow2(c.active_queue, 16, K10S_QUEUE_CAP_MAX);   // (which one filled is not
+            c.unschedulable = grow2(c.unschedulable, 16, K10S_QUEUE_CAP_MAX);  // recorded: both grow)
+            grown = true;
+        }
+        if (!grown) {   // every stop is at a maximum: they stay the replicas' errors
             e->h_active[1] = 0;
+            HIPCHK(hipSetDevice(e->device));
+            HIPCHK(hipMemsetAsync(e->d_active + 1, 0, 4, e->stream));
             return K10S_OK;
         }
         EngineCore n;
         int32_t rc = core_create(n, e->text.c_str(), e->blob.empty() ? nullptr : e->blob.data(), e->blob.size(),
-                                 e->params.data(), e->R, c, e->device);
+                                 e->params.data(), e->R, c, e->device, e);
         for (size_t i = 0; rc == K10S_OK && i < e->history.size(); i++) rc = core_call(n, e->history[i]);
         if (rc != K10S_OK) {
+            const std::string m = g_err;
             core_free(n);
-            return rc;
+            if (e->d_state) {   // the stopped batch is intact: keep its results readable
+                e->h_active[1] = 0;
+                (void)hipMemsetAsync(e->d_active + 1, 0, 4, e->stream);
+            }
+            return set_err(rc, "regrow: " + m);
         }
         std::lock_guard<std::mutex> g(e->hdr_mu);
         std::swap(static_cast<EngineCore&>(*e), n);
         core_free(n);
+        e->caps = c;
+        e->regrows += 1;
     }
 }
 
@@ -535,6 +594,7 @@ uint32_t k10s_engine_profile_width(void) { return K10S_PROF_SLOTS; }
 
 static int32_t read_hdr(const k10s_engine* e, uint32_t r, RepHdr& h) {
     if (r >= e->R) return set_err(K10S_E_INVALID, "replica index out of range");
+    if (int32_t rc = live(*e)) return rc;
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipMemcpy(&h, e->d_state + (size_t)r * e->L.stride + e->L.hdr, sizeof h, hipMemcpyDeviceToHost));
     return K10S_OK;
@@ -579,6 +639,7 @@ int32_t k10s_engine_placements(const k10s_engine* e, uint32_t r, k10s_placement*
 int32_t k10s_engine_pod_records(const k10s_engine* e, uint32_t r, k10s_pod_record* out, uint32_t cap, uint32_t* n) {
     if (!e || !n) return set_err(K10S_E_INVALID, "null");
     if (r >= e->R) return set_err(K10S_E_INVALID, "replica index out of range");
+    if (int32_t rc = live(*e)) return rc;
     uint32_t k = e->L.rec_on ? (e->hs.n_pods < cap ? e->hs.n_pods : cap) : 0;
     HIPCHK(hipSetDevice(e->device));
     if (k) HIPCHK(hipMemcpy(out, e->d_state + (size_t)r * e->L.stride + e->L.prec, sizeof(k10s_pod_record) * k,
@@ -591,6 +652,7 @@ int32_t k10s_engine_group_sizes(const k10s_engine* e, uint32_t r, uint32_t* crea
                                 uint32_t* n) {
     if (!e || !n) return set_err(K10S_E_INVALID, "null");
     if (r >= e->R) return set_err(K10S_E_INVALID, "replica index out of range");
+    if (int32_t rc = live(*e)) return rc;
     uint32_t G = (uint32_t)e->hs.group_names.size();
     uint32_t k = G < cap ? G : cap;
     std::vector<GroupState> gs(G);
@@ -625,5 +687,17 @@ int32_t k10s_engine_name_bounds(const k10s_engine* e, uint32_t* group_bound, uin
     return K10S_OK;
 }
 uint32_t k10s_engine_node_entry_bytes(const k10s_engine* e) { return e ? (e->L.packed ? 8u : 12u) : 0u; }
+int32_t k10s_engine_capacities(const k10s_engine* e, k10s_capacities* out, uint32_t* regrows) {
+    if (!e || !out) return set_err(K10S_E_INVALID, "null");
+    *out = e->caps;
+    out->event_heap = e->L.cap_heap;
+    out->active_queue = e->L.cap_aq;
+    out->unschedulable = e->L.cap_uq;
+    out->group_name_bound = e->hs.group_bound;
+    out->ca_name_bound = e->hs.ca_bound;
+    out->delay_fifo = e->L.cap_fq ? e->L.cap_fq : K10S_FIFO_OFF;
+    if (regrows) *regrows = e->regrows;
+    return K10S_OK;
+}
 
 }  // extern "C"

@@ -123,9 +123,13 @@ __global__ K10S_RUN_BOUNDS void k10s_run_kernel(uint32_t n_replicas, int mode, d
     (void)active;   // the same pointer, read after the loop through the constant block
 #if K10S_DEVICE
     if (more && threadIdx.x == 0) atomicAdd(K10S_DC.active, 1u);
-    // a replica stopped at a generated-name bound: the host recompiles the batch with a larger
-    // universe and replays it (k10s_host.cpp regrow)
-    if (threadIdx.x == 0 && k10s_hdr.error_code == K10S_ERR_NAME_BOUND) K10S_DC.active[1] = 1u;
+    // a replica stopped at a capacity the reference does not have (a generated-name universe, the
+    // event heap, the scheduler queues): the host recompiles the batch with it doubled and replays it
+    // (k10s_host.cpp regrow)
+    if (threadIdx.x == 0) {
+        const uint32_t ec = k10s_hdr.error_code;
+        if (ec == K10S_ERR_NAME_BOUND || ec == K10S_ERR_HEAP_FULL || ec == K10S_ERR_QUEUE_FULL) K10S_DC.active[1] = 1u;
+    }
 #endif
 }
 

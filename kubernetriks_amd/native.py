@@ -145,10 +145,11 @@ def _decl(L, prefix: str):
         "node_entry_bytes": (u32, [vp]),
         "default_params": (i32, [vp, P(ReplicaParams)]),
         "name_bounds": (i32, [vp, P(u32), P(u32)]),
+        "capacities": (i32, [vp, P(Capacities), P(u32)]),
     }
     out = {}
     for name, (res, args) in sig.items():
-        if name in ("node_entry_bytes", "name_bounds") and not hasattr(L, prefix + name):
+        if name in ("node_entry_bytes", "name_bounds", "capacities") and not hasattr(L, prefix + name):
             continue   # a library from an earlier round (A/B tooling)
         f = getattr(L, prefix + name)
         f.restype = res
@@ -185,6 +186,15 @@ class EngineBase:
         g, c = ctypes.c_uint32(), ctypes.c_uint32()
         self._check(self._fn["name_bounds"](self._h, ctypes.byref(g), ctypes.byref(c)))
         return int(g.value), int(c.value)
+
+    @property
+    def capacities(self):
+        """(effective capacities as a dict, regrows since create): event_heap, active_queue,
+        unschedulable, the name bounds and delay_fifo as compiled, after any regrow
+        (include/k10s.h k10s_engine_capacities)."""
+        c, n = Capacities(), ctypes.c_uint32()
+        self._check(self._fn["capacities"](self._h, ctypes.byref(c), ctypes.byref(n)))
+        return {f: int(getattr(c, f)) for f, _ in Capacities._fields_}, int(n.value)
 
     @property
     def node_names(self) -> List[str]:

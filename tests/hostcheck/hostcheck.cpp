@@ -34,6 +34,7 @@ struct HC {
         uint64_t budget;
     };
     std::vector<Call> history;
+    uint32_t regrows = 0;
 };
 
 // The engine's working header is a separate copy during a run, like the LDS staging of the device
@@ -133,27 +134,46 @@ int hc_run(void* p, int mode, double until, double max_time, uint64_t budget) {
     const HC::Call k{mode, until, max_time, budget};
     h->history.push_back(k);
     hc_call(h, k);
-    // name-bound regrow (k10s_host.cpp regrow): recompile with the exhausted universe doubled and
-    // replay every call, until no replica stops at K10S_ERR_NAME_BOUND
+    // capacity regrow (k10s_host.cpp regrow): recompile with every exhausted capacity doubled (a
+    // generated-name universe, the event heap, the scheduler queues) and replay every call, until no
+    // replica stops at K10S_ERR_NAME_BOUND / HEAP_FULL / QUEUE_FULL below its maximum
     for (;;) {
-        bool grow_ca = false, grow_group = false;
+        bool grow_ca = false, grow_group = false, grow_heap = false, grow_queue = false;
         for (uint32_t r = 0; r < h->R; r++) {
             const RepHdr& H = *make_rep(h->state.data(), h->L, r).h();
-            if (H.error_code != K10S_ERR_NAME_BOUND) continue;
-            if (H.error_kind == K10S_EV_PS_CA_REQ) grow_ca = true;
-            else grow_group = true;
+            if (H.error_code == K10S_ERR_NAME_BOUND) {
+                if (H.error_kind == K10S_EV_PS_CA_REQ) grow_ca = true;
+                else grow_group = true;
+            } else if (H.error_code == K10S_ERR_HEAP_FULL) {
+                grow_heap = true;
+            } else if (H.error_code == K10S_ERR_QUEUE_FULL) {
+                grow_queue = true;
+            }
         }
         k10s_capacities c = h->caps;
         c.group_name_bound = h->hs.group_bound;
         c.ca_name_bound = h->hs.ca_bound;
-        const uint32_t MAXB = 1u << 20;
+        c.event_heap = h->L.cap_heap;
+        c.active_queue = h->L.cap_aq;
+        c.unschedulable = h->L.cap_uq;
+        const uint32_t MAXB = 1u << 20, MAXQ = 1u << 30;
+        auto grow2 = [](uint32_t cur, uint32_t fl, uint32_t mx) { return std::min<uint32_t>(2 * std::max<uint32_t>(cur, fl), mx); };
         bool grown = false;
         if (grow_group && c.group_name_bound < MAXB) {
-            c.group_name_bound = std::min<uint32_t>(2 * std::max<uint32_t>(c.group_name_bound, 32), MAXB);
+            c.group_name_bound = grow2(c.group_name_bound, 32, MAXB);
             grown = true;
         }
         if (grow_ca && c.ca_name_bound < MAXB) {
-            c.ca_name_bound = std::min<uint32_t>(2 * std::max<uint32_t>(c.ca_name_bound, 32), MAXB);
+            c.ca_name_bound = grow2(c.ca_name_bound, 32, MAXB);
+            grown = true;
+        }
+        if (grow_heap && c.event_heap < MAXQ) {
+            c.event_heap = grow2(c.event_heap, 64, MAXQ);
+            grown = true;
+        }
+        if (grow_queue && (c.active_queue < MAXQ || c.unschedulable < MAXQ)) {
+            c.active_queue = grow2(c.active_queue, 16, MAXQ);
+            c.unschedulable = grow2(c.unschedulable, 16, MAXQ);
             grown = true;
         }
         if (!grown) return 0;
@@ -161,12 +181,24 @@ int hc_run(void* p, int mode, double until, double max_time, uint64_t budget) {
         HC* n = hc_compile(h->text.c_str(), h->blob.empty() ? nullptr : h->blob.data(), h->blob.size(),
                            h->params.data(), h->R, c, e);
         if (!n) return -1;
-        n->caps = h->caps;   // the caller's capacities; the bounds live in hs
         n->history = h->history;
+        n->regrows = h->regrows + 1;
         for (const HC::Call& x : n->history) hc_call(n, x);
         std::swap(*h, *n);
         delete n;
     }
+}
+int hc_capacities(void* p, k10s_capacities* out, uint32_t* regrows) {
+    HC* h = (HC*)p;
+    *out = h->caps;
+    out->event_heap = h->L.cap_heap;
+    out->active_queue = h->L.cap_aq;
+    out->unschedulable = h->L.cap_uq;
+    out->group_name_bound = h->hs.group_bound;
+    out->ca_name_bound = h->hs.ca_bound;
+    out->delay_fifo = h->L.cap_fq ? h->L.cap_fq : K10S_FIFO_OFF;
+    if (regrows) *regrows = h->regrows;
+    return 0;
 }
 int hc_name_bounds(void* p, uint32_t* group_bound, uint32_t* ca_bound) {
     HC* h = (HC*)p;

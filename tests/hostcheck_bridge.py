@@ -70,7 +70,7 @@ class HostEngine(EngineBase):
     def run(self, mode=RUN_UNTIL_ALL_FINISHED, until_time=0.0, max_time=1e12, max_events_per_launch=0):
         self._forget_names()
         if self._L.hc_run(self._h, mode, until_time, max_time, max_events_per_launch) != 0:
-            raise RuntimeError("hostcheck: name-bound regrow failed to recompile the scenario")
+            raise RuntimeError("hostcheck: capacity regrow failed to recompile the scenario")
         return 0.0
 
     def run_until_all_finished(self, max_time: float = 1e12, max_events_per_launch: int = 0):

@@ -72,6 +72,11 @@ def test_variant_build_matches_product(product_rows, variant):
         pytest.fail(f"{lib} not built (__graft_entry__.build() builds it)")
     got = _run(lib)
     assert got["engine"] != product_rows["engine"]
+    # the library is the variant of THESE sources, not a stale one from an earlier build
+    from kubernetriks_amd.build import build_id
+    import __graft_entry__ as ge
+    extra = [x for x, out in ge.VARIANT_BUILDS if lib.endswith(out)][0]
+    assert got["engine"].endswith("build " + build_id(extra)), (got["engine"], build_id(extra))
     for r, (a, b) in enumerate(zip(got["rows"], product_rows["rows"])):
         assert a == b, (variant, r, a, b)
     assert sum(x["counters"][14] for x in got["rows"]) == sum(x["counters"][14] for x in product_rows["rows"])
