@@ -16,7 +16,8 @@ for i, f in enumerate(files):
     r = d["roofline"]
     row = {"file": f"{tag}/{os.path.basename(f)}", "label": labels[i] if i < len(labels) else "",
            "engine": d["engine"][-12:], "c3_kernel_ms": round(r["kernel_ms_per_launch"], 2), "c3_frac": round(r["frac"], 4),
-           "c3_placements_per_s": round(d["value"])}
+           "c3_placements_per_s": round(d["value"]),
+           "c3_nodes_read_per_placement": round(d["totals"]["nodes_read"] / max(d["totals"]["placements"], 1), 1)}
     bl = d.get("backlog")
     if bl:
         tot = bl["totals"]
