@@ -1932,13 +1932,37 @@ static_assert(K10S_TILE >= 1 && K10S_TILE <= 32, "K10S_TILE");
 // Bit j set: pod j of the tile (need bit j: request rc8[j] = cpu << 8, rr[j] = ram, both > 0 and cpu
 // < 2^24) fits some node of the packed cache (cpu field >= cpu, ram field >= ram).  Absent nodes hold
 // (0, 0) and fit nothing.  *nread: cache entries read.
+// bnd (not NULL, block size 2^sh with 6 <= sh <= 8): the pass reads the whole cache and leaves each
+// block's bound in bnd[b] (tile_scan_pruned below).
+#if K10S_DEVICE
+template <int S>
+K10S_D void bmax_step(uint32_t& c, uint64_t& r) {
+    uint32_t a, b, la, lb, ha, hb;
+    xpair<S>(c, a, b);
+    c = a > b ? a : b;
+    xpair<S>((uint32_t)r, la, lb);
+    xpair<S>((uint32_t)(r >> 32), ha, hb);
+    const uint64_t ra = join64(la, ha), rb = join64(lb, hb);
+    r = ra > rb ? ra : rb;
+}
+// (cpu, ram) maxima over the 2^(sh-2) lanes of a block (every lane of the group gets them)
+K10S_D void block_max(uint32_t& c, uint64_t& r, uint32_t sh) {
+    bmax_step<0>(c, r);
+    bmax_step<1>(c, r);
+    bmax_step<2>(c, r);
+    bmax_step<3>(c, r);
+    if (sh >= 7) bmax_step<4>(c, r);
+    if (sh >= 8) bmax_step<5>(c, r);
+}
+#endif
 K10S_HD uint32_t fit_tile(const uint64_t* s_node, uint32_t n_nodes, const uint32_t* rc8, const uint64_t* rr,
-                          uint32_t need, uint32_t* nread) {
+                          uint32_t need, uint32_t* nread, uint64_t* bnd = nullptr, uint32_t sh = 6) {
     uint32_t found = 0;
 #if K10S_DEVICE
     const uint32_t l4 = 4u * (uint32_t)lane_id();
+    const bool wb = bnd != nullptr;   // wave-uniform
     uint32_t base = 0;
-    for (; base < n_nodes && (found & need) != need; base += 512) {
+    for (; base < n_nodes && (wb || (found & need) != need); base += 512) {
         // a lane's 8 nodes of this 512-node block (past the end: entries 0..3 re-read, then zeroed)
         const uint32_t a0 = base + l4, a1 = base + 256u + l4;
         const uint32_t b0 = a0 < n_nodes ? a0 : 0u, b1 = a1 < n_nodes ? a1 : 0u;
@@ -1969,18 +1993,177 @@ K10S_HD uint32_t fit_tile(const uint64_t* s_node, uint32_t n_nodes, const uint32
             for (int k = 0; k < 8; k++) f |= hi[k] >= rc8[j] && ram[k] >= rr[j];
             if (__ballot(f)) found |= 1u << j;
         }
+        if (wb) {   // the blocks' (cpu, ram) maxima: lane-local over 4 entries, then over the block's lanes
+            uint32_t ca = 0, cb = 0;
+            uint64_t ra = 0, rb = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                ca = (hi[k] >> 8) > ca ? (hi[k] >> 8) : ca;
+                ra = ram[k] > ra ? ram[k] : ra;
+                cb = (hi[k + 4] >> 8) > cb ? (hi[k + 4] >> 8) : cb;
+                rb = ram[k + 4] > rb ? ram[k + 4] : rb;
+            }
+            block_max(ca, ra, sh);
+            block_max(cb, rb, sh);
+            if ((l4 & ((4u << (sh - 2)) - 1u)) == 0) {   // the block's first lane writes its bound
+                if (a0 < n_nodes) bnd[a0 >> sh] = nc_pack(ca, ra);
+                if (a1 < n_nodes) bnd[a1 >> sh] = nc_pack(cb, rb);
+            }
+        }
     }
     *nread = base < n_nodes ? base : n_nodes;
 #else
     uint32_t n = 0;
-    for (; n < n_nodes && (found & need) != need; n++) {
+    if (bnd)
+        for (uint32_t b = 0; (b << sh) < n_nodes; b++) bnd[b] = 0;
+    for (; n < n_nodes && (bnd || (found & need) != need); n++) {
         const uint64_t x = s_node[n];
         for (int j = 0; j < K10S_TILE; j++)
             if ((need >> j & 1u) && (uint32_t)(x >> 32) >= rc8[j] && (x & K10S_PK_RAM) >= rr[j]) found |= 1u << j;
+        if (bnd) {
+            const NcEnt v = nc_unpack(x), b = nc_unpack(bnd[n >> sh]);
+            bnd[n >> sh] = nc_pack(v.cpu > b.cpu ? v.cpu : b.cpu, v.ram > b.ram ? v.ram : b.ram);
+        }
     }
     *nread = n;
 #endif
     return found;
+}
+
+// ---- pruned scans inside a cycle tile (round 6) ---------------------------------------------------
+// The tile's fit pass (fit_tile with bnd) reads the whole packed cache and leaves, per block of 2^sh
+// consecutive nodes (the layout's nblocks <= 64 blocks, 6 <= sh <= 8), the componentwise maximum
+// (cpu, ram) of the block's entries.  Until the tile ends the cycle changes the cache only by
+// reserve_node_resources (scheduler.rs:118-123), which lowers an entry, so each bound stays >= every
+// entry of its block.  A fitting pod of the tile then scans blocks best bound first and stops when
+// no unvisited block can hold the argmax: with rc, rr > 0 (no 0/0), the LeastAllocated score is
+// monotone in (cpu, ram) (schedule_scan_pruned's argument: correctly rounded quotients of exactly
+// represented integers), so a node's score is <= its block bound's, and a block whose bound score is
+// below the best found — or equal with every index below the best node (the last maximum in name
+// order wins, kube_scheduler.rs:140-148) — is skipped.  A bound that fits no request means no node of
+// the block fits.  Measured on the host (tools/prune_study.py, 64-node blocks with tight bounds): the
+// backlog's fitting pods visit 1.02 blocks per scan (129 of 4,096 entries); C3's light regime 47
+// blocks (74 %), which is why the serial cycle (C3) keeps the screened full scan.  More than
+// K10S_TILE_PRUNE_MAX visited blocks fall back to the full scan (same result).  A visited block's bound
+// is tightened to its entries' maxima (the scan reads them all), so a block that an earlier pod of
+// the tile reserved on is not left looking better than it is.
+#ifndef K10S_TILE_PRUNE
+#define K10S_TILE_PRUNE 1
+#endif
+#ifndef K10S_TILE_PRUNE_MAX
+#define K10S_TILE_PRUNE_MAX 6
+#endif
+// Returns K10S_SCHED_OK / NO_SUFFICIENT_RESOURCES, or -1 (fall back to the full scan).  *nread:
+// entries read (bounds + visited blocks).  Preconditions: weight 1.0, rc > 0, rr > 0, both within
+// the packed fields.
+K10S_HD_NOINL int tile_scan_pruned(const uint64_t* s_node, uint64_t* bnd, uint32_t N, uint32_t sh, uint32_t rc,
+                             uint64_t rr, int32_t* chosen, uint32_t* nread) {
+    const uint32_t NB = (N + (1u << sh) - 1u) >> sh;
+    uint32_t reads = NB, visits = 0;
+    uint64_t best_key = 0;
+    int32_t best_n = -1;
+#if K10S_DEVICE
+    const uint32_t lane = (uint32_t)lane_id();
+    rc = uniform_u32(rc);
+    rr = uniform_u64(rr);
+    const double frc = uniform_f64((double)rc), frr = uniform_f64(u64_f64(rr));
+    uint64_t bkey = 0;   // lane b: block b's bound score key (0: nothing in the block fits)
+    if (lane < NB) {
+        const NcEnt v = nc_unpack(bnd[lane]);
+        if (rc <= v.cpu && rr <= v.ram) bkey = score_key(la_exact(v.cpu, v.ram, rr, frc, frr));
+    }
+    for (;;) {
+        const int32_t last = (int32_t)(((lane + 1u) << sh) - 1u);   // block's largest index
+        const bool alive = bkey != 0 && (best_n < 0 || bkey > best_key || (bkey == best_key && last > best_n));
+        uint64_t k = alive ? bkey : 0;
+        int32_t bi = alive ? (int32_t)lane : -1;
+        wave_argmax(k, bi);
+        bi = (int32_t)uniform_u32((uint32_t)bi);
+        if (bi < 0) break;
+        if (visits == K10S_TILE_PRUNE_MAX) {
+            *nread = reads;
+            return -1;
+        }
+        visits++;
+        const uint32_t lo = (uint32_t)bi << sh, hi = (lo + (1u << sh)) < N ? (lo + (1u << sh)) : N;
+        uint64_t lk = 0;
+        int32_t ln = -1;
+        uint32_t mc = 0;   // the block's (cpu, ram) maxima: its bound, tightened (reservations earlier in
+        uint64_t mr = 0;   // the tile left it above the entries)
+        for (uint32_t m = lo; m < hi; m += 64) {   // lane i: nodes lo + i, lo + 64 + i, ... (ascending)
+            const uint32_t n = m + lane;
+            if (n < hi) {
+                const NcEnt v = nc_unpack(s_node[n]);
+                mc = v.cpu > mc ? v.cpu : mc;
+                mr = v.ram > mr ? v.ram : mr;
+                if (rc <= v.cpu && rr <= v.ram) {
+                    const uint64_t kk = score_key(la_exact(v.cpu, v.ram, rr, frc, frr));
+                    if (kk >= lk) {
+                        lk = kk;
+                        ln = (int32_t)n;
+                    }
+                }
+            }
+        }
+        reads += hi - lo;
+        block_max(mc, mr, 8);
+        if (lane == 0) bnd[bi] = nc_pack(mc, mr);
+        wave_argmax(lk, ln);
+        lk = uniform_u64(lk);
+        ln = (int32_t)uniform_u32((uint32_t)ln);
+        if (ln >= 0 && (lk > best_key || (lk == best_key && ln > best_n))) {
+            best_key = lk;
+            best_n = ln;
+        }
+        if (lane == (uint32_t)bi) bkey = 0;
+    }
+#else
+    uint64_t keys[64];
+    for (uint32_t b = 0; b < NB; b++) {
+        const NcEnt v = nc_unpack(bnd[b]);
+        keys[b] = (rc <= v.cpu && rr <= v.ram) ? score_key(la_score(v.cpu, v.ram, rc, rr)) : 0;
+    }
+    for (;;) {
+        int32_t bi = -1;
+        uint64_t k = 0;
+        for (uint32_t b = 0; b < NB; b++) {
+            const int32_t last = (int32_t)(((b + 1u) << sh) - 1u);
+            const bool alive = keys[b] != 0 && (best_n < 0 || keys[b] > best_key || (keys[b] == best_key && last > best_n));
+            if (alive && keys[b] >= k) {   // (key, block) maximum: the device's wave_argmax
+                k = keys[b];
+                bi = (int32_t)b;
+            }
+        }
+        if (bi < 0) break;
+        if (visits == K10S_TILE_PRUNE_MAX) {
+            *nread = reads;
+            return -1;
+        }
+        visits++;
+        const uint32_t lo = (uint32_t)bi << sh, hi = (lo + (1u << sh)) < N ? (lo + (1u << sh)) : N;
+        uint32_t mc = 0;
+        uint64_t mr = 0;
+        for (uint32_t n = lo; n < hi; n++) {
+            const NcEnt v = nc_unpack(s_node[n]);
+            mc = v.cpu > mc ? v.cpu : mc;
+            mr = v.ram > mr ? v.ram : mr;
+            if (rc <= v.cpu && rr <= v.ram) {
+                const uint64_t kk = score_key(la_score(v.cpu, v.ram, rc, rr));
+                if (kk > best_key || (kk == best_key && (int32_t)n > best_n)) {
+                    best_key = kk;
+                    best_n = (int32_t)n;
+                }
+            }
+        }
+        reads += hi - lo;
+        bnd[bi] = nc_pack(mc, mr);
+        keys[bi] = 0;
+    }
+#endif
+    *nread = reads;
+    if (best_n < 0) return K10S_SCHED_NO_SUFFICIENT_RESOURCES;
+    *chosen = best_n;
+    return K10S_SCHED_OK;
 }
 
 // ---- best-node pass of a cycle tile (exact picks for the pods that fit) --------------------------
@@ -2336,7 +2519,8 @@ inline void k10s_prune_cycle_pick(uint32_t rc, uint64_t rr, int32_t pick) {
 #endif
 #define K10S_PICK_SCAN (-1)
 #define K10S_PICK_NOFIT (-2)
-template <bool PLUG>
+#define K10S_PICK_PRUNED (-3)   // the tile's block bounds are valid: tile_scan_pruned (TILE builds only)
+template <bool PLUG, bool TILE = false>
 K10S_HD int32_t cycle_attempt(Ctx& c, double t, QInfo q, int32_t pick, double& cycle_dur, uint32_t& fails) {
     RepHdr* h = &c.H();
     const double w = c.P().score_weight;
@@ -2364,6 +2548,10 @@ K10S_HD int32_t cycle_attempt(Ctx& c, double t, QInfo q, int32_t pick, double& c
         } else if (pick >= 0) {
             st = K10S_SCHED_OK;
             chosen = pick;
+        } else if (TILE && pick == K10S_PICK_PRUNED) {
+            uint32_t pr = 0;
+            st = tile_scan_pruned(c.V().s_node(), c.V().s_bram(), c.S().n_nodes, c.Ly().bshift, rc, rr, &chosen, &pr);
+            nread = pr;
         } else if (PLUG) {
             st = schedule_scan_plugins(c, rc, rr, &chosen);
             nread = c.S().n_nodes;
@@ -2380,7 +2568,7 @@ K10S_HD int32_t cycle_attempt(Ctx& c, double t, QInfo q, int32_t pick, double& c
             else
                 st = schedule_scan<true, false>(c.V().s_cpu(), c.V().s_ram(), c.V().s_present(), c.S().n_nodes, rc, rr,
                                                 w, &chosen);
-            nread = c.S().n_nodes;
+            nread += c.S().n_nodes;   // (after a pruned scan that gave up: its reads too)
         }
         h->counters[K10S_C_NODES_READ] += nread;
         K10S_PROF_ADD(c, PROF_SCAN, t_scan);
@@ -2532,10 +2720,13 @@ K10S_HD_NOINL void run_scheduling_cycle_tiles(Ctx& c, double t) {
             K10S_PROF_ADD(c, PROF_SCAN, t_fit);
         }
 #else
+        // block bounds for the pods that fit (tile_scan_pruned): blocks of 64..256 nodes
+        const uint32_t bsh = c.Ly().bshift;
+        const bool bounds = K10S_TILE_PRUNE && bsh <= 8;
         if (need && h->s_node_count > 0) {
             uint32_t nread = 0;
             const uint64_t t_fit = prof_now();
-            found = fit_tile(s_node, N, rc8, rrq, need, &nread);
+            found = fit_tile(s_node, N, rc8, rrq, need, &nread, bounds ? c.V().s_bram() : nullptr, bsh);
             h->counters[K10S_C_NODES_READ] += nread;
             K10S_PROF_ADD(c, PROF_SCAN, t_fit);
         }
@@ -2551,6 +2742,9 @@ K10S_HD_NOINL void run_scheduling_cycle_tiles(Ctx& c, double t) {
             u.attempts = uniform_u32(q.attempts);
             u.pod = uniform_u32(q.pod);
             int32_t pick = (nofit >> j) & 1u ? K10S_PICK_NOFIT : K10S_PICK_SCAN;
+#if !K10S_TILE_BEST
+            if (bounds && ((need & found) >> j & 1u)) pick = K10S_PICK_PRUNED;
+#endif
 #if K10S_TILE_BEST
             if ((found >> j) & 1u) {   // fits some node of the snapshot: resolve from the lane values
                 const uint64_t t_pick = prof_now();
@@ -2602,7 +2796,7 @@ K10S_HD_NOINL void run_scheduling_cycle_tiles(Ctx& c, double t) {
 #endif
             // every assignment of the tile marks its lane (a pod outside need, e.g. one zero
             // request, is placed by the scan and changes the cache too)
-            const int32_t placed = cycle_attempt<false>(c, t, u, pick, cycle_dur, fails);
+            const int32_t placed = cycle_attempt<false, true>(c, t, u, pick, cycle_dur, fails);
             if (placed >= 0) rlanes |= 1ull << (((uint32_t)placed >> 2) & 63u);
         }
     }

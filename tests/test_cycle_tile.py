@@ -44,7 +44,8 @@ def _engine(backend):
 
 def backlog_scenario(seed: int, n_nodes: int = 24, n_pods: int = 300, identical: bool = False, cond_move: bool = False,
                      cycle: float = 10.0, removals: bool = False, weight: float = 1.0, zero_every: int = 0,
-                     huge_every: int = 0, pod_removals: bool = False, bursts: bool = True, half_zero_every: int = 0) -> str:
+                     huge_every: int = 0, pod_removals: bool = False, bursts: bool = True, half_zero_every: int = 0,
+                     tiny_every: int = 0) -> str:
     rng = random.Random(seed)
     cfg = SimulationConfig()
     cfg.enable_unscheduled_pods_conditional_move = cond_move
@@ -54,6 +55,8 @@ def backlog_scenario(seed: int, n_nodes: int = 24, n_pods: int = 300, identical:
     for k in range(n_nodes):
         cpu = 8000 if identical else rng.choice([4000, 8000, 16000])
         ram = 32 * GIB if identical else rng.choice([16, 32, 64]) * GIB
+        if tiny_every and k % tiny_every:   # most nodes hold no pod: a large cache that saturates early
+            cpu, ram = 100, GIB // 4
         c.create_node(0.0, Node(f"node_{k:03d}", cpu, ram))
     if removals:   # half the nodes leave mid-run, a quarter come back under the same names
         for k in range(0, n_nodes, 2):
@@ -99,6 +102,11 @@ CASES = {
     "identical_cond_move_many": dict(seed=16, n_nodes=260, n_pods=1500, identical=True, cond_move=True),
     "one_zero_request": dict(seed=17, n_nodes=40, n_pods=600, half_zero_every=3),
     "one_zero_request_identical": dict(seed=18, n_nodes=300, n_pods=2000, identical=True, half_zero_every=5),
+    # round 6: the fitting pods' pruned scans over the fit pass's block bounds, with 64-, 128- and
+    # 256-node blocks (the bound reductions span 16, 32 and 64 lanes), ties across blocks
+    "pruned_blocks_128": dict(seed=19, n_nodes=5000, n_pods=1500, cycle=5.0, tiny_every=25),
+    "pruned_blocks_128_identical": dict(seed=20, n_nodes=4500, n_pods=1500, identical=True, tiny_every=20),
+    "pruned_blocks_256": dict(seed=23, n_nodes=9000, n_pods=1500, removals=True, tiny_every=40),
 }
 
 
@@ -154,8 +162,46 @@ def test_tile_best_variant_host():
         env = dict(os.environ, K10S_HOSTCHECK_LIB=out, K10S_TILE_BEST_VARIANT="1")
         r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-n", "4", "-m", "not gpu", "-p", "no:cacheprovider",
                             os.path.join(repo, "tests", "test_cycle_tile.py"), os.path.join(repo, "tests", "test_engine_parity.py"),
-                            "-k", "(cycle_tiles_match_oracle or fuzz_host or tiles_replace or place_without) and not variant"],
+                            "-k", "(cycle_tiles_match_oracle or fuzz_host or tiles_replace or place_without) and not variant "
+                                  "and not pruned_blocks"],
                            env=env, cwd=repo, capture_output=True, text=True, timeout=1200)
         assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    finally:
+        os.unlink(out)
+
+
+def test_tile_pruned_scans_read_less_host():
+    """Round 6: a tile's pods that fit scan the blocks whose bound can still win (tile_scan_pruned)
+    instead of the whole cache.  The host build without it (K10S_TILE_PRUNE=0) gives the same results
+    and reads more node-cache entries."""
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hc = os.path.join(repo, "tests", "hostcheck")
+    out = os.path.join(repo, "build", f"libk10s_hostcheck_noprune_{os.getpid()}.so")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-ffp-contract=off", "-w", "-DK10S_TILE_PRUNE=0",
+                           "-shared", "-o", out, os.path.join(hc, "hostcheck.cpp"),
+                           os.path.join(repo, "kubernetriks_amd", "csrc", "k10s_builder.cpp")])
+    try:
+        import ctypes
+        import hostcheck_bridge as hb
+        scn = backlog_scenario(24, n_nodes=700, n_pods=3000)
+        a = HostEngine(scn, 1)
+        a.run_until_all_finished(1e6)
+        L = ctypes.CDLL(out)
+        saved = hb._lib, hb.LIB_PATH
+        try:
+            hb._lib, hb.LIB_PATH = None, out
+            os.environ["K10S_HOSTCHECK_LIB"] = out
+            b = HostEngine(scn, 1)
+            b.run_until_all_finished(1e6)
+            ra, rb = a.results()[0], b.results()[0]
+        finally:
+            hb._lib, hb.LIB_PATH = saved
+            os.environ.pop("K10S_HOSTCHECK_LIB", None)
+        del L
+        ka, kb = dict(ra["counters"]), dict(rb["counters"])
+        na, nb = ka.pop("nodes_read"), kb.pop("nodes_read")
+        assert ka == kb and parity.feq(ra["time"], rb["time"])
+        assert na < 0.95 * nb, (na, nb)
     finally:
         os.unlink(out)
