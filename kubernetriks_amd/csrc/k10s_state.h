@@ -265,6 +265,9 @@ struct RepHdr {
                                   // 0, every PodStartedRunning finds its pod in storage (below)
     uint32_t cyc_fails;           // attempts of the previous scheduling cycle that found no node: the cycle
                                   // runs the batched fit pass (k10s_engine.h fit_tile) only after one
+    uint32_t aq_sorted;           // the action queue is in sorted mode (k10s_engine.h aq_push): positions
+    uint32_t aq_head;             // [aq_head, aq_head + aq_size) hold it in strictly ascending timestamp
+    int64_t aq_last;              // order; aq_last = the newest entry's key (total_key)
     HeapEv fq_win[K10S_NFQ * K10S_FQW];
     HeapEv heap_lds[K10S_HEAP_TOP];
 #if K10S_AQ_TOP

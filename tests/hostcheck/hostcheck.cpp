@@ -288,6 +288,15 @@ extern "C" int hc_debug_queues(void* p, uint32_t r, double* aq, uint32_t* aq_pod
     return 0;
 }
 
+// The action queue's mode (k10s_engine.h aq_push: 1 = sorted) and length, for tests/test_action_queue.py.
+extern "C" int hc_aq_mode(void* p, uint32_t r, uint32_t* sorted, uint32_t* n) {
+    HC* h = (HC*)p;
+    Rep v = make_rep(h->state.data(), h->L, r);
+    *sorted = v.h()->aq_sorted;
+    *n = v.h()->aq_size;
+    return 0;
+}
+
 // The host score (bit-identical to the device's), for tests/test_scan_adversarial.py.
 extern "C" double hc_la_score(uint32_t ac, uint64_t ar, uint32_t rc, uint64_t rr) { return la_score(ac, ar, rc, rr); }
 // The event loop's screened scan test (k10s_engine.h scan_screen, operands formed as

@@ -26,7 +26,7 @@ def _engine(backend):
     return Engine
 
 
-def queue_scenario(seed, n_pods, per_cycle, ties=0.0, cycle=10.0, n_nodes=48, move_all=False):
+def queue_scenario(seed, n_pods, per_cycle, ties=0.0, cycle=10.0, n_nodes=48, move_all=False, removals=0.0):
     """About `per_cycle` pods arrive between two cycles, at distinct times unless `ties` (the share of
     pods that take the previous pod's creation time); `move_all`: a small cluster, so failed pods
     come back through the unschedulable map with equal-time batches."""
@@ -46,6 +46,8 @@ def queue_scenario(seed, n_pods, per_cycle, ties=0.0, cycle=10.0, n_nodes=48, mo
         cpu = rng.choice([250, 500, 1000, 2000]) * (4 if move_all else 1)
         ram = int(rng.uniform(0.5, 4.0) * GIB) * (8 if move_all else 1)
         w.create_pod(round(t, 6), Pod(f"pod_{i:05d}", cpu, ram, float(rng.randint(5, 200))))
+        if removals and rng.random() < removals:   # often while unschedulable: a stale map entry
+            w.remove_pod(round(t + rng.uniform(1.0, 300.0), 6), f"pod_{i:05d}")
     return scenario_text(cfg, c, w)
 
 
@@ -57,6 +59,14 @@ CASES = {
     "ties": dict(seed=5, n_pods=600, per_cycle=50, ties=0.3),        # equal keys: the heap path
     "ties_long": dict(seed=6, n_pods=1500, per_cycle=300, ties=0.5),
     "requeued": dict(seed=7, n_pods=700, per_cycle=60, n_nodes=6, move_all=True),
+    # round 6: the sorted mode (aq_push) and the device's bulk move-all appends — a backlog whose
+    # arrivals end, so the drain's cycles pop requeued entries with distinct keys only; stale map
+    # entries of removed pods inside the moved batches; arrivals with equal keys interleaved with the
+    # requeues (the mode entered and left between cycles); a map longer than 64 entries per move
+    "requeue_drain": dict(seed=8, n_pods=1200, per_cycle=200, n_nodes=6, move_all=True),
+    "requeue_drain_stale": dict(seed=9, n_pods=1200, per_cycle=200, n_nodes=6, move_all=True, removals=0.15),
+    "requeue_ties": dict(seed=10, n_pods=900, per_cycle=90, n_nodes=8, move_all=True, ties=0.4),
+    "requeue_long_map": dict(seed=11, n_pods=2500, per_cycle=600, n_nodes=10, move_all=True, removals=0.05),
 }
 # what each case's cycles see (pushes by PodScheduleRequest between two cycles; requeues aside):
 # (smallest largest queue, largest largest queue, cycles with equal keys: "none" / "all")
@@ -101,3 +111,25 @@ def test_cases_reach_their_regime(case):
         assert not any(t for _, t in q), case
     elif ties == "all":
         assert all(t for n, t in q if n > 1), case
+
+
+def test_sorted_mode_runs_in_the_drain():
+    """The requeue-drain scenarios spend cycles in sorted mode (k10s_engine.h aq_push): stepping the
+    host build through the drain, some cycle start finds the queue sorted, and the result still equals
+    the oracle at the end (test_cycle_pop_sequence_matches_oracle)."""
+    import ctypes
+    import hostcheck_bridge as hb
+    from kubernetriks_amd.native import RUN_UNTIL_TIME  # noqa: F401
+    L = hb.lib()
+    L.hc_aq_mode.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+    seen = 0
+    for case in ("requeue_drain", "requeue_drain_stale", "requeue_long_map"):
+        eng = HostEngine(queue_scenario(**CASES[case]), 1)
+        for t in range(5, 20000, 10):   # between two cycles (10-s interval), when the queue is filled
+            eng.step_until_time(t + 0.5)
+            srt, n = ctypes.c_uint32(), ctypes.c_uint32()
+            L.hc_aq_mode(eng._h, 0, ctypes.byref(srt), ctypes.byref(n))
+            seen += int(srt.value == 1 and n.value > 1)
+            if eng.results()[0]["status"] != "running":
+                break
+    assert seen > 0

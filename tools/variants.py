@@ -12,6 +12,8 @@ Live knobs (round 4 removed the measured-and-not-kept alternatives; their A/B hi
   round 5   WINDOWS=0|1, WIN_NOTSCHED=0|1, FUSE_FINISH=0|1, RUNS=0|1 (events handled together);
             SEC_SGPR=0|1 (section bases from the LDS table / from the workgroup id); TILE_BEST=1,
             TILE_ALWAYS=1 (best-node tiles, measured and not kept)
+  round 6   TILE_PRUNE=0|1 (block-bound scans of a tile's fitting pods), AQ_SORTED=0|1 (sorted-mode action
+            queue and bulk move-all appends)
   NAME=v    -DK10S_NAME=v (any of the above by name), parts joined by '+'
 Usage: tools/variants.py prof w8 s1 WAVES_PER_EU=8+FQW=4 ..."""
 import os
