@@ -1022,13 +1022,28 @@ K10S_HD bool u_less(const QInfo& a, const QInfo& b) {
     int64_t ka = total_key(a.timestamp), kb = total_key(b.timestamp);
     return ka < kb || (ka == kb && a.pod < b.pod);
 }
+// The map's last key (RepHdr::uq_tail, round 6): a failed attempt's timestamp is its cycle's time
+// plus the cycle's duration so far, above every entry already in the map, so the insert is an append.
+// Knowing the tail's key, that append reads nothing (one dependent read per failed attempt before:
+// the backlog fails about 4 attempts per placement).  A timestamp equal to the tail's, or an unknown
+// tail (after the move / flush compactions), takes the walk below, which also restores the tail.
+#ifndef K10S_UQ_TAIL
+#define K10S_UQ_TAIL 1   // A/B knob: 0 = always the walk (round 5)
+#endif
 K10S_HELPER void uq_insert(Ctx& c, const QInfo& q) {
     if (c.H().uq_size >= c.Ly().cap_uq) {
         fail(c, K10S_ERR_QUEUE_FULL);
         return;
     }
     QInfo* d = c.V().uq();
+    const int64_t kq = total_key(q.timestamp);
     uint32_t pos = c.H().uq_size++;
+    if (K10S_UQ_TAIL && (pos == 0 || kq > c.H().uq_tail)) {
+        d[pos] = q;   // strictly after every entry: no equal key to replace
+        c.H().uq_tail = kq;
+        return;
+    }
+    const uint32_t end = pos;   // the tail's position before this insert
     while (pos > 0) {  // timestamps are almost always >= the tail: short backward walk
         QInfo prev = d[pos - 1];
         if (!u_less(q, prev)) {
@@ -1037,13 +1052,16 @@ K10S_HELPER void uq_insert(Ctx& c, const QInfo& q) {
                 d[pos - 1] = q;
                 for (uint32_t i = pos; i + 1 < c.H().uq_size; i++) d[i] = d[i + 1];
                 c.H().uq_size--;
-                return;
+                return;   // (the tail's key is unchanged)
             }
+            if (pos == end) c.H().uq_tail = kq;   // appended: q is the tail
             break;
         }
+        if (pos == end) c.H().uq_tail = total_key(prev.timestamp);   // prev becomes the tail
         d[pos] = prev;
         pos--;
     }
+    if (pos == 0 && end == 0) c.H().uq_tail = kq;
     d[pos] = q;
 }
 
@@ -1137,6 +1155,7 @@ __device__ __attribute__((noinline)) void s_move_all_dev(Ctx& c) {
     }
     c.H().counters[K10S_C_REQUEUED] += moved;
     c.H().uq_size = w;
+    c.H().uq_tail = 0x7FFFFFFFFFFFFFFFll;   // (the kept entries' last key: not tracked; uq_insert)
 }
 #endif
 K10S_HELPER void s_move(Ctx& c, int mode, double t, uint32_t cpu, uint64_t ram) {
@@ -1190,6 +1209,7 @@ K10S_HELPER void s_move(Ctx& c, int mode, double t, uint32_t cpu, uint64_t ram) 
         }
     }
     c.H().uq_size = w;
+    c.H().uq_tail = 0x7FFFFFFFFFFFFFFFll;   // (the kept entries' last key: not tracked; uq_insert)
 }
 K10S_HD void s_move_after_free(Ctx& c, uint32_t cpu, uint64_t ram) {
     if (c.P().enable_unscheduled_pods_conditional_move) s_move(c, 2, 0.0, cpu, ram);
@@ -2117,8 +2137,13 @@ K10S_HD uint32_t fit_tile(const uint64_t* s_node, uint32_t n_nodes, const uint32
 // K10S_TILE_PRUNE_MAX visited blocks fall back to the full scan (same result).  A visited block's bound
 // is tightened to its entries' maxima (the scan reads them all), so a block that an earlier pod of
 // the tile reserved on is not left looking better than it is.
+// Measured and not kept (default 0, profiles/r06_g1_tile_prune_ab.json, r06_g2_aq_sorted_ab.json): the
+// backlog line reads 2,660 instead of 5,032 node-cache entries per placement, but its time does not
+// fall (1,990 -> 1,989-1,997 ms; with the sorted action queue 1,804 -> 1,844-1,857 ms) — those scans
+// are not on the backlog's critical path — and the larger tile function moves the run kernel's
+// register allocation (C3 -0.5 to +1 %).  Kept as a knob with its parity tests (tests/test_cycle_tile.py).
 #ifndef K10S_TILE_PRUNE
-#define K10S_TILE_PRUNE 1
+#define K10S_TILE_PRUNE 0
 #endif
 #ifndef K10S_TILE_PRUNE_MAX
 #define K10S_TILE_PRUNE_MAX 6
@@ -2462,8 +2487,8 @@ K10S_HD uint32_t tile_lanes_host(const uint64_t* s_node, uint32_t n_nodes, uint3
 #if !K10S_DEVICE && defined(K10S_PRUNE_STUDY)
 // Tooling (tools/prune_study.py): how many entries an exact block-pruned scan would read, with tight
 // componentwise block bounds, best-first block order, for block sizes 16..512.  Slots: [2i] entries
-// read (bounds + blocks), [2i+1] blocks scanned; [12] scans.
-extern "C" uint64_t k10s_prune_stats[32];
+// read (bounds + blocks), [2i+1] blocks scanned; [12] scans; [40..43] near ties of the argmax.
+extern "C" uint64_t k10s_prune_stats[48];
 inline void k10s_prune_study(const uint64_t* s, uint32_t N, uint32_t rc, uint64_t rr) {
     k10s_prune_stats[12] += 1;
     for (int bi = 0; bi < 6; bi++) {
@@ -2529,10 +2554,10 @@ inline void k10s_prune_study(const uint64_t* s, uint32_t N, uint32_t rc, uint64_
         if (!(rc <= v.cpu && rr <= v.ram)) continue;
         const double sc = la_score(v.cpu, v.ram, rc, rr);
         const double du = (bs - sc) * 0.02;
-        if (sc == bs) k10s_prune_stats[28] += 1;
-        if (du <= 1e-5) k10s_prune_stats[29] += 1;
-        if (du <= 1e-4) k10s_prune_stats[30] += 1;
-        if (du <= 1e-3) k10s_prune_stats[31] += 1;
+        if (sc == bs) k10s_prune_stats[40] += 1;
+        if (du <= 1e-5) k10s_prune_stats[41] += 1;
+        if (du <= 1e-4) k10s_prune_stats[42] += 1;
+        if (du <= 1e-3) k10s_prune_stats[43] += 1;
     }
 }
 // Cycle depth study: the cache at the cycle's start (snapshot) and the nodes reserved so far in

@@ -268,6 +268,8 @@ struct RepHdr {
     uint32_t aq_sorted;           // the action queue is in sorted mode (k10s_engine.h aq_push): positions
     uint32_t aq_head;             // [aq_head, aq_head + aq_size) hold it in strictly ascending timestamp
     int64_t aq_last;              // order; aq_last = the newest entry's key (total_key)
+    int64_t uq_tail;              // total_key of the unschedulable map's last entry's timestamp
+                                  // (k10s_engine.h uq_insert); INT64_MAX = not known
     HeapEv fq_win[K10S_NFQ * K10S_FQW];
     HeapEv heap_lds[K10S_HEAP_TOP];
 #if K10S_AQ_TOP

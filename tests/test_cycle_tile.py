@@ -171,14 +171,15 @@ def test_tile_best_variant_host():
 
 
 def test_tile_pruned_scans_read_less_host():
-    """Round 6: a tile's pods that fit scan the blocks whose bound can still win (tile_scan_pruned)
-    instead of the whole cache.  The host build without it (K10S_TILE_PRUNE=0) gives the same results
-    and reads more node-cache entries."""
+    """Round 6: a tile's pods that fit scan the blocks whose bound can still win (tile_scan_pruned,
+    the K10S_TILE_PRUNE=1 knob: measured and not kept) instead of the whole cache.  The host build with
+    it gives the same results as the default and reads fewer node-cache entries; it also runs this
+    file's host cases."""
     import subprocess
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     hc = os.path.join(repo, "tests", "hostcheck")
-    out = os.path.join(repo, "build", f"libk10s_hostcheck_noprune_{os.getpid()}.so")
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-ffp-contract=off", "-w", "-DK10S_TILE_PRUNE=0",
+    out = os.path.join(repo, "build", f"libk10s_hostcheck_prune_{os.getpid()}.so")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-ffp-contract=off", "-w", "-DK10S_TILE_PRUNE=1",
                            "-shared", "-o", out, os.path.join(hc, "hostcheck.cpp"),
                            os.path.join(repo, "kubernetriks_amd", "csrc", "k10s_builder.cpp")])
     try:
@@ -202,6 +203,12 @@ def test_tile_pruned_scans_read_less_host():
         ka, kb = dict(ra["counters"]), dict(rb["counters"])
         na, nb = ka.pop("nodes_read"), kb.pop("nodes_read")
         assert ka == kb and parity.feq(ra["time"], rb["time"])
-        assert na < 0.95 * nb, (na, nb)
+        assert nb < 0.95 * na, (na, nb)
+        import sys
+        env = dict(os.environ, K10S_HOSTCHECK_LIB=out)
+        r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-n", "4", "-m", "not gpu", "-p", "no:cacheprovider",
+                            os.path.join(repo, "tests", "test_cycle_tile.py"), "-k", "cycle_tiles_match_oracle"],
+                           env=env, cwd=repo, capture_output=True, text=True, timeout=1200)
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     finally:
         os.unlink(out)

@@ -324,3 +324,56 @@ def test_finish_relay_fused_and_refused():
     finally:
         hb.LIB_PATH, hb._lib, hb.build = saved
     assert 0 < fused < finished, (fused, finished)
+
+
+def gauge_straddle_scenario(seed: int) -> str:
+    """windows next to the gauge recorder.  Network delays of 1.2-2.6 s make every
+    cycle's assignment pipeline span several 5-s gauge ticks (M_GAUGE_TICK, a heap event and not a
+    window kind), and the node-component binds (the gauge's per-slot allocatable, N_BIND) and the
+    storage assignments of a window land on both sides of a tick: a window that ran across a tick, or
+    applied its binds in another order, would change a gauge row (node averages summed in name order,
+    cluster sums) against the oracle."""
+    rng = random.Random(seed)
+    cfg = test_simulation_config()
+    cfg.scheduling_cycle_interval = rng.choice([5.0, 7.0])
+    cfg.as_to_ps_network_delay = rng.choice([1.2, 1.9, 2.5])
+    cfg.as_to_node_network_delay = rng.choice([1.3, 2.6])
+    cfg.sched_to_as_network_delay = rng.choice([0.4, 1.1])
+    cfg.ps_to_sched_network_delay = 0.3
+    cluster = GenericClusterTrace()
+    for i in range(rng.randint(3, 12)):
+        cluster.create_node(0.0, Node(f"node_{i:02d}", rng.choice([16000, 64000]), rng.choice([64, 256]) << 30))
+    workload = GenericWorkloadTrace()
+    for i in range(400):
+        workload.create_pod(float(rng.randint(0, 200)) + rng.choice([0.0, 0.5, 4.9]),
+                            Pod(f"pod_{i:04d}", rng.choice([100, 500, 3000]), rng.choice([1 << 28, 1 << 30, 8 << 30]),
+                                float(rng.randint(1, 60))))
+    return scenario_text(cfg, cluster, workload)
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+@pytest.mark.parametrize("seed", range(6))
+def test_windows_keep_gauge_rows_exact(backend, seed):
+    scn = gauge_straddle_scenario(seed)
+    od, eng = parity.run_pair(engine_cls(backend), scn, max_time=20000.0)
+    assert parity.compare(od, eng) == [], seed
+    assert len(eng.gauges(0)) > 20
+
+
+def test_gauge_straddle_scenarios_use_windows():
+    """The gauge-straddle scenarios above do run windows (host build with event statistics)."""
+    out = _stats_lib()
+    L = ctypes.CDLL(out)
+    import hostcheck_bridge as hb
+    saved = (hb.LIB_PATH, hb._lib, hb.build)
+    try:
+        hb.LIB_PATH, hb._lib, hb.build = out, None, (lambda: None)
+        st = (ctypes.c_uint64 * 48).in_dll(L, "k10s_host_stats")
+        for seed in range(6):
+            before = [int(st[i]) for i in (0, 41, 42)]
+            eng = hb.HostEngine(gauge_straddle_scenario(seed), 1)
+            eng.run_until_all_finished(max_time=20000.0)
+            events, wins, win_events = (int(st[i]) - b for i, b in zip((0, 41, 42), before))
+            assert wins > 100 and win_events > 0.25 * events, (seed, events, wins, win_events)
+    finally:
+        hb.LIB_PATH, hb._lib, hb.build = saved

@@ -23,9 +23,9 @@ def main():
     out = os.path.join(REPO, "build", "libk10s_prunestudy.so")
     defs = os.path.join(REPO, "build", "prunestudy_defs.cpp")
     with open(defs, "w") as f:
-        f.write('#include <cstdint>\nextern "C" uint64_t k10s_prune_stats[32];\nuint64_t k10s_prune_stats[32];\n')
+        f.write('#include <cstdint>\nextern "C" uint64_t k10s_prune_stats[48];\nuint64_t k10s_prune_stats[48];\n')
     hc = os.path.join(REPO, "tests", "hostcheck")
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-ffp-contract=off", "-DK10S_PRUNE_STUDY", "-shared",
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-ffp-contract=off", "-DK10S_PRUNE_STUDY", "-DK10S_TILE_PRUNE=0", "-shared",
                            "-o", out, os.path.join(hc, "hostcheck.cpp"),
                            os.path.join(REPO, "kubernetriks_amd", "csrc", "k10s_builder.cpp"), defs])
     import hostcheck_bridge as hb
@@ -39,7 +39,7 @@ def main():
         cluster, workload = wl.c3_traces(n_nodes=nodes, n_pods=pods, arrival_window=1200.0, seed=123)
     eng = hb.HostEngine(scenario_text(SimulationConfig(), cluster, workload), 1)
     eng.run_until_all_finished(max_time=1e7)
-    st = (ctypes.c_uint64 * 32).in_dll(hb.lib(), "k10s_prune_stats")
+    st = (ctypes.c_uint64 * 48).in_dll(hb.lib(), "k10s_prune_stats")
     scans = max(int(st[12]), 1)
     rows = {}
     for i in range(6):
@@ -52,8 +52,8 @@ def main():
                       "cycles": int(st[13]), "attempts_per_cycle": round(att / max(int(st[13]), 1), 2),
                       "distinct_reserved_per_cycle": round(st[15] / max(int(st[13]), 1), 2),
                       "snapshot_depth_share": depth,
-                      "per_scan_nodes_tied": round(st[28] / scans, 1), "within_1e-5": round(st[29] / scans, 1),
-                      "within_1e-4": round(st[30] / scans, 1), "within_1e-3": round(st[31] / scans, 1)}, indent=1))
+                      "per_scan_nodes_tied": round(st[40] / scans, 1), "within_1e-5": round(st[41] / scans, 1),
+                      "within_1e-4": round(st[42] / scans, 1), "within_1e-3": round(st[43] / scans, 1)}, indent=1))
 
 
 if __name__ == "__main__":
