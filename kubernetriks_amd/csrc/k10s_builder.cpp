@@ -820,6 +820,11 @@ Layout make_layout(const HostScenario& hs, const k10s_capacities& caps, bool all
     // hot scheduler-cache SoA first (the scan target), then per-entity records
     const uint64_t wide = L.packed ? 0 : 1;
     L.s_node = take(L.packed ? 8 * N : 0);
+    // per-block fronts of the packed cache (k10s_engine.h front_scan): up to 64 blocks of 64 nodes
+    L.front = (L.packed && N <= 4096) ? 1u : 0u;
+    const uint64_t nbf = L.front ? (N + 63) / 64 : 0;
+    L.fr_val = take(8 * 8 * nbf);
+    L.fr_idx = take(8 * nbf);
     L.s_cpu = take(wide * 4 * N);
     L.s_ram = take(wide * 8 * N);
     L.s_present = take(8 * (uint64_t)L.words_nodes);

@@ -288,6 +288,20 @@ K10S_HD uint32_t wave_sum_u32(uint32_t v) {
 #endif
     return v;
 }
+K10S_HD uint64_t wave_or_u64(uint64_t v) {   // every lane gets the OR over the wave
+#if K10S_DEVICE
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32), a, b;
+    xpair<0>(lo, a, b); lo = a | b; xpair<0>(hi, a, b); hi = a | b;
+    xpair<1>(lo, a, b); lo = a | b; xpair<1>(hi, a, b); hi = a | b;
+    xpair<2>(lo, a, b); lo = a | b; xpair<2>(hi, a, b); hi = a | b;
+    xpair<3>(lo, a, b); lo = a | b; xpair<3>(hi, a, b); hi = a | b;
+    xpair<4>(lo, a, b); lo = a | b; xpair<4>(hi, a, b); hi = a | b;
+    xpair<5>(lo, a, b); lo = a | b; xpair<5>(hi, a, b); hi = a | b;
+    return join64(lo, hi);
+#else
+    return v;
+#endif
+}
 // Make a value provably wave-uniform for the compiler (it already is by construction).
 K10S_HD uint32_t uniform_u32(uint32_t v) {
 #if K10S_DEVICE

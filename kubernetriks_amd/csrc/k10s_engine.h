@@ -186,6 +186,8 @@ struct Rep {
 #endif
     K10S_HD RepHdr* h() const { return at<RepHdr>(L().hdr); }
     K10S_HD uint64_t* s_node() const { return hot<uint64_t>(SEC_SNODE, L().s_node); }
+    K10S_HD uint64_t* fr_val() const { return at<uint64_t>(L().fr_val); }
+    K10S_HD uint8_t* fr_idx() const { return at<uint8_t>(L().fr_idx); }
     K10S_HD uint32_t* s_cpu() const { return at<uint32_t>(L().s_cpu); }
     K10S_HD uint64_t* s_ram() const { return at<uint64_t>(L().s_ram); }
     K10S_HD uint64_t* s_present() const { return hot<uint64_t>(SEC_PRES, L().s_present); }
@@ -327,9 +329,18 @@ K10S_HD void nc_put(Ctx& c, uint32_t n, NcEnt v) {
         c.V().s_ram()[n] = v.ram;
     }
 }
+// A packed entry of node n changed: its 64-node block's front is stale (front_scan).  Wave-uniform
+// callers only (a lane-parallel writer ORs its blocks into fr_dirty itself: run_batch).
+#ifndef K10S_FRONT
+#define K10S_FRONT 1   // A/B knob: 0 = every fast-path attempt scans the whole cache (round 5)
+#endif
+K10S_HD void fr_mark(Ctx& c, uint32_t n) {
+    if (K10S_FRONT && c.Ly().front) c.H().fr_dirty |= 1ull << (n >> 6);
+}
 // reserve_node_resources (scheduler.rs:118-123) after Fit: request <= allocatable, no borrow
 K10S_HD void nc_reserve(Ctx& c, uint32_t n, uint32_t rc, uint64_t rr) {
     if (nc_packed(c)) {
+        fr_mark(c, n);
         c.V().s_node()[n] -= nc_pack(rc, rr);
     } else {
         c.V().s_cpu()[n] -= rc;
@@ -344,6 +355,7 @@ K10S_HD bool nc_release(Ctx& c, uint32_t n, NcEnt v, uint32_t rc, uint64_t rr) {
             fail(c, K10S_ERR_NODE_CACHE_RANGE);
             return false;
         }
+        fr_mark(c, n);
         c.V().s_node()[n] = nc_pack(v.cpu + rc, v.ram + rr);
     } else {
         c.V().s_cpu()[n] = v.cpu + rc;
@@ -1729,6 +1741,228 @@ K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const ui
     return K10S_SCHED_OK;
 }
 
+// ---- per-block fronts of the packed node cache (round 6) -----------------------------------------
+// Which nodes can be schedule_one's answer at all.  With weight 1.0 and both requests > 0 the
+// LeastAllocated score is monotone in (cpu, ram) (correctly rounded quotients of exactly represented
+// integers: schedule_scan_pruned's argument) and Fit is too, so a node n is never the answer when a
+// later node m > n (name order) has at least as much of both: m fits whenever n does, scores at least
+// as much, and wins a tie (the last maximum, kube_scheduler.rs:140-148).  The answer is therefore in
+// the index-aware front {n : no m > n with cpu_m >= cpu_n and ram_m >= ram_n}, and within any block
+// of nodes in the block's own front.  At C3 the whole cache's front holds 40 of 4,096 nodes and a
+// 64-node block's 3.9 on average (tools/prune_study.py): identical empty nodes collapse to their
+// last one, and a loaded node below an empty one of its type never wins.
+// The engine keeps, per 64-node block (<= 64 blocks, N <= 4,096), its front's entries and node
+// offsets (K10S_FR_K slots; a block with more is scanned whole: fr_over), rebuilt lazily: every change
+// of an entry (reserve, release, add, remove) marks its block in fr_dirty, and the next scan rebuilds
+// the marked blocks first (four per memory round trip).  A fast-path attempt then reads K10S_FR_K
+// slots per block (512 B per 64 blocks... 4 KB at C3) instead of the whole cache (32 KB), scores them
+// like the screened scan (the first slot exactly, the rest screened against the wave's threshold),
+// and takes the wave's (score, index) maximum.  The result is the full scan's by the argument above;
+// entries read = slots + rebuilt and overflowing blocks' nodes.
+#define K10S_FR_K 8
+#if K10S_DEVICE
+K10S_D uint64_t readlane_u64(uint64_t v, uint32_t j) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)j) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)j);
+}
+// Block b's front from its entries (lane i holds node 64b + i, 0 past the end): the highest lane that
+// no processed front lane dominates is itself in the front (every lane above it is in the front or
+// dominated by a front lane above it, which would dominate it too); it then marks the lanes below it
+// that it dominates.  One iteration per front node.  Returns the front's size.
+K10S_D uint32_t fr_block(uint64_t* fv, uint8_t* fi, uint32_t b, uint64_t x) {
+    const uint32_t lane = (uint32_t)lane_id();
+    const uint32_t cpu = (uint32_t)(x >> K10S_PK_SHIFT);
+    const uint64_t ram = x & K10S_PK_RAM;
+    bool dom = x == 0;   // an absent node holds (0, 0): it fits no request with cpu > 0
+    uint64_t front = 0;
+    for (;;) {
+        const uint64_t cand = __ballot(!dom) & ~front;
+        if (cand == 0) break;
+        const uint32_t j = 63u - (uint32_t)__builtin_clzll(cand);
+        front |= 1ull << j;
+        const uint64_t xj = readlane_u64(x, j);
+        dom = dom || (lane < j && cpu <= (uint32_t)(xj >> K10S_PK_SHIFT) && ram <= (xj & K10S_PK_RAM));
+    }
+    const uint32_t nf = (uint32_t)__popcll(front);
+    const uint32_t rank = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(front >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)front, 0u));
+    if (((front >> lane) & 1ull) && rank < K10S_FR_K) {
+        fv[b * K10S_FR_K + rank] = x;
+        fi[b * K10S_FR_K + rank] = (uint8_t)lane;
+    }
+    if (lane >= nf && lane < K10S_FR_K) fv[b * K10S_FR_K + lane] = 0;   // unused slots fit nothing
+    return nf;
+}
+#endif
+// Rebuild every marked block's front; returns the entries read.
+K10S_HD_NOINL uint32_t fr_refresh(Ctx& c) {
+    uint64_t dirty = uniform_u64(c.H().fr_dirty);
+    if (dirty == 0) return 0;
+    const uint32_t N = uniform_u32(c.S().n_nodes);
+    const uint64_t* sn = c.V().s_node();
+    uint64_t* fv = c.V().fr_val();
+    uint8_t* fi = c.V().fr_idx();
+    uint64_t over = uniform_u64(c.H().fr_over);
+    uint32_t reads = 0;
+#if K10S_DEVICE
+    const uint32_t lane = (uint32_t)lane_id();
+    while (dirty) {
+        uint32_t bs[4];
+        uint64_t xs[4];
+        uint32_t k = 0;
+        K10S_UNROLL
+        for (uint32_t i = 0; i < 4; i++) {   // the next four marked blocks' loads together
+            bs[i] = 0;
+            xs[i] = 0;
+            if (dirty) {
+                const uint32_t b = (uint32_t)__builtin_ctzll(dirty);
+                dirty &= dirty - 1;
+                bs[i] = b;
+                const uint32_t n = 64u * b + lane;
+                if (n < N) xs[i] = sn[n];
+                reads += N - 64u * b < 64u ? N - 64u * b : 64u;
+                k = i + 1;
+            }
+        }
+        K10S_UNROLL
+        for (uint32_t i = 0; i < 4; i++) {
+            if (i < k) {
+                const uint32_t nf = fr_block(fv, fi, bs[i], xs[i]);
+                over = nf > K10S_FR_K ? (over | (1ull << bs[i])) : (over & ~(1ull << bs[i]));
+            }
+        }
+    }
+#else
+    while (dirty) {
+        const uint32_t b = (uint32_t)__builtin_ctzll(dirty);
+        dirty &= dirty - 1;
+        const uint32_t lo = 64u * b, hi = lo + 64u < N ? lo + 64u : N;
+        reads += hi - lo;
+        uint32_t mem[64];
+        uint32_t nf = 0;
+        for (uint32_t k = hi; k-- > lo;) {   // from the last node: kept iff no kept later node dominates it
+            const uint64_t x = sn[k];
+            if (x == 0) continue;
+            const NcEnt v = nc_unpack(x);
+            bool dom = false;
+            for (uint32_t q = 0; q < nf && !dom; q++) {
+                const NcEnt w = nc_unpack(sn[mem[q]]);
+                dom = w.cpu >= v.cpu && w.ram >= v.ram;
+            }
+            if (!dom) mem[nf++] = k;
+        }
+        for (uint32_t r = 0; r < K10S_FR_K; r++) {   // slots in ascending node order
+            if (r < nf) {
+                const uint32_t k = mem[nf - 1 - r];
+                fv[b * K10S_FR_K + r] = sn[k];
+                fi[b * K10S_FR_K + r] = (uint8_t)(k - lo);
+            } else {
+                fv[b * K10S_FR_K + r] = 0;
+            }
+        }
+        over = nf > K10S_FR_K ? (over | (1ull << b)) : (over & ~(1ull << b));
+    }
+#endif
+    c.H().fr_dirty = 0;
+    c.H().fr_over = over;
+    return reads;
+}
+// schedule_one over the fronts (fr_refresh first): K10S_SCHED_OK / NO_SUFFICIENT_RESOURCES;
+// *nread: entries read.  Preconditions: weight 1.0, rc > 0, rr > 0, the cache packed with fronts.
+K10S_HD_NOINL int front_scan(Ctx& c, uint32_t rc, uint64_t rr, int32_t* chosen, uint32_t* nread) {
+    const uint32_t N = uniform_u32(c.S().n_nodes);
+    const uint32_t NB = (N + 63u) >> 6;
+    const uint64_t over = uniform_u64(c.H().fr_over);
+    const uint64_t* fv = c.V().fr_val();
+    const uint8_t* fi = c.V().fr_idx();
+    const uint64_t* sn = c.V().s_node();
+    uint32_t reads = NB * K10S_FR_K;
+    uint64_t best_key = 0;
+    int32_t best_n = -1;
+#if K10S_DEVICE
+    const uint32_t lane = (uint32_t)lane_id();
+    rc = uniform_u32(rc);
+    rr = uniform_u64(rr);
+    const double frc = uniform_f64((double)rc), frr = uniform_f64(u64_f64(rr));
+    const float fa = (float)rc;
+    const float fr = __builtin_fmaf((float)(uint32_t)(rr >> 32), 4294967296.0f, (float)(uint32_t)rr);
+    double bs = -__builtin_inf();
+    int32_t bn = -1;
+    uint64_t x[K10S_FR_K];
+    uint64_t ix = 0;
+    if (lane < NB) {
+        const ulonglong2* p = reinterpret_cast<const ulonglong2*>(fv + lane * K10S_FR_K);
+        K10S_UNROLL
+        for (int k = 0; k < K10S_FR_K / 2; k++) {
+            const ulonglong2 q = p[k];
+            x[2 * k] = q.x;
+            x[2 * k + 1] = q.y;
+        }
+        ix = *reinterpret_cast<const uint64_t*>(fi + lane * K10S_FR_K);
+    } else {
+        K10S_UNROLL
+        for (int k = 0; k < K10S_FR_K; k++) x[k] = 0;
+    }
+    auto consider = [&](uint64_t e, int32_t n) {   // a fitting entry's exact score into the lane best
+        const NcEnt v = nc_unpack(e);
+        if (rc <= v.cpu && rr <= v.ram) {
+            const double s = la_exact(v.cpu, v.ram, rr, frc, frr);
+            if (s > bs || (s == bs && n > bn)) {
+                bs = s;
+                bn = n;
+            }
+        }
+    };
+    consider(x[0], (int32_t)(64u * lane + (uint32_t)(ix & 0xFFu)));
+    float lu = bn >= 0 ? screen_u(bs) : __builtin_inff();
+    const float thr = __builtin_bit_cast(float, uniform_u32(__builtin_bit_cast(uint32_t, wave_min_f32(lu))));
+    const float T = thr + K10S_SCREEN_EPS;   // +inf when no lane scored: screens nothing out
+    K10S_UNROLL
+    for (int k = 1; k < K10S_FR_K; k++) {
+        const NcEnt v = nc_unpack(x[k]);
+        if (x[k] != 0 && !scan_screen(v.cpu, v.ram, fa, fr, T))
+            consider(x[k], (int32_t)(64u * lane + (uint32_t)((ix >> (8 * k)) & 0xFFu)));
+    }
+    // blocks whose front overflowed the slots: the whole block, one node per lane
+    for (uint64_t ov = over; ov; ov &= ov - 1) {
+        const uint32_t b = (uint32_t)__builtin_ctzll(ov);
+        const uint32_t n = 64u * b + lane;
+        reads += N - 64u * b < 64u ? N - 64u * b : 64u;
+        if (n < N) {
+            const uint64_t e = sn[n];
+            const NcEnt v = nc_unpack(e);
+            if (e != 0 && !scan_screen(v.cpu, v.ram, fa, fr, T)) consider(e, (int32_t)n);
+        }
+    }
+    best_key = bn >= 0 ? score_key(bs) : 0;
+    best_n = bn;
+    wave_argmax(best_key, best_n);
+    best_n = (int32_t)uniform_u32((uint32_t)best_n);
+#else
+    for (uint32_t b = 0; b < NB; b++) {
+        auto consider = [&](uint64_t e, int32_t n) {
+            const NcEnt v = nc_unpack(e);
+            if (e != 0 && rc <= v.cpu && rr <= v.ram) {
+                const uint64_t k = score_key(la_score(v.cpu, v.ram, rc, rr));
+                if (k > best_key || (k == best_key && n > best_n)) {
+                    best_key = k;
+                    best_n = n;
+                }
+            }
+        };
+        for (uint32_t k = 0; k < K10S_FR_K; k++) consider(fv[b * K10S_FR_K + k], (int32_t)(64u * b + fi[b * K10S_FR_K + k]));
+        if ((over >> b) & 1ull) {
+            const uint32_t hi = 64u * b + 64u < N ? 64u * b + 64u : N;
+            reads += hi - 64u * b;
+            for (uint32_t n = 64u * b; n < hi; n++) consider(sn[n], (int32_t)n);
+        }
+    }
+#endif
+    *nread = reads;
+    if (best_n < 0) return K10S_SCHED_NO_SUFFICIENT_RESOURCES;
+    *chosen = best_n;
+    return K10S_SCHED_OK;
+}
+
 // ---- score plugins beyond LeastAllocated alone (k10s_replica_params.score_plugins) --------------
 // MostAllocatedResources is an extension: the reference registry (plugin.rs:13-23) has only Fit and
 // LeastAllocatedResources.  Defined as kube-scheduler's MostAllocated strategy in this model's terms
@@ -2534,6 +2768,65 @@ inline void k10s_prune_study(const uint64_t* s, uint32_t N, uint32_t rc, uint64_
         k10s_prune_stats[2 * bi] += reads;
         k10s_prune_stats[2 * bi + 1] += blocks;
     }
+    // the index-aware Pareto front: nodes not weakly dominated (cpu and ram both >=) by a later node
+    // — the only possible last maxima for any request; [44] its size summed over scans
+    {
+        std::vector<std::pair<uint32_t, uint64_t>> stair;   // seen (cpu, max ram at >= cpu), cpu descending
+        uint64_t front = 0;
+        for (uint32_t n = N; n-- > 0;) {
+            const NcEnt v = nc_unpack(s[n]);
+            if (v.cpu == 0 && v.ram == 0) continue;
+            bool dom = false;
+            for (const auto& p : stair) {
+                if (p.first < v.cpu) break;
+                if (p.second >= v.ram) {
+                    dom = true;
+                    break;
+                }
+            }
+            if (dom) continue;
+            front += 1;
+            // insert (cpu, ram) keeping cpu descending with ram the running max
+            std::vector<std::pair<uint32_t, uint64_t>> nx;
+            bool put = false;
+            for (const auto& p : stair) {
+                if (!put && p.first <= v.cpu) {
+                    nx.push_back({v.cpu, v.ram});
+                    put = true;
+                }
+                if (p.first < v.cpu && p.second <= v.ram) continue;   // now dominated in the staircase
+                if (p.first == v.cpu) continue;
+                nx.push_back(p);
+            }
+            if (!put) nx.push_back({v.cpu, v.ram});
+            uint64_t mx = 0;
+            for (auto& p : nx) {
+                mx = p.second > mx ? p.second : mx;
+                p.second = mx;
+            }
+            stair.swap(nx);
+        }
+        k10s_prune_stats[44] += front;
+    }
+    // per 64-node block: its own index-aware front (within the block); [45] sum of sizes, [46] blocks
+    // with more than 8, [47] the largest seen
+    for (uint32_t b = 0; b * 64 < N; b++) {
+        uint32_t cnt = 0;
+        const uint32_t hi = (b + 1) * 64 < N ? (b + 1) * 64 : N;
+        for (uint32_t k = b * 64; k < hi; k++) {
+            const NcEnt v = nc_unpack(s[k]);
+            if (v.cpu == 0 && v.ram == 0) continue;
+            bool dom = false;
+            for (uint32_t m = k + 1; m < hi && !dom; m++) {
+                const NcEnt w = nc_unpack(s[m]);
+                dom = w.cpu >= v.cpu && w.ram >= v.ram;
+            }
+            cnt += dom ? 0 : 1;
+        }
+        k10s_prune_stats[45] += cnt;
+        k10s_prune_stats[46] += cnt > 8 ? 1 : 0;
+        if (cnt > k10s_prune_stats[47]) k10s_prune_stats[47] = cnt;
+    }
     // near ties of the argmax: nodes with exactly its score, within 1e-5 of its u, within 1e-4
     uint64_t bk = 0;
     for (uint32_t n = 0; n < N; n++) {
@@ -2654,6 +2947,12 @@ K10S_HD int32_t cycle_attempt(Ctx& c, double t, QInfo q, int32_t pick, double& c
             nread = c.S().n_nodes;
         } else if (!nc_packed(c) && c.Ly().pruned && w == 1.0 && rc > 0 && rr > 0) {
             st = schedule_scan_pruned(c, rc, rr, &chosen, &nread);
+        }
+        if (st < 0 && K10S_FRONT && !PLUG && c.Ly().front && w == 1.0 && rc > 0 && rr > 0) {
+            nread += fr_refresh(c);
+            uint32_t fr = 0;
+            st = front_scan(c, rc, rr, &chosen, &fr);
+            nread += fr;
         }
         if (st < 0) {
 #if !K10S_DEVICE && defined(K10S_PRUNE_STUDY)
@@ -2963,6 +3262,7 @@ K10S_HD void s_add_node(Ctx& c, const HeapEv& e) {
     uint64_t ar = f2u(e.x);
     const NcEnt cap = {ac, ar};
     nc_put(c, n, cap);
+    fr_mark(c, n);
     // the stored node's capacity: a node reaches the scheduler straight from its creation,
     // allocatable = capacity (node.rs:60-66); only MostAllocated reads it (wide layout)
     if (!nc_packed(c)) {
@@ -3052,6 +3352,7 @@ K10S_HD void on_scheduler(Ctx& c, const HeapEv& e) {
         // cpu > 0 fits it and the event loop's screened scan needs no presence words
         const NcEnt zero = {0u, 0ull};
         nc_put(c, n, zero);
+        fr_mark(c, n);
         h->s_node_count -= 1;
         node_bound_changed(c, n);
         if (c.V().node(n).flags & NF_S_ASSIGN) {  // reschedule_unfinished_pods (352-364), name order
@@ -4341,6 +4642,11 @@ K10S_HD void init_replica(Ctx& c) {
         v.node(i) = ns;
     }
     for (uint32_t i = lane; i < L->words_nodes; i += K10S_LANES) v.s_present()[i] = 0;
+    if (L->front) {   // empty fronts: every node is absent, (0, 0)
+        const uint32_t nbf = (N + 63u) / 64u;
+        for (uint32_t i = lane; i < 8u * nbf; i += K10S_LANES) v.fr_val()[i] = 0;
+        for (uint32_t i = lane; i < 8u * nbf; i += K10S_LANES) v.fr_idx()[i] = 0;
+    }
     for (uint32_t i = lane; i < L->words_uids; i += K10S_LANES) v.pend_rm()[i] = 0;
     const bool perturb = pr->perturb != 0;
     k10s_pod_record* prec = v.prec();
@@ -4429,6 +4735,7 @@ K10S_HD void init_replica(Ctx& c) {
         }
         const NcEnt cap = {sc->def_cpu[def], sc->def_ram[def]};
         nc_put(c, n, cap);
+        fr_mark(c, n);
         if (!nc_packed(c)) {   // capacities (MostAllocated): wide layout only
             v.s_ccpu()[n] = cap.cpu;
             v.s_cram()[n] = cap.ram;
@@ -4989,6 +5296,7 @@ K10S_HD_NOINL uint32_t run_batch(Ctx& c, uint32_t k) {
     const uint32_t log0 = uniform_u32(H.log_n) - 1u;   // event 0 was logged by the event loop
     const uint32_t pool_head = uniform_u32(H.pool_head);
     uint32_t cnt = 0;   // per lane: PF_UNSCHED pods (PS_CREATE_POD_REQ) / newly present nodes (S_ADD_NODE)
+    uint64_t fbits = 0;  // S_ADD_NODE: the blocks whose front the lane's node changes (fr_mark)
     K10S_FOR_RUN(i, K) {
         const RunEv r = run_ev(c, src, i);
         const bool node_kind = k != K10S_EV_AS_CREATE_POD_REQ && k != K10S_EV_PS_CREATE_POD_REQ &&
@@ -5054,6 +5362,7 @@ K10S_HD_NOINL uint32_t run_batch(Ctx& c, uint32_t k) {
         case K10S_EV_S_ADD_NODE: {   // scheduler.rs:391-405 (packed cache, empty unschedulable map)
             const NcEnt ent = {r.b, f2u(r.x)};
             nc_put(c, r.a, ent);
+            fbits |= 1ull << (r.a >> 6);
             const uint64_t bit = 1ull << (r.a & 63u);
 #if K10S_DEVICE
             const uint64_t old = atomicOr((unsigned long long*)&c.V().s_present()[r.a >> 6], (unsigned long long)bit);
@@ -5100,7 +5409,10 @@ K10S_HD_NOINL uint32_t run_batch(Ctx& c, uint32_t k) {
         H.as_node_count += K;
         break;
     case K10S_EV_PS_NODE_ADDED: H.counters[K10S_C_PROCESSED_NODES] += K; break;
-    case K10S_EV_S_ADD_NODE: H.s_node_count += wave_sum_u32(cnt); break;
+    case K10S_EV_S_ADD_NODE:
+        H.s_node_count += wave_sum_u32(cnt);
+        if (K10S_FRONT && c.Ly().front) H.fr_dirty |= wave_or_u64(fbits);
+        break;
     default: break;
     }
     if (cls >= 0) {

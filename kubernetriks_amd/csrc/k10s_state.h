@@ -270,6 +270,8 @@ struct RepHdr {
     int64_t aq_last;              // order; aq_last = the newest entry's key (total_key)
     int64_t uq_tail;              // total_key of the unschedulable map's last entry's timestamp
                                   // (k10s_engine.h uq_insert); INT64_MAX = not known
+    uint64_t fr_dirty;            // 64-node blocks whose front is stale (front_scan rebuilds them)
+    uint64_t fr_over;             // blocks whose front has more than K10S_FR_K entries (scanned whole)
     HeapEv fq_win[K10S_NFQ * K10S_FQW];
     HeapEv heap_lds[K10S_HEAP_TOP];
 #if K10S_AQ_TOP
@@ -355,6 +357,8 @@ struct Layout {
     uint64_t hdr;
     uint64_t s_cpu, s_ram, s_present;    // hot scheduler-cache SoA (scan target; wide layout)
     uint64_t s_node;                     // packed layout: u64 per node, cpu << 40 | ram (k10s_engine.h nc_*)
+    uint64_t fr_val, fr_idx;             // per 64-node block: its index-aware front (k10s_engine.h
+                                         // front_scan), K10S_FR_K packed entries + their node offsets
     uint64_t s_bcpu, s_bram;             // per-block maxima of the present nodes' allocatable
     uint64_t s_ccpu, s_cram;             // scheduler-cache capacity SoA (MostAllocated, an extension)
     uint64_t node, pend_rm, pod, prec, slot, pool_ring;
@@ -377,6 +381,8 @@ struct Layout {
     uint32_t packed;      // 1: node cache packed in s_node (8 B per node); 0: wide SoA s_cpu / s_ram
     uint32_t tnonneg;     // 1: every event time of the scenario and its replicas' parameters is >= 0
                           // (times_nonneg): no emission can precede the clock
+    uint32_t front;       // 1: the packed cache keeps per-block fronts (<= 64 blocks of 64 nodes)
+    uint32_t pad_front;
 };
 
 // Everything a launch reads but never writes, as one block (device: __constant__ memory).

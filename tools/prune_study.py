@@ -25,7 +25,7 @@ def main():
     with open(defs, "w") as f:
         f.write('#include <cstdint>\nextern "C" uint64_t k10s_prune_stats[48];\nuint64_t k10s_prune_stats[48];\n')
     hc = os.path.join(REPO, "tests", "hostcheck")
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-ffp-contract=off", "-DK10S_PRUNE_STUDY", "-DK10S_TILE_PRUNE=0", "-shared",
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-ffp-contract=off", "-DK10S_PRUNE_STUDY", "-DK10S_TILE_PRUNE=0", "-DK10S_FRONT=0", "-shared",
                            "-o", out, os.path.join(hc, "hostcheck.cpp"),
                            os.path.join(REPO, "kubernetriks_amd", "csrc", "k10s_builder.cpp"), defs])
     import hostcheck_bridge as hb
@@ -53,7 +53,10 @@ def main():
                       "distinct_reserved_per_cycle": round(st[15] / max(int(st[13]), 1), 2),
                       "snapshot_depth_share": depth,
                       "per_scan_nodes_tied": round(st[40] / scans, 1), "within_1e-5": round(st[41] / scans, 1),
-                      "within_1e-4": round(st[42] / scans, 1), "within_1e-3": round(st[43] / scans, 1)}, indent=1))
+                      "within_1e-4": round(st[42] / scans, 1), "within_1e-3": round(st[43] / scans, 1),
+                      "pareto_front_per_scan": round(st[44] / scans, 1),
+                      "block64_front_mean": round(st[45] / scans / ((nodes + 63) // 64), 2),
+                      "block64_fronts_over_8_per_scan": round(st[46] / scans, 3), "block64_front_max": int(st[47])}, indent=1))
 
 
 if __name__ == "__main__":
