@@ -2948,7 +2948,10 @@ K10S_HD int32_t cycle_attempt(Ctx& c, double t, QInfo q, int32_t pick, double& c
         } else if (!nc_packed(c) && c.Ly().pruned && w == 1.0 && rc > 0 && rr > 0) {
             st = schedule_scan_pruned(c, rc, rr, &chosen, &nread);
         }
-        if (st < 0 && K10S_FRONT && !PLUG && c.Ly().front && w == 1.0 && rc > 0 && rr > 0) {
+        // fronts in the serial cycle only: a tile's cycle (after failed attempts) places few pods, and
+        // rebuilding the blocks that the finishes since the last cycle marked would cost more than
+        // its full scans (backlog +9 %, profiles/r06_g6_fronts_ab.json)
+        if (st < 0 && K10S_FRONT && !PLUG && !TILE && c.Ly().front && w == 1.0 && rc > 0 && rr > 0) {
             nread += fr_refresh(c);
             uint32_t fr = 0;
             st = front_scan(c, rc, rr, &chosen, &fr);
