@@ -1769,7 +1769,7 @@ K10S_D uint64_t readlane_u64(uint64_t v, uint32_t j) {
 // no processed front lane dominates is itself in the front (every lane above it is in the front or
 // dominated by a front lane above it, which would dominate it too); it then marks the lanes below it
 // that it dominates.  One iteration per front node.  Returns the front's size.
-K10S_D uint32_t fr_block(uint64_t* fv, uint8_t* fi, uint32_t b, uint64_t x, uint64_t* front_out = nullptr) {
+K10S_D uint32_t fr_block(uint64_t* fv, uint8_t* fi, uint32_t b, uint64_t x) {
     const uint32_t lane = (uint32_t)lane_id();
     const uint32_t cpu = (uint32_t)(x >> K10S_PK_SHIFT);
     const uint64_t ram = x & K10S_PK_RAM;
@@ -1790,12 +1790,10 @@ K10S_D uint32_t fr_block(uint64_t* fv, uint8_t* fi, uint32_t b, uint64_t x, uint
         fi[b * K10S_FR_K + rank] = (uint8_t)lane;
     }
     if (lane >= nf && lane < K10S_FR_K) fv[b * K10S_FR_K + lane] = 0;   // unused slots fit nothing
-    if (front_out) *front_out = front;
     return nf;
 }
 #endif
-// Rebuild every marked block's front; returns the entries read.  (The device rebuilds the marked
-// blocks inside front_scan, with the scan's own slot loads in flight.)
+// Rebuild every marked block's front; returns the entries read.
 K10S_HD_NOINL uint32_t fr_refresh(Ctx& c) {
     uint64_t dirty = uniform_u64(c.H().fr_dirty);
     if (dirty == 0) return 0;
@@ -1873,21 +1871,14 @@ K10S_HD_NOINL uint32_t fr_refresh(Ctx& c) {
 K10S_HD_NOINL int front_scan(Ctx& c, uint32_t rc, uint64_t rr, int32_t* chosen, uint32_t* nread) {
     const uint32_t N = uniform_u32(c.S().n_nodes);
     const uint32_t NB = (N + 63u) >> 6;
-#if !K10S_DEVICE
-    const uint32_t rebuilt = fr_refresh(c);
-#endif
     const uint64_t over = uniform_u64(c.H().fr_over);
     const uint64_t* fv = c.V().fr_val();
     const uint8_t* fi = c.V().fr_idx();
     const uint64_t* sn = c.V().s_node();
     uint32_t reads = NB * K10S_FR_K;
-#if !K10S_DEVICE
-    reads += rebuilt;
-#endif
     uint64_t best_key = 0;
     int32_t best_n = -1;
 #if K10S_DEVICE
-    (void)over;
     const uint32_t lane = (uint32_t)lane_id();
     rc = uniform_u32(rc);
     rr = uniform_u64(rr);
@@ -1896,9 +1887,6 @@ K10S_HD_NOINL int front_scan(Ctx& c, uint32_t rc, uint64_t rr, int32_t* chosen, 
     const float fr = __builtin_fmaf((float)(uint32_t)(rr >> 32), 4294967296.0f, (float)(uint32_t)rr);
     double bs = -__builtin_inf();
     int32_t bn = -1;
-    uint64_t* fvw = c.V().fr_val();
-    uint8_t* fiw = c.V().fr_idx();
-    // lane b: block b's slots as stored (a marked block's are replaced below)
     uint64_t x[K10S_FR_K];
     uint64_t ix = 0;
     if (lane < NB) {
@@ -1913,57 +1901,6 @@ K10S_HD_NOINL int front_scan(Ctx& c, uint32_t rc, uint64_t rr, int32_t* chosen, 
     } else {
         K10S_UNROLL
         for (int k = 0; k < K10S_FR_K; k++) x[k] = 0;
-    }
-    // the marked blocks (fr_mark): rebuilt four per memory round trip (the slot loads above are in
-    // flight meanwhile); the stored slots are updated for later scans, and lane b takes block b's new
-    // slots from the front's lanes directly
-    uint64_t dirty = uniform_u64(c.H().fr_dirty);
-    uint64_t ovr = uniform_u64(c.H().fr_over);
-    if (dirty) {
-        while (dirty) {
-            uint32_t bsk[4];
-            uint64_t xs[4];
-            uint32_t kk = 0;
-            K10S_UNROLL
-            for (uint32_t i = 0; i < 4; i++) {
-                bsk[i] = 0;
-                xs[i] = 0;
-                if (dirty) {
-                    const uint32_t b = (uint32_t)__builtin_ctzll(dirty);
-                    dirty &= dirty - 1;
-                    bsk[i] = b;
-                    const uint32_t n = 64u * b + lane;
-                    if (n < N) xs[i] = sn[n];
-                    reads += N - 64u * b < 64u ? N - 64u * b : 64u;
-                    kk = i + 1;
-                }
-            }
-            K10S_UNROLL
-            for (uint32_t i = 0; i < 4; i++) {
-                if (i < kk) {
-                    uint64_t fm = 0;
-                    const uint32_t nf = fr_block(fvw, fiw, bsk[i], xs[i], &fm);
-                    ovr = nf > K10S_FR_K ? (ovr | (1ull << bsk[i])) : (ovr & ~(1ull << bsk[i]));
-                    const bool mine = lane == bsk[i];
-                    K10S_UNROLL
-                    for (int r = 0; r < K10S_FR_K; r++) {   // the front's lanes in ascending order
-                        uint64_t v = 0;
-                        uint32_t off = 0;
-                        if (fm) {
-                            off = (uint32_t)__builtin_ctzll(fm);
-                            fm &= fm - 1;
-                            v = readlane_u64(xs[i], off);
-                        }
-                        if (mine) {
-                            x[r] = v;
-                            ix = (ix & ~(0xFFull << (8 * r))) | ((uint64_t)off << (8 * r));
-                        }
-                    }
-                }
-            }
-        }
-        c.H().fr_dirty = 0;
-        c.H().fr_over = ovr;
     }
     auto consider = [&](uint64_t e, int32_t n) {   // a fitting entry's exact score into the lane best
         const NcEnt v = nc_unpack(e);
@@ -1985,32 +1922,15 @@ K10S_HD_NOINL int front_scan(Ctx& c, uint32_t rc, uint64_t rr, int32_t* chosen, 
         if (x[k] != 0 && !scan_screen(v.cpu, v.ram, fa, fr, T))
             consider(x[k], (int32_t)(64u * lane + (uint32_t)((ix >> (8 * k)) & 0xFFu)));
     }
-    // blocks whose front overflowed the slots: the whole block, one node per lane, four blocks per
-    // memory round trip
-    for (uint64_t ov = ovr; ov;) {
-        uint32_t ob[4];
-        uint64_t oe[4];
-        uint32_t kk = 0;
-        K10S_UNROLL
-        for (uint32_t i = 0; i < 4; i++) {
-            ob[i] = 0;
-            oe[i] = 0;
-            if (ov) {
-                const uint32_t b = (uint32_t)__builtin_ctzll(ov);
-                ov &= ov - 1;
-                ob[i] = b;
-                const uint32_t n = 64u * b + lane;
-                if (n < N) oe[i] = sn[n];
-                reads += N - 64u * b < 64u ? N - 64u * b : 64u;
-                kk = i + 1;
-            }
-        }
-        K10S_UNROLL
-        for (uint32_t i = 0; i < 4; i++) {
-            if (i < kk) {
-                const NcEnt v = nc_unpack(oe[i]);
-                if (oe[i] != 0 && !scan_screen(v.cpu, v.ram, fa, fr, T)) consider(oe[i], (int32_t)(64u * ob[i] + lane));
-            }
+    // blocks whose front overflowed the slots: the whole block, one node per lane
+    for (uint64_t ov = over; ov; ov &= ov - 1) {
+        const uint32_t b = (uint32_t)__builtin_ctzll(ov);
+        const uint32_t n = 64u * b + lane;
+        reads += N - 64u * b < 64u ? N - 64u * b : 64u;
+        if (n < N) {
+            const uint64_t e = sn[n];
+            const NcEnt v = nc_unpack(e);
+            if (e != 0 && !scan_screen(v.cpu, v.ram, fa, fr, T)) consider(e, (int32_t)n);
         }
     }
     best_key = bn >= 0 ? score_key(bs) : 0;
@@ -3032,8 +2952,9 @@ K10S_HD int32_t cycle_attempt(Ctx& c, double t, QInfo q, int32_t pick, double& c
         // rebuilding the blocks that the finishes since the last cycle marked would cost more than
         // its full scans (backlog +9 %, profiles/r06_g6_fronts_ab.json)
         if (st < 0 && K10S_FRONT && !PLUG && !TILE && c.Ly().front && w == 1.0 && rc > 0 && rr > 0) {
+            nread += fr_refresh(c);
             uint32_t fr = 0;
-            st = front_scan(c, rc, rr, &chosen, &fr);   // (rebuilds the marked blocks first)
+            st = front_scan(c, rc, rr, &chosen, &fr);
             nread += fr;
         }
         if (st < 0) {
