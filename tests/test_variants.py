@@ -8,7 +8,10 @@ panic in that workload).  Variants:
 * prof        K10S_PROF=1: cycle attribution (wider header, 106 VGPRs, 4 waves/SIMD, per-lane
               source dispatch in the compiled loop);
 * exec_check  K10S_EXEC_CHECK=3: EXEC guards at every lane-parallel helper and bounded sift loops (a
-              guard that fires stops the replica with K10S_ERR_EXEC_GUARD: none may)."""
+              guard that fires stops the replica with K10S_ERR_EXEC_GUARD: none may);
+* full_scan   K10S_FRONT=0: the screened full scan instead of the per-block Pareto fronts, on a C3
+              slice (4,096 nodes and no autoscaler, so the product build's fronts are on); every row
+              must match except the engine-only node-cache entries read (counter 16)."""
 import json
 import os
 import subprocess
@@ -21,22 +24,35 @@ import parity
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SLICE = ["c5_autoscaled", "64", "4096", "16384", "20000"]
-VARIANTS = {"prof": "build/libk10s_prof.so", "exec_check": "build/libk10s_EXEC_CHECK3.so"}
+SLICE_C3 = ["c3", "64", "4096", "16384", "20000"]
+VARIANTS = {"prof": ("build/libk10s_prof.so", SLICE), "exec_check": ("build/libk10s_EXEC_CHECK3.so", SLICE),
+            "full_scan": ("build/libk10s_FRONT0.so", SLICE_C3)}
+NODES_READ = 16   # K10S_C_NODES_READ: engine-only, differs by scan design
 
 
-def _run(lib=None, timeout=240):
+def _run(lib=None, timeout=240, slice_=SLICE):
     env = dict(os.environ)
     if lib:
         env["K10S_LIB"] = lib
-    p = subprocess.run([sys.executable, "-u", os.path.join(REPO, "tools", "variant_run.py"), *SLICE], cwd=REPO, env=env,
+    p = subprocess.run([sys.executable, "-u", os.path.join(REPO, "tools", "variant_run.py"), *slice_], cwd=REPO, env=env,
                        capture_output=True, text=True, timeout=timeout)
     assert p.returncode == 0, p.stderr[-3000:]
     return json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][-1])
 
 
+_PRODUCT = {}
+
+
+def _product(slice_):
+    key = tuple(slice_)
+    if key not in _PRODUCT:
+        _PRODUCT[key] = _run(slice_=slice_)
+    return _PRODUCT[key]
+
+
 @pytest.fixture(scope="module")
 def product_rows():
-    return _run()
+    return _product(SLICE)
 
 
 @pytest.mark.gpu
@@ -66,11 +82,12 @@ def test_product_slice_matches_oracle(product_rows):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("variant", sorted(VARIANTS))
-def test_variant_build_matches_product(product_rows, variant):
-    lib = VARIANTS[variant]
+def test_variant_build_matches_product(variant):
+    lib, slice_ = VARIANTS[variant]
     if not os.path.exists(os.path.join(REPO, lib)):
         pytest.fail(f"{lib} not built (__graft_entry__.build() builds it)")
-    got = _run(lib)
+    product_rows = _product(slice_)
+    got = _run(lib, slice_=slice_)
     assert got["engine"] != product_rows["engine"]
     # the library is the variant of THESE sources, not a stale one from an earlier build
     from kubernetriks_amd.build import build_id
@@ -78,5 +95,9 @@ def test_variant_build_matches_product(product_rows, variant):
     extra = [x for x, out in ge.VARIANT_BUILDS if lib.endswith(out)][0]
     assert got["engine"].endswith("build " + build_id(extra)), (got["engine"], build_id(extra))
     for r, (a, b) in enumerate(zip(got["rows"], product_rows["rows"])):
+        if variant == "full_scan":
+            a, b = dict(a), dict(b)
+            a["counters"] = a["counters"][:NODES_READ] + a["counters"][NODES_READ + 1:]
+            b["counters"] = b["counters"][:NODES_READ] + b["counters"][NODES_READ + 1:]
         assert a == b, (variant, r, a, b)
     assert sum(x["counters"][14] for x in got["rows"]) == sum(x["counters"][14] for x in product_rows["rows"])
