@@ -220,7 +220,8 @@ def pmc_traffic(workload, R, nodes, pods, pruned, score_plugins, engine):
 def roofline(entry_b, extra_b, scanned, nread, attempts, placements, launches, kernel_ms, traffic):
     """The `roofline` object of k10s_run_kernel, per launch.  `achieved` / `frac` count the bytes the
     kernel reads and writes for the scans: per node-cache entry READ (nodes_read: every scanned node,
-    plus the cycle tiles' shared fit passes, whose failed attempts read no entry of their own) the
+    plus the cycle tiles' shared fit passes, whose failed attempts read no entry of their own; with the
+    per-block fronts the front slots, the rebuilt blocks and the overflowing blocks) the
     entry's size (8 B packed cpu << 40 | ram, 12 B wide u32 + u64; + 12 B of capacity for
     MostAllocated), 12 B per attempt (the pod's request) and one entry per placement (the
     reservation).  `survey_pricing` is SURVEY.md 8(d)'s algorithmic volume of the serial reference

@@ -55,10 +55,11 @@ for step in "$@"; do
         || { echo "BENCH FAILED"; tail -20 "$O/bench$n.err"; exit 1; }
       tail -c 600 "$O/bench$n.json"; echo ;;
     stats)
-      (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/stats" -o run \
-        -- python3 "$R/bench.py" $(args_of "$rest") > "$O/stats.json" 2> "$O/stats.err") \
-        || { echo "STATS FAILED"; tail -20 "$O/stats.err"; exit 1; }
-      find "$O/stats" -name "*kernel_stats.csv" -exec cat {} \; ;;
+      n=$(ls -d "$O"/stats*/ 2>/dev/null | wc -l); sd=stats; [ "$n" -gt 0 ] && sd=stats$n
+      (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/$sd" -o run \
+        -- python3 "$R/bench.py" $(args_of "$rest") > "$O/$sd.json" 2> "$O/$sd.err") \
+        || { echo "STATS FAILED"; tail -20 "$O/$sd.err"; exit 1; }
+      find "$O/$sd" -name "*kernel_stats.csv" -exec cat {} \; ;;
     pmc)
       name=${rest%%:*}; r2=${rest#*:}; ctrs=${r2%%:*}; bargs=""; [[ "$r2" == *:* ]] && bargs=${r2#*:}
       (cd /tmp && timeout -k 10 -s KILL 600 rocprofv3 --kernel-trace --output-format csv -d "$O/pmc_$name" -o run \
