@@ -1760,6 +1760,9 @@ K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const ui
 // and takes the wave's (score, index) maximum.  The result is the full scan's by the argument above;
 // entries read = slots + rebuilt and overflowing blocks' nodes.
 #define K10S_FR_K 8
+#ifndef K10S_FRONT_COMPACT
+#define K10S_FRONT_COMPACT 1   // A/B knob: 0 = one exact-scoring branch per slot any lane kept
+#endif
 #if K10S_DEVICE
 K10S_D uint64_t readlane_u64(uint64_t v, uint32_t j) {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)j) << 32) |
@@ -1916,12 +1919,31 @@ K10S_HD_NOINL int front_scan(Ctx& c, uint32_t rc, uint64_t rr, int32_t* chosen, 
     float lu = bn >= 0 ? screen_u(bs) : __builtin_inff();
     const float thr = __builtin_bit_cast(float, uniform_u32(__builtin_bit_cast(uint32_t, wave_min_f32(lu))));
     const float T = thr + K10S_SCREEN_EPS;   // +inf when no lane scored: screens nothing out
+#if K10S_FRONT_COMPACT
+    // the screen of slots 1..7 first, then one exact scoring per round for each lane's next surviving
+    // slot (rounds = the most survivors any lane has, not the slots any lane kept)
+    uint32_t sm = 0;
+    K10S_UNROLL
+    for (int k = 1; k < K10S_FR_K; k++) {
+        const NcEnt v = nc_unpack(x[k]);
+        sm |= (x[k] != 0 && !scan_screen(v.cpu, v.ram, fa, fr, T)) ? 1u << k : 0u;
+    }
+    while (__ballot(sm != 0u)) {
+        const uint32_t k = sm ? (uint32_t)__builtin_ctz(sm) : 0u;
+        uint64_t e = x[1];
+        K10S_UNROLL
+        for (int q = 2; q < K10S_FR_K; q++) e = k == (uint32_t)q ? x[q] : e;
+        if (sm) consider(e, (int32_t)(64u * lane + (uint32_t)((ix >> (8u * k)) & 0xFFu)));
+        sm &= sm - 1u;
+    }
+#else
     K10S_UNROLL
     for (int k = 1; k < K10S_FR_K; k++) {
         const NcEnt v = nc_unpack(x[k]);
         if (x[k] != 0 && !scan_screen(v.cpu, v.ram, fa, fr, T))
             consider(x[k], (int32_t)(64u * lane + (uint32_t)((ix >> (8 * k)) & 0xFFu)));
     }
+#endif
     // blocks whose front overflowed the slots (about 4 of 64 blocks per C3 scan): the whole block,
     // one node per lane, four blocks per memory round trip
     for (uint64_t ov = over; ov;) {
@@ -1939,11 +1961,32 @@ K10S_HD_NOINL int front_scan(Ctx& c, uint32_t rc, uint64_t rr, int32_t* chosen, 
                 if (ob[i] < N) oe[i] = sn[ob[i]];
             }
         }
+#if K10S_FRONT_COMPACT
+        uint32_t om = 0;
+        K10S_UNROLL
+        for (int i = 0; i < 4; i++) {
+            const NcEnt v = nc_unpack(oe[i]);
+            om |= (oe[i] != 0 && !scan_screen(v.cpu, v.ram, fa, fr, T)) ? 1u << i : 0u;
+        }
+        while (__ballot(om != 0u)) {
+            const uint32_t i = om ? (uint32_t)__builtin_ctz(om) : 0u;
+            uint64_t e = oe[0];
+            uint32_t n = ob[0];
+            K10S_UNROLL
+            for (int q = 1; q < 4; q++) {
+                e = i == (uint32_t)q ? oe[q] : e;
+                n = i == (uint32_t)q ? ob[q] : n;
+            }
+            if (om) consider(e, (int32_t)n);
+            om &= om - 1u;
+        }
+#else
         K10S_UNROLL
         for (int i = 0; i < 4; i++) {
             const NcEnt v = nc_unpack(oe[i]);
             if (oe[i] != 0 && !scan_screen(v.cpu, v.ram, fa, fr, T)) consider(oe[i], (int32_t)ob[i]);
         }
+#endif
     }
     best_key = bn >= 0 ? score_key(bs) : 0;
     best_n = bn;
