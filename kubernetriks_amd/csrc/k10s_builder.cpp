@@ -821,7 +821,7 @@ Layout make_layout(const HostScenario& hs, const k10s_capacities& caps, bool all
     const uint64_t wide = L.packed ? 0 : 1;
     L.s_node = take(L.packed ? 8 * N : 0);
     // per-block fronts of the packed cache (k10s_engine.h front_scan): up to 64 blocks of 64 nodes
-    L.front = (L.packed && N <= 4096) ? 1u : 0u;
+    L.front = (L.packed && N > 512 && N <= 4096) ? 1u : 0u;
     const uint64_t nbf = L.front ? (N + 63) / 64 : 0;
     L.fr_val = take(8 * 8 * nbf);
     L.fr_idx = take(8 * nbf);

@@ -9,12 +9,15 @@ free cpu and free ram — K10S_FR_K = 8 slots per block, a block with a larger f
 * Host and GPU: clusters built so the fronts overflow (staircases), sit at the slot count, tie
   (identical nodes), end in a ragged block, and lose and regain nodes mid-run, through the event loop
   against the oracle event for event; the host run checks the fronts cut the entries read, and that
-  a cache over 4,096 nodes (fronts off) reads every node per attempt.
+  a cache over 4,096 nodes or up to 512 (fronts off) reads every node per attempt; random scenarios
+  over 520-1,119 nodes.
 """
+import os
 import random
 
 import pytest
 
+import gen
 import parity
 from hostcheck_bridge import HostEngine
 from kubernetriks_amd.scenario import GenericClusterTrace, GenericWorkloadTrace, Node, Pod, SimulationConfig, scenario_text
@@ -158,7 +161,7 @@ def test_front_clusters_in_the_event_loop(backend, kind):
 @pytest.mark.parametrize("N", [4000, 4033, 4095])
 def test_front_ragged_last_block(backend, N):
     if backend == "host":
-        N = N % 640 + 65
+        N = 513 + N % 100   # 513, 546, 608: ragged, and above the 512 nodes below which fronts are off
     cpu, ram = node_sets(N, 5)["front9"]
     scn = _scenario(cpu, ram, 300 if backend == "gpu" else 120, seed=N)
     od, eng = parity.run_pair(_engine(backend), scn, max_time=50000.0)
@@ -170,7 +173,7 @@ def test_front_ragged_last_block(backend, N):
 def test_front_node_removal_and_return(backend, kind):
     """Removed nodes' entries drop to (0, 0) and their blocks rebuild; returning nodes land at new
     cache positions (new names sort after the old ones) and rebuild theirs."""
-    N = 2048 if backend == "gpu" else 400
+    N = 2048 if backend == "gpu" else 576
     cpu, ram = node_sets(N, 13)[kind]
     scn = _scenario(cpu, ram, 300 if backend == "gpu" else 140, seed=3, churn=True)
     od, eng = parity.run_pair(_engine(backend), scn, max_time=50000.0)
@@ -180,7 +183,8 @@ def test_front_node_removal_and_return(backend, kind):
 
 def test_fronts_read_fewer_entries_host():
     """c3_like at 1,024 nodes: the fronts read a fraction of the cache per attempt; the same cluster
-    over 4,096 nodes of capacity (one extra node: 4,097, no fronts) reads it all."""
+    over 4,096 nodes of capacity (one extra node: 4,097, no fronts) reads it all, and so does one of
+    512 nodes (fronts only above 512)."""
     rng = random.Random(1)
     cpu, ram = node_sets(1024, 2)["c3_like"]
     scn = _scenario(cpu, ram, 200, seed=9)
@@ -195,3 +199,32 @@ def test_fronts_read_fewer_entries_host():
     assert parity.compare(od2, eng2, log=False) == []
     k2 = eng2.results()[0]["counters"]
     assert k2["nodes_read"] >= 4097 * k2["attempts"], k2
+    # up to 512 nodes a full scan is one memory round trip: no fronts (k10s_builder.cpp make_layout)
+    scn3 = _scenario(cpu[:512], ram[:512], 60, seed=9)
+    od3, eng3 = parity.run_pair(HostEngine, scn3, max_time=50000.0, log=False)
+    assert parity.compare(od3, eng3, log=False) == []
+    k3 = eng3.results()[0]["counters"]
+    assert k3["nodes_read"] >= 512 * k3["attempts"], k3
+
+
+# Random scenarios (tests/gen.py: mixed node sizes, removals, default groups, integer and real
+# times, conditional move) over 520-1,119 nodes, so the fronts are on.  K10S_FRONT_FUZZ_GPU_SEEDS=N
+# widens the GPU sweep.
+FRONT_FUZZ_GPU = list(range(int(os.environ.get("K10S_FRONT_FUZZ_GPU_SEEDS", "24"))))
+
+
+def _front_fuzz(backend, seed):
+    scn = gen.random_scenario(50_000 + seed, n_pods=300, n_nodes=520 + (seed * 37) % 600)
+    od, eng = parity.run_pair(_engine(backend), scn, max_time=20000.0)
+    assert parity.compare(od, eng) == [], seed
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_front_fuzz_host(seed):
+    _front_fuzz("host", seed)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", FRONT_FUZZ_GPU)
+def test_front_fuzz_gpu(seed):
+    _front_fuzz("gpu", seed)
