@@ -238,6 +238,10 @@ def roofline(entry_b, extra_b, scanned, nread, attempts, placements, launches, k
             "bytes_per_launch": read, "node_entry_bytes": int(entry_b),
             "pricing": (f"bytes read: {int(entry_b + extra_b)} B per node-cache entry read (nodes_read) + 12 B per "
                         f"attempt + {int(entry_b)} B per placement"),
+            "note": ("the per-block Pareto fronts (DESIGN.md section 3) read a fraction of the node cache per "
+                     "placement, so the priced bytes and frac fall as the kernel gets faster; it is bound by each "
+                     "replica's chain of dependent memory round trips, not by bandwidth (traffic_frac, DESIGN.md "
+                     "section 6)"),
             "survey_pricing": {"bytes_per_launch": survey, "equivalent_GBps": survey / sec / 1e9,
                                "note": "SURVEY.md 8(d): 12 B per node per attempt + 12 B per attempt + 12 B per "
                                        "placement of the serial reference; a work rate, not a bandwidth"}}
