@@ -30,9 +30,11 @@ GPU, and exits with their status; under torch.distributed.run WORLD_SIZE must eq
 
 Prints ONE JSON line (rank 0).  `value` = placements of all ranks / max-over-ranks wall time of
 the timed steps.  `roofline`: the dominant kernel is k10s_run_kernel (the whole event loop incl. the
-scheduling scans); algorithmic bytes per launch = Σ_attempts (12·|node cache| + 12) + 12·placements
-(SURVEY.md §8(d)), divided by the launch's HIP-event time, against the 8 TB/s HBM3E peak.  The packed
-node cache reads 8 B per node for the same work; that rate is `achieved_physical` / `frac_physical`.
+scheduling scans); its bytes per launch are the bytes it reads for the scans (8 B per node-cache
+entry read, `nodes_read`, + 12 B per attempt + 8 B per placement; roofline() below), divided by the
+launch's HIP-event time measured on the engine's stream, against the 8 TB/s HBM3E peak.  SURVEY.md
+§8(d)'s 12 B per node per attempt of the serial reference is reported beside it as a work rate
+(`survey_pricing`), and `traffic` is the PMC-measured HBM bytes of the same build when committed.
 `cpu_baseline`: the repo's CPU oracle (a string-keyed restatement of the reference, kind "port";
 the Rust reference cannot be built here), one process per usable host core, each running one
 replica of the same workload to completion.
