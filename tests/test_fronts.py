@@ -228,3 +228,25 @@ def test_front_fuzz_host(seed):
 @pytest.mark.parametrize("seed", FRONT_FUZZ_GPU)
 def test_front_fuzz_gpu(seed):
     _front_fuzz("gpu", seed)
+
+
+@pytest.mark.parametrize("kind", ["staircase64", "front9", "c3_like"])
+def test_front_invariant_between_events_host(kind):
+    """White-box: at checkpoints through a run (after budgeted launches of a few events), every block
+    not marked stale holds exactly its index-aware front in its slots and the right overflow bit
+    (tests/hostcheck hc_front_check recomputes each block from the node cache)."""
+    import ctypes
+    from hostcheck_bridge import lib as hclib
+    L = hclib()
+    L.hc_front_check.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+    L.hc_front_check.restype = ctypes.c_int
+    cpu, ram = node_sets(640, 23)[kind]
+    scn = _scenario(cpu, ram, 160, seed=5, churn=True)
+    eng = HostEngine(scn, 1)
+    checked = 0
+    for t in range(1, 400, 7):
+        eng.step_until_time(float(t), 13)
+        r = L.hc_front_check(eng._h, 0)
+        assert r >= 0, (kind, t, -r - 1)
+        checked += r
+    assert checked > 0
