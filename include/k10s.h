@@ -380,6 +380,11 @@ int32_t k10s_engine_name_bounds(const k10s_engine* e, uint32_t* group_bound, uin
    (K10S_FIFO_OFF when off), the other fields as given at create.  *regrows (may be NULL) = batches
    recompiled by regrow since create. */
 int32_t k10s_engine_capacities(const k10s_engine* e, k10s_capacities* out, uint32_t* regrows);
+/* Test support: checks replica `replica`'s per-block Pareto fronts of the packed node cache against
+   its node cache (every block not marked stale holds exactly its front).
+   *result = blocks checked, -(1 + the first block that breaks it), or 0 when the batch keeps no
+   fronts (a cache of up to 512 or more than 4,096 nodes, or not packed). */
+int32_t k10s_engine_check_fronts(const k10s_engine* e, uint32_t replica, int32_t* result);
 
 /* Name tables of the compiled scenario (index -> name), for mapping logs back to names.  The
    returned strings belong to the engine and stay valid until the next run / sync that regrows the

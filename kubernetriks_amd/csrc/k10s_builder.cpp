@@ -823,8 +823,8 @@ Layout make_layout(const HostScenario& hs, const k10s_capacities& caps, bool all
     // per-block fronts of the packed cache (k10s_engine.h front_scan): up to 64 blocks of 64 nodes
     L.front = (L.packed && N > 512 && N <= 4096) ? 1u : 0u;
     const uint64_t nbf = L.front ? (N + 63) / 64 : 0;
-    L.fr_val = take(8 * 8 * nbf);
-    L.fr_idx = take(8 * nbf);
+    L.fr_val = take(8 * K10S_FR_K * nbf);
+    L.fr_idx = take(K10S_FR_K * nbf);
     L.s_cpu = take(wide * 4 * N);
     L.s_ram = take(wide * 8 * N);
     L.s_present = take(8 * (uint64_t)L.words_nodes);

@@ -1759,7 +1759,7 @@ K10S_HD int schedule_scan(const uint32_t* s_cpu, const uint64_t* s_ram, const ui
 // like the screened scan (the first slot exactly, the rest screened against the wave's threshold),
 // and takes the wave's (score, index) maximum.  The result is the full scan's by the argument above;
 // entries read = slots + rebuilt and overflowing blocks' nodes.
-#define K10S_FR_K 8
+// (K10S_FR_K, the front slots per block: k10s_state.h)
 #ifndef K10S_FRONT_COMPACT
 #define K10S_FRONT_COMPACT 1   // A/B knob: 0 = one exact-scoring branch per slot any lane kept
 #endif

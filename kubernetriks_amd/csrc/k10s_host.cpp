@@ -12,6 +12,7 @@
 
 #include "../../include/k10s.h"
 #include "k10s_builder.h"
+#include "k10s_front_check.h"
 #include "k10s_results.h"
 
 using namespace k10s;
@@ -684,6 +685,23 @@ int32_t k10s_engine_name_bounds(const k10s_engine* e, uint32_t* group_bound, uin
     if (!e || !group_bound || !ca_bound) return set_err(K10S_E_INVALID, "null");
     *group_bound = e->hs.group_bound;
     *ca_bound = e->hs.ca_bound;
+    return K10S_OK;
+}
+int32_t k10s_engine_check_fronts(const k10s_engine* e, uint32_t replica, int32_t* result) {
+    if (!e || !result) return set_err(K10S_E_INVALID, "null");
+    RepHdr h;
+    if (int32_t rc = read_hdr(e, replica, h)) return rc;
+    *result = 0;
+    if (!e->L.front) return K10S_OK;
+    const uint32_t N = e->dsc.n_nodes;
+    const uint32_t nb = std::min<uint32_t>((N + 63u) / 64u, 64u);
+    std::vector<uint64_t> sn(N), fv((size_t)nb * K10S_FR_K);
+    std::vector<uint8_t> fi((size_t)nb * K10S_FR_K);
+    const uint8_t* base = e->d_state + (size_t)replica * e->L.stride;
+    HIPCHK(hipMemcpy(sn.data(), base + e->L.s_node, 8 * (size_t)N, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(fv.data(), base + e->L.fr_val, 8 * fv.size(), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(fi.data(), base + e->L.fr_idx, fi.size(), hipMemcpyDeviceToHost));
+    *result = k10s_front_check(sn.data(), fv.data(), fi.data(), N, h.fr_dirty, h.fr_over, K10S_FR_K);
     return K10S_OK;
 }
 uint32_t k10s_engine_node_entry_bytes(const k10s_engine* e) { return e ? (e->L.packed ? 8u : 12u) : 0u; }

@@ -206,6 +206,8 @@ struct alignas(16) FqRing {
 };
 static_assert(sizeof(FqRing) == 32, "FqRing must be 32 B");
 
+#define K10S_FR_K 8   // front slots per 64-node block of the packed node cache (k10s_engine.h front_scan)
+
 struct RepHdr {
     double clock;            // clock, next_seq and error_code: one 16-B LDS read in emit
     uint32_t next_seq;

@@ -146,10 +146,11 @@ def _decl(L, prefix: str):
         "default_params": (i32, [vp, P(ReplicaParams)]),
         "name_bounds": (i32, [vp, P(u32), P(u32)]),
         "capacities": (i32, [vp, P(Capacities), P(u32)]),
+        "check_fronts": (i32, [vp, u32, P(ctypes.c_int32)]),
     }
     out = {}
     for name, (res, args) in sig.items():
-        if name in ("node_entry_bytes", "name_bounds", "capacities") and not hasattr(L, prefix + name):
+        if name in ("node_entry_bytes", "name_bounds", "capacities", "check_fronts") and not hasattr(L, prefix + name):
             continue   # a library from an earlier round (A/B tooling)
         f = getattr(L, prefix + name)
         f.restype = res
@@ -195,6 +196,15 @@ class EngineBase:
         c, n = Capacities(), ctypes.c_uint32()
         self._check(self._fn["capacities"](self._h, ctypes.byref(c), ctypes.byref(n)))
         return {f: int(getattr(c, f)) for f, _ in Capacities._fields_}, int(n.value)
+
+    def check_fronts(self, r: int = 0) -> int:
+        """Test support (include/k10s.h k10s_engine_check_fronts): blocks of replica r whose front
+        slots were checked against the node cache; raises if one is wrong; 0 without fronts."""
+        out = ctypes.c_int32()
+        self._check(self._fn["check_fronts"](self._h, r, ctypes.byref(out)))
+        if out.value < 0:
+            raise AssertionError(f"replica {r}: block {-out.value - 1} does not hold its front")
+        return int(out.value)
 
     @property
     def node_names(self) -> List[str]:

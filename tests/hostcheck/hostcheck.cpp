@@ -11,6 +11,7 @@
 
 #include "../../kubernetriks_amd/csrc/k10s_builder.h"
 #include "../../kubernetriks_amd/csrc/k10s_engine.h"
+#include "../../kubernetriks_amd/csrc/k10s_front_check.h"
 #include "../../kubernetriks_amd/csrc/k10s_results.h"
 
 using namespace k10s;
@@ -297,49 +298,14 @@ extern "C" int hc_aq_mode(void* p, uint32_t r, uint32_t* sorted, uint32_t* n) {
     return 0;
 }
 
-// The fronts' invariant (k10s_engine.h fr_block / fr_refresh), for tests/test_fronts.py: every block
-// that is not marked stale holds exactly its index-aware front in its slots (the first K10S_FR_K in
-// node order, unused slots 0) and its overflow bit says whether the front is longer.  Returns the
-// number of blocks checked, or -(1 + the first block that breaks it); 0 when the layout has no fronts.
-extern "C" int hc_front_check(void* p, uint32_t r) {
+// The fronts' invariant (k10s_front_check.h), the test-only mirror of k10s_engine_check_fronts.
+extern "C" int hc_check_fronts(void* p, uint32_t r, int32_t* result) {
     HC* h = (HC*)p;
     Rep v = make_rep(h->state.data(), h->L, r);
-    if (!h->L.front) return 0;
-    const uint32_t N = h->sc.n_nodes;
-    const uint64_t* sn = v.s_node();
-    const uint64_t* fv = v.fr_val();
-    const uint8_t* fi = v.fr_idx();
-    const uint64_t dirty = v.h()->fr_dirty, over = v.h()->fr_over;
-    int checked = 0;
-    for (uint32_t b = 0; 64u * b < N; b++) {
-        if ((dirty >> b) & 1ull) continue;
-        const uint32_t lo = 64u * b, hi = lo + 64u < N ? lo + 64u : N;
-        uint32_t mem[64];
-        uint32_t nf = 0;
-        for (uint32_t k = hi; k-- > lo;) {
-            const uint64_t x = sn[k];
-            if (x == 0) continue;
-            const NcEnt e = nc_unpack(x);
-            bool dom = false;
-            for (uint32_t q = 0; q < nf && !dom; q++) {
-                const NcEnt w = nc_unpack(sn[mem[q]]);
-                dom = w.cpu >= e.cpu && w.ram >= e.ram;
-            }
-            if (!dom) mem[nf++] = k;
-        }
-        bool ok = ((over >> b) & 1ull) == (nf > K10S_FR_K ? 1ull : 0ull);
-        for (uint32_t s2 = 0; s2 < K10S_FR_K && ok; s2++) {
-            if (s2 < nf) {
-                const uint32_t k = mem[nf - 1 - s2];
-                ok = fv[b * K10S_FR_K + s2] == sn[k] && fi[b * K10S_FR_K + s2] == (uint8_t)(k - lo);
-            } else {
-                ok = fv[b * K10S_FR_K + s2] == 0;
-            }
-        }
-        if (!ok) return -(1 + (int)b);
-        checked++;
-    }
-    return checked;
+    *result = h->L.front ? k10s_front_check(v.s_node(), v.fr_val(), v.fr_idx(), h->sc.n_nodes, v.h()->fr_dirty,
+                                            v.h()->fr_over, K10S_FR_K)
+                         : 0;
+    return 0;
 }
 
 // The host score (bit-identical to the device's), for tests/test_scan_adversarial.py.

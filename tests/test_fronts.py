@@ -230,23 +230,22 @@ def test_front_fuzz_gpu(seed):
     _front_fuzz("gpu", seed)
 
 
+@pytest.mark.parametrize("backend", BACKENDS)
 @pytest.mark.parametrize("kind", ["staircase64", "front9", "c3_like"])
-def test_front_invariant_between_events_host(kind):
-    """White-box: at checkpoints through a run (after budgeted launches of a few events), every block
-    not marked stale holds exactly its index-aware front in its slots and the right overflow bit
-    (tests/hostcheck hc_front_check recomputes each block from the node cache)."""
-    import ctypes
-    from hostcheck_bridge import lib as hclib
-    L = hclib()
-    L.hc_front_check.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
-    L.hc_front_check.restype = ctypes.c_int
-    cpu, ram = node_sets(640, 23)[kind]
-    scn = _scenario(cpu, ram, 160, seed=5, churn=True)
-    eng = HostEngine(scn, 1)
+def test_front_invariant_between_events(backend, kind):
+    """White-box: at checkpoints through a run (launches of 13 events), every block not marked stale
+    holds exactly its index-aware front in its slots and the right overflow bit, recomputed from the
+    replica's node cache (k10s_engine_check_fronts; the host engine's hc_check_fronts); the run still
+    equals the oracle."""
+    N = 2048 if backend == "gpu" else 640
+    cpu, ram = node_sets(N, 23)[kind]
+    scn = _scenario(cpu, ram, 300 if backend == "gpu" else 160, seed=5, churn=True)
+    eng = _engine(backend)(scn, 2, caps=parity.parity_caps(True, gauges=parity.GAUGE_ROWS))
     checked = 0
     for t in range(1, 400, 7):
         eng.step_until_time(float(t), 13)
-        r = L.hc_front_check(eng._h, 0)
-        assert r >= 0, (kind, t, -r - 1)
-        checked += r
+        checked += eng.check_fronts(0) + eng.check_fronts(1)
     assert checked > 0
+    eng.run_until_all_finished(50000.0)
+    od, _ = parity.run_pair(HostEngine, scn, max_time=50000.0)
+    assert parity.compare(od, eng) == [], kind
